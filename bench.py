@@ -1,0 +1,177 @@
+#!/usr/bin/env python
+"""Benchmark: OpenFWI 70x70 FWI gradient step on MI355X (BASELINE.json metric, configs[1]).
+
+One step = one iteration of the InversionEngine loop body for config 2 (FlatVel-A, 8 shots per
+GPU, nt = 1000, TV regulariser): HIP coefficient fields -> 1000 forward steps (store-all
+history) -> L1 misfit -> TV -> hand-written adjoint (1000 steps) -> gradient finalize ->
+[N>1: one RCCL all-reduce of the 20 KB model gradient] -> Adam -> clamp -> cosine LR.
+Inputs (velocity model, observed data) are synthetic and resident in HBM before timing.
+
+value = shot-timesteps/s over the whole job = N * ns_per_gpu * nt * B / (step time, max over
+ranks).  Weak scaling: every rank owns 8 shots of an 8N-shot survey.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--ns 8] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "shot-timesteps/sec (fwd+adj) + per-iter FWI wallclock, OpenFWI 70×70"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--ns", type=int, default=8, help="shots per GPU")
+    p.add_argument("--nt", type=int, default=1000)
+    p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-shots", type=int, default=4)
+    return p.parse_args()
+
+
+def cpu_baseline(ctx, vtrue, nshots):
+    """Oracle (CPU restatement, OpenMP) forward+adjoint on a bounded sample of the workload."""
+    from oracle import oracle as O
+    c = dict(ctx, ns=nshots)
+    f = O.OracleFWI(c, 1)
+    vn = ((vtrue - 1500) / 3000 * 2 - 1).astype(np.float32)
+    y, _ = f.forward(vn)
+    v0 = (vn * 0.9).astype(np.float32)
+    t0 = time.perf_counter()
+    seis, cf = f.forward(v0, keep_history=True)
+    _, ds = O.l1_loss(seis, y)
+    f.finalize(cf, *f.adjoint(cf, ds))
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": round(nshots * c["nt"] / dt, 1), "unit": "shot-timesteps/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/fwi_oracle.c fwd+adj+finalize, {nshots} shots x {c['nt']} steps, 70x70 "
+                      f"(310x310 padded), {dt:.2f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from red_diffeq.core.inversion import grad_all_reduce
+    from red_diffeq.core.losses import l1_misfit
+    from red_diffeq.regularization.benchmark import total_variation_loss
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import prepare_initial_model, s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.synthetic import make_model
+
+    B, nsl, nt = a.batch, a.ns, a.nt
+    ns_tot = nsl * world
+    ctx = dict(n_grid=70, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns_tot)
+    fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none,
+                     shots=(rank * nsl, (rank + 1) * nsl))
+    vtrue = make_model("flatvel", 70, 70, seed=8888, batch=B)
+    vt = torch.from_numpy(vtrue)
+    with torch.no_grad():
+        y = fwi(v_normalize(vt).to(dev))                         # observed data, local shots
+    mu0 = torch.cat([prepare_initial_model(vt[i:i + 1], "smoothed", sigma=10.0) for i in range(B)])
+    mu = torch.nn.functional.pad(mu0, (1, 1, 1, 1)).to(dev).requires_grad_(True)
+    opt = torch.optim.Adam([mu], lr=0.03)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=300, eta_min=0.0)
+    nobs = torch.full((B,), float(ns_tot * nt * 70), device=dev) if world > 1 else None
+    lam = 0.01
+
+    def step():
+        v_in = mu[:, :, 1:-1, 1:-1]
+        if world > 1:
+            v_in = grad_all_reduce(v_in)
+        loss = l1_misfit(fwi(v_in), y, None, nobs) + lam * total_variation_loss(mu)
+        opt.zero_grad(set_to_none=True)
+        loss.sum().backward()
+        opt.step()
+        with torch.no_grad():
+            mu.data.clamp_(-1, 1)
+        sched.step()
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    t_step = el.item() / a.steps
+
+    # ---- phase timing with HIP events on the stream the graphs/kernels are launched on ----
+    plan = fwi._plan(70, 70, dev)
+    sz = plan.sizes(B)
+    npad = sz.Hp * sz.Wp
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    fw_ms, adj_ms = [], []
+    v_in = mu.detach()[:, :, 1:-1, 1:-1]
+    dseis = torch.randn(B, nsl, sz.nrec, plan.ng, device=dev)
+    for _ in range(max(3, a.steps // 2)):
+        ev[0].record()
+        coeffs, vstat = plan.coeffs(v_in, 0)
+        seis, hist = plan.forward(coeffs, B, keep_history=True)
+        ev[1].record()
+        ev[2].record()
+        gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+        ev[3].record()
+        torch.cuda.synchronize()
+        fw_ms.append(ev[0].elapsed_time(ev[1]))
+        adj_ms.append(ev[2].elapsed_time(ev[3]))
+        del hist
+    fw_ms, adj_ms = float(np.median(fw_ms)), float(np.median(adj_ms))
+    adj_launch_us = adj_ms * 1e3 / nt
+    adj_bytes = 16.0 * npad * nsl * B            # adjoint 16*Npad B per shot-step
+    fwd_bytes = 12.0 * npad * nsl * B
+    achieved = adj_bytes / (adj_launch_us * 1e-6) / 1e9
+
+    units = world * nsl * nt * B
+    out = {
+        "metric": METRIC, "value": round(units / t_step, 1), "unit": "shot-timesteps/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "configs[1]: OpenFWI FlatVel-A 70x70 (310x310 padded), 8 shots/GPU, nt=1000, "
+                               "fwd+adj gradient + TV + Adam step",
+                   "global_batch": B, "shots_per_gpu": nsl, "shots_total": ns_tot, "nt": nt,
+                   "parallelism": f"shot-parallel x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_adj_step", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": adj_bytes, "avg_launch_us": round(adj_launch_us, 3)},
+        "phases_ms": {"coeffs+forward": round(fw_ms, 3), "adjoint": round(adj_ms, 3),
+                      "fwd_GBps_alg": round(fwd_bytes * nt / (fw_ms * 1e-3) / 1e9, 1)},
+        "fwd_adj_only_shot_ts_per_s": round(nsl * nt * B / ((fw_ms + adj_ms) * 1e-3), 1),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ctx, vtrue[:1], a.cpu_sample_shots)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+/*
+ * red_diffeq_fwi.h — C ABI of the MI355X-native FWI hot path (libred_diffeq_hip.so).
+ *
+ * Replaces, as a drop-in boundary, the compute behind the reference's Python plugin
+ * ``FWIForward`` (SimingShan/red-diffeq red_diffeq/solvers/pde.py:6-93) and the autograd
+ * adjoint PyTorch derives from it (triggered at red_diffeq/core/inversion.py:86).  The Python
+ * mirror of the reference interface (red-diffeq_amd/red_diffeq/solvers/pde.py) binds these
+ * symbols with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain pointers and sizes; device pointers unless stated "host".  No torch types.
+ *   - Every call is stream-ordered on the given hipStream_t (NULL = legacy default stream) and
+ *     returns 0 or a negative error code (-hipError_t, or RDQ_E_* below).
+ *   - The caller owns every buffer; sizes come from rdq_fwi_sizes().  The plan owns only the
+ *     uploaded geometry (a few KB) and its cached hipGraphs.
+ *   - Results are deterministic: no float atomics; every reduction has a fixed order.
+ *   - Layout: padded grid Hp = nz + 2*nbc rows, Wp = nx + 2*nbc columns, row pitch `ld`
+ *     floats (Wp rounded up to 64).  fp32 throughout, as the reference.
+ */
+#ifndef RED_DIFFEQ_FWI_H
+#define RED_DIFFEQ_FWI_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDQ_E_INVALID (-10001) /* bad argument / shape */
+#define RDQ_E_NOMEM (-10002)   /* host allocation failed */
+
+/* Acquisition geometry, host memory.  Mirrors FWIForward's ctx after __init__ and adj_sr
+ * (pde.py:16-23, 54-59): all indices already on the padded grid. */
+typedef struct rdq_fwi_geom {
+    int32_t nz, nx;            /* model size (rows = depth, cols = width) */
+    int32_t nbc;               /* sponge width, pde.py ctx['nbc'] */
+    int32_t nt;                /* time steps */
+    int32_t ns, ng;            /* shots, receivers */
+    int32_t sample_temporal;   /* record every k-th step (pde.py:82) */
+    float dx, dt;
+    int32_t isz, igz;          /* source / receiver row on the padded grid */
+    const int32_t *isx;        /* host [ns] source columns (padded grid) */
+    const int32_t *igx;        /* host [ng] receiver columns (padded grid) */
+    const double *wavelet;     /* host [nt] Ricker wavelet (pde.py:26-36), fp64 */
+} rdq_fwi_geom;
+
+typedef struct rdq_fwi_plan rdq_fwi_plan;
+
+/* Byte sizes of the caller-owned buffers for batch B (number of velocity models). */
+typedef struct rdq_fwi_sizes_t {
+    int32_t Hp, Wp, ld, nrec;  /* padded grid, row pitch (floats), recorded steps */
+    size_t coeffs;             /* float [5][B][Hp][ld]: alpha, temp1, temp2, kappa, beta */
+    size_t vstat;              /* float vmin[B] then int64 argmin[B] (row-major index into nz*nx) */
+    size_t seis;               /* float [B][ns][nrec][ng] */
+    size_t history;            /* float [nt+2][B][ns][Hp][ld]; slot j = P_{j-1} */
+    size_t ring;               /* float [3][B][ns][Hp][ld]: forward w/o history, or adjoint lambdas */
+    size_t gA;                 /* float [B][Hp][ld]  adjoint accumulator d(loss)/d(alpha) */
+    size_t gk_part;            /* double [B][n_adj_blocks] sponge-coefficient partial sums */
+    size_t gbeta;              /* float [B][ns] source-amplitude gradient */
+    size_t colsum;             /* double [B][Hp][nx] replicate-fold workspace */
+} rdq_fwi_sizes_t;
+
+/* Create / destroy a plan (uploads geometry; replaces FWIForward.__init__, pde.py:8-24). */
+int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **plan);
+int rdq_fwi_plan_destroy(rdq_fwi_plan *plan);
+int rdq_fwi_sizes(const rdq_fwi_plan *plan, int32_t B, rdq_fwi_sizes_t *out);
+/* 1 = capture each time loop into a cached hipGraph (default), 0 = direct launches. */
+int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
+
+/* Velocity input convention of rdq_fwi_coeffs / rdq_fwi_grad_finalize. */
+#define RDQ_VEL_NORMALIZED 0  /* v_norm in [-1,1], denormalised in-kernel: (v+1)/2*3000+1500 */
+#define RDQ_VEL_PHYSICAL 1    /* velocity in m/s (FWIForward(normalize=False) or a custom denorm) */
+
+/* K3: coefficient fields from a velocity v[b][0][iz][ix] given by element strides (any view,
+ * e.g. mu[:, :, 1:-1, 1:-1]).  Replaces v_denormalize + F.pad(replicate) + get_Abc + the
+ * alpha/temp1/temp2/beta lines (data_trans.py:13-15, pde.py:91, 38-52, 63-71). */
+int rdq_fwi_coeffs(const rdq_fwi_plan *plan, int32_t B, const float *v, const int64_t strides[4],
+                   int32_t vel_mode, float *coeffs, void *vstat, hipStream_t stream);
+
+/* K1: forward time loop (pde.py:74-86).  history == NULL: no-grad forward through the 3-slice
+ * `ring`; otherwise every P_j is kept in `history` for the adjoint (ring unused). */
+int rdq_fwi_forward(const rdq_fwi_plan *plan, int32_t B, const float *coeffs, float *seis,
+                    float *history, float *ring, hipStream_t stream);
+
+/* K2: discrete adjoint of the forward (the autograd backward of pde.py:74-86), given
+ * dseis = d(loss)/d(seis).  Writes the accumulators gA, gk_part, gbeta (overwritten). */
+int rdq_fwi_adjoint(const rdq_fwi_plan *plan, int32_t B, const float *coeffs,
+                    const float *history, const float *dseis, float *ring, float *gA,
+                    double *gk_part, float *gbeta, hipStream_t stream);
+
+/* K4: d(loss)/d(v) [B][nz][nx] (contiguous) from the accumulators: chain through
+ * alpha/beta/sponge(vmin), replicate-pad fold, and (RDQ_VEL_NORMALIZED) the x1500 of the
+ * denormalisation. */
+int rdq_fwi_grad_finalize(const rdq_fwi_plan *plan, int32_t B, const float *coeffs,
+                          const void *vstat, const float *gA, const double *gk_part,
+                          const float *gbeta, int32_t vel_mode, double *colsum, float *g_v,
+                          hipStream_t stream);
+
+/* K5: L1 observation loss (red_diffeq/core/losses.py:14-41), contiguous [B][n] operands.
+ * forward:  loss[b] = sum(|y - pred| * mask) / nobs[b],  nobs[b] = max(sum(mask), 1)
+ * backward: dpred = sign(pred - y) * mask * (gout[b] / nobs[b])       (mask NULL = all ones)
+ * `partial` is a workspace of rdq_l1_partial_bytes(B, n) bytes. */
+size_t rdq_l1_partial_bytes(int32_t B, int64_t n);
+int rdq_l1_forward(int32_t B, int64_t n, const float *pred, const float *y, const float *mask,
+                   float *loss, float *nobs, void *partial, hipStream_t stream);
+int rdq_l1_backward(int32_t B, int64_t n, const float *pred, const float *y, const float *mask,
+                    const float *nobs, const float *gout, float *dpred, hipStream_t stream);
+
+/* K6: TV / Tikhonov regulariser (red_diffeq/regularization/benchmark.py:4-37) on a contiguous
+ * mu[B][1][H][W].  kind: 0 = TV (mean|dx| + mean|dy|), 1 = Tikhonov (mean dx^2 + mean dy^2).
+ * backward writes grad = d(sum_b gout[b] * loss[b]) / d(mu) (overwritten). */
+int rdq_smooth_reg_forward(int32_t kind, int32_t B, int32_t H, int32_t W, const float *mu,
+                           float *loss, hipStream_t stream);
+int rdq_smooth_reg_backward(int32_t kind, int32_t B, int32_t H, int32_t W, const float *mu,
+                            const float *gout, float *grad, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RED_DIFFEQ_FWI_H */

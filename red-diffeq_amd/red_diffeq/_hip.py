@@ -1,0 +1,100 @@
+"""ctypes binding of the in-tree HIP library (C ABI: include/red_diffeq_fwi.h).
+
+The product path has exactly one implementation: the HIP kernels in
+red-diffeq_amd/lib/libred_diffeq_hip.so running on an MI355X.  There is no CPU fallback: if the
+library is missing, or a tensor is not on a ROCm device, calls raise ``RuntimeError``.
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libred_diffeq_hip.so")
+
+c_int32, c_int64, c_float, c_double, c_size_t, c_void_p = (
+    ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
+
+
+class FwiGeom(ctypes.Structure):
+    """struct rdq_fwi_geom."""
+    _fields_ = [("nz", c_int32), ("nx", c_int32), ("nbc", c_int32), ("nt", c_int32),
+                ("ns", c_int32), ("ng", c_int32), ("sample_temporal", c_int32),
+                ("dx", c_float), ("dt", c_float), ("isz", c_int32), ("igz", c_int32),
+                ("isx", ctypes.POINTER(c_int32)), ("igx", ctypes.POINTER(c_int32)),
+                ("wavelet", ctypes.POINTER(c_double))]
+
+
+class FwiSizes(ctypes.Structure):
+    """struct rdq_fwi_sizes_t."""
+    _fields_ = [("Hp", c_int32), ("Wp", c_int32), ("ld", c_int32), ("nrec", c_int32),
+                ("coeffs", c_size_t), ("vstat", c_size_t), ("seis", c_size_t), ("history", c_size_t),
+                ("ring", c_size_t), ("gA", c_size_t), ("gk_part", c_size_t), ("gbeta", c_size_t),
+                ("colsum", c_size_t)]
+
+
+# name -> (restype, argtypes); must match include/red_diffeq_fwi.h (tests check every symbol)
+SIGNATURES = {
+    "rdq_fwi_plan_create": (c_int32, [ctypes.POINTER(FwiGeom), ctypes.POINTER(c_void_p)]),
+    "rdq_fwi_plan_destroy": (c_int32, [c_void_p]),
+    "rdq_fwi_sizes": (c_int32, [c_void_p, c_int32, ctypes.POINTER(FwiSizes)]),
+    "rdq_fwi_set_graphs": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_coeffs": (c_int32, [c_void_p, c_int32, c_void_p, ctypes.POINTER(c_int64), c_int32,
+                                 c_void_p, c_void_p, c_void_p]),
+    "rdq_fwi_forward": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rdq_fwi_adjoint": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+    "rdq_fwi_grad_finalize": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rdq_l1_partial_bytes": (c_size_t, [c_int32, c_int64]),
+    "rdq_l1_forward": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
+    "rdq_l1_backward": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
+    "rdq_smooth_reg_forward": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rdq_smooth_reg_backward": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                          c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def load_library():
+    """Load the HIP library and declare every exported signature (raises if absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"red-diffeq_amd HIP library not built: {LIB_PATH} is missing "
+                "(run `make -C red-diffeq_amd` or __graft_entry__.build()).")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = lib
+    return _lib
+
+
+def lib():
+    return load_library()
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def require_device(*tensors):
+    """The product path runs on a ROCm device only: refuse CPU tensors loudly."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("red-diffeq_amd kernels run on the MI355X only (got a CPU tensor); "
+                               "there is deliberately no CPU fallback")
+
+
+def stream_of(t):
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)

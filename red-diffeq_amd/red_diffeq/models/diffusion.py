@@ -1,0 +1,402 @@
+"""U-Net epsilon-predictor and Gaussian diffusion schedule — inference subset of the reference
+red_diffeq/models/diffusion.py (Unet 220-301, blocks 78-218, schedules 304-326,
+GaussianDiffusion 328-437, q_sample 516-519).
+
+Module tree and parameter names are the reference's, so a reference checkpoint
+(``torch.load(path)["model"]`` = a GaussianDiffusion state_dict, 296 keys at dim=64) loads
+unchanged.  The RED regulariser only runs the forward pass (its U-Net output is detached,
+regularization/diffusion.py:74), so training/sampling loops (p_losses, Trainer, Dataset,
+ddim/p_sample loops) are out of scope.
+
+The arithmetic of every block goes through ``red_diffeq.models.unet_ops``.
+"""
+import math
+from collections import namedtuple
+from functools import partial
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..utils.diffusion_utils import extract
+from . import unet_ops as ops
+
+ModelPrediction = namedtuple("ModelPrediction", ["pred_noise", "pred_x_start"])
+
+
+def exists(x):
+    return x is not None
+
+
+def default(val, d):
+    if exists(val):
+        return val
+    return d() if callable(d) else d
+
+
+def cast_tuple(t, length=1):
+    return t if isinstance(t, tuple) else (t,) * length
+
+
+def divisible_by(numer, denom):
+    return numer % denom == 0
+
+
+def identity(t, *args, **kwargs):
+    return t
+
+
+def normalize_to_neg_one_to_one(img):
+    return img * 2 - 1
+
+
+def unnormalize_to_zero_to_one(t):
+    return (t + 1) * 0.5
+
+
+class _Rearrange(nn.Module):
+    """Parameter-free stand-in for einops' Rearrange at index 0 of Downsample (keeps keys)."""
+
+    def forward(self, x):
+        return ops.pixel_unshuffle2(x)
+
+
+def Upsample(dim, dim_out=None):
+    """nearest x2 then 3x3 conv (reference diffusion.py:78-79); keys ``.1.weight/.1.bias``."""
+    return nn.Sequential(nn.Upsample(scale_factor=2, mode="nearest"), nn.Conv2d(dim, default(dim_out, dim), 3, padding=1))
+
+
+def Downsample(dim, dim_out=None):
+    """2x2 pixel-unshuffle then 1x1 conv (reference diffusion.py:81-82)."""
+    return nn.Sequential(_Rearrange(), nn.Conv2d(dim * 4, default(dim_out, dim), 1))
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.g = nn.Parameter(torch.ones(1, dim, 1, 1))
+
+    def forward(self, x):
+        return ops.rmsnorm(x, self.g)
+
+
+class SinusoidalPosEmb(nn.Module):
+    def __init__(self, dim, theta=10000):
+        super().__init__()
+        self.dim = dim
+        self.theta = theta
+
+    def forward(self, x):
+        half = self.dim // 2
+        emb = math.log(self.theta) / (half - 1)
+        emb = torch.exp(torch.arange(half, device=x.device) * -emb)
+        emb = x[:, None] * emb[None, :]
+        return torch.cat((emb.sin(), emb.cos()), dim=-1)
+
+
+class Block(nn.Module):
+    """conv3x3 -> GroupNorm(8) -> (scale+1, shift) -> SiLU (reference diffusion.py:134-149)."""
+
+    def __init__(self, dim, dim_out, groups=8):
+        super().__init__()
+        self.proj = nn.Conv2d(dim, dim_out, 3, padding=1)
+        self.norm = nn.GroupNorm(groups, dim_out)
+        self.act = nn.SiLU()
+
+    def forward(self, x, scale_shift=None):
+        x = ops.conv2d(x, self.proj)
+        return ops.group_norm_affine_silu(x, self.norm, scale_shift)
+
+
+class ResnetBlock(nn.Module):
+    def __init__(self, dim, dim_out, *, time_emb_dim=None, groups=8):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.SiLU(), nn.Linear(time_emb_dim, dim_out * 2)) if exists(time_emb_dim) else None
+        self.block1 = Block(dim, dim_out, groups=groups)
+        self.block2 = Block(dim_out, dim_out, groups=groups)
+        self.res_conv = nn.Conv2d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
+
+    def forward(self, x, time_emb=None):
+        scale_shift = None
+        if exists(self.mlp) and exists(time_emb):
+            te = ops.linear(F.silu(time_emb), self.mlp[1])
+            scale_shift = te[:, :, None, None].chunk(2, dim=1)
+        h = self.block1(x, scale_shift=scale_shift)
+        h = self.block2(h)
+        res = ops.conv2d(x, self.res_conv) if isinstance(self.res_conv, nn.Conv2d) else x
+        return h + res
+
+
+class LinearAttention(nn.Module):
+    def __init__(self, dim, heads=4, dim_head=32, num_mem_kv=4):
+        super().__init__()
+        self.scale = dim_head ** -0.5
+        self.heads = heads
+        hidden = dim_head * heads
+        self.norm = RMSNorm(dim)
+        self.mem_kv = nn.Parameter(torch.randn(2, heads, dim_head, num_mem_kv))
+        self.to_qkv = nn.Conv2d(dim, hidden * 3, 1, bias=False)
+        self.to_out = nn.Sequential(nn.Conv2d(hidden, dim, 1), RMSNorm(dim))
+
+    def forward(self, x):
+        return ops.linear_attention(x, self)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, heads=4, dim_head=32, num_mem_kv=4, flash=False):
+        super().__init__()
+        self.heads = heads
+        hidden = dim_head * heads
+        self.norm = RMSNorm(dim)
+        self.attend = nn.Identity()   # denoising-diffusion-pytorch Attend: no parameters
+        self.mem_kv = nn.Parameter(torch.randn(2, heads, num_mem_kv, dim_head))
+        self.to_qkv = nn.Conv2d(dim, hidden * 3, 1, bias=False)
+        self.to_out = nn.Conv2d(hidden, dim, 1)
+
+    def forward(self, x):
+        return ops.full_attention(x, self)
+
+
+class Unet(nn.Module):
+    """Same constructor and module tree as the reference Unet (diffusion.py:220-271)."""
+
+    def __init__(self, dim, init_dim=None, out_dim=None, dim_mults=(1, 2, 4, 8), channels=3,
+                 self_condition=False, resnet_block_groups=8, learned_variance=False,
+                 learned_sinusoidal_cond=False, random_fourier_features=False, learned_sinusoidal_dim=16,
+                 sinusoidal_pos_emb_theta=10000, attn_dim_head=32, attn_heads=4, full_attn=None,
+                 flash_attn=False):
+        super().__init__()
+        if learned_sinusoidal_cond or random_fourier_features:
+            raise NotImplementedError("learned/random Fourier time embeddings are not used by red-diffeq")
+        self.channels = channels
+        self.self_condition = self_condition
+        input_channels = channels * (2 if self_condition else 1)
+        init_dim = default(init_dim, dim)
+        self.init_conv = nn.Conv2d(input_channels, init_dim, 7, padding=3)
+        dims = [init_dim, *map(lambda m: dim * m, dim_mults)]
+        in_out = list(zip(dims[:-1], dims[1:]))
+        block = partial(ResnetBlock, groups=resnet_block_groups)
+        time_dim = dim * 4
+        self.random_or_learned_sinusoidal_cond = False
+        self.time_mlp = nn.Sequential(SinusoidalPosEmb(dim, theta=sinusoidal_pos_emb_theta),
+                                      nn.Linear(dim, time_dim), nn.GELU(), nn.Linear(time_dim, time_dim))
+        if not full_attn:
+            full_attn = (*((False,) * (len(dim_mults) - 1)), True)
+        n = len(dim_mults)
+        full_attn = cast_tuple(full_attn, n)
+        attn_heads = cast_tuple(attn_heads, n)
+        attn_dim_head = cast_tuple(attn_dim_head, n)
+        self.downs = nn.ModuleList([])
+        self.ups = nn.ModuleList([])
+        for ind, ((di, do), fa, hh, dh) in enumerate(zip(in_out, full_attn, attn_heads, attn_dim_head)):
+            last = ind >= len(in_out) - 1
+            attn = Attention if fa else LinearAttention
+            self.downs.append(nn.ModuleList([
+                block(di, di, time_emb_dim=time_dim), block(di, di, time_emb_dim=time_dim),
+                attn(di, dim_head=dh, heads=hh),
+                Downsample(di, do) if not last else nn.Conv2d(di, do, 3, padding=1)]))
+        mid = dims[-1]
+        self.mid_block1 = block(mid, mid, time_emb_dim=time_dim)
+        self.mid_attn = Attention(mid, heads=attn_heads[-1], dim_head=attn_dim_head[-1])
+        self.mid_block2 = block(mid, mid, time_emb_dim=time_dim)
+        for ind, ((di, do), fa, hh, dh) in enumerate(zip(*map(reversed, (in_out, full_attn, attn_heads, attn_dim_head)))):
+            last = ind == len(in_out) - 1
+            attn = Attention if fa else LinearAttention
+            self.ups.append(nn.ModuleList([
+                block(do + di, do, time_emb_dim=time_dim), block(do + di, do, time_emb_dim=time_dim),
+                attn(do, dim_head=dh, heads=hh),
+                Upsample(do, di) if not last else nn.Conv2d(do, di, 3, padding=1)]))
+        self.out_dim = default(out_dim, channels * (1 if not learned_variance else 2))
+        self.final_res_block = block(dim * 2, dim, time_emb_dim=time_dim)
+        self.final_conv = nn.Conv2d(dim, self.out_dim, 1)
+
+    @property
+    def downsample_factor(self):
+        return 2 ** (len(self.downs) - 1)
+
+    def _time(self, time):
+        t = self.time_mlp[0](time)
+        t = ops.linear(t, self.time_mlp[1])
+        t = F.gelu(t)
+        return ops.linear(t, self.time_mlp[3])
+
+    def _resample(self, x, m):
+        if isinstance(m, nn.Conv2d):
+            return ops.conv2d(x, m)
+        if isinstance(m[0], nn.Upsample):
+            return ops.conv2d(ops.upsample_nearest2(x), m[1])
+        return ops.conv2d(ops.pixel_unshuffle2(x), m[1])
+
+    def forward(self, x, time, x_self_cond=None):
+        assert all(divisible_by(d, self.downsample_factor) for d in x.shape[-2:]), \
+            f"your input dimensions {x.shape[-2:]} need to be divisible by {self.downsample_factor}, given the unet"
+        if self.self_condition:
+            x_self_cond = default(x_self_cond, lambda: torch.zeros_like(x))
+            x = torch.cat((x_self_cond, x), dim=1)
+        x = ops.conv2d(x, self.init_conv)
+        r = x.clone()
+        t = self._time(time)
+        h = []
+        for b1, b2, attn, down in self.downs:
+            x = b1(x, t)
+            h.append(x)
+            x = b2(x, t)
+            x = attn(x) + x
+            h.append(x)
+            x = self._resample(x, down)
+        x = self.mid_block1(x, t)
+        x = self.mid_attn(x) + x
+        x = self.mid_block2(x, t)
+        for b1, b2, attn, up in self.ups:
+            x = torch.cat((x, h.pop()), dim=1)
+            x = b1(x, t)
+            x = torch.cat((x, h.pop()), dim=1)
+            x = b2(x, t)
+            x = attn(x) + x
+            x = self._resample(x, up)
+        x = torch.cat((x, r), dim=1)
+        x = self.final_res_block(x, t)
+        return ops.conv2d(x, self.final_conv)
+
+
+# ------------------------------------------------------------------------------ schedules
+def linear_beta_schedule(timesteps):
+    scale = 1000 / timesteps
+    return torch.linspace(scale * 0.0001, scale * 0.02, timesteps, dtype=torch.float64)
+
+
+def cosine_beta_schedule(timesteps, s=0.008):
+    steps = timesteps + 1
+    t = torch.linspace(0, timesteps, steps, dtype=torch.float64) / timesteps
+    ac = torch.cos((t + s) / (1 + s) * math.pi * 0.5) ** 2
+    ac = ac / ac[0]
+    return torch.clip(1 - ac[1:] / ac[:-1], 0, 0.999)
+
+
+def sigmoid_beta_schedule(timesteps, start=-3, end=3, tau=1, clamp_min=1e-05):
+    steps = timesteps + 1
+    t = torch.linspace(0, timesteps, steps, dtype=torch.float64) / timesteps
+    v_start = torch.tensor(start / tau).sigmoid()
+    v_end = torch.tensor(end / tau).sigmoid()
+    ac = (-((t * (end - start) + start) / tau).sigmoid() + v_end) / (v_end - v_start)
+    ac = ac / ac[0]
+    return torch.clip(1 - ac[1:] / ac[:-1], 0, 0.999)
+
+
+class GaussianDiffusion(nn.Module):
+    """Schedule buffers + the inference-side q/p math (reference diffusion.py:328-437, 516-519)."""
+
+    def __init__(self, model, *, image_size, timesteps=1000, sampling_timesteps=None, objective="pred_v",
+                 beta_schedule="sigmoid", schedule_fn_kwargs=dict(), ddim_sampling_eta=0.0,
+                 auto_normalize=True, offset_noise_strength=0.0, min_snr_loss_weight=False, min_snr_gamma=5):
+        super().__init__()
+        assert not (type(self) == GaussianDiffusion and model.channels != model.out_dim)
+        self.model = model
+        self.channels = model.channels
+        self.self_condition = model.self_condition
+        if isinstance(image_size, int):
+            image_size = (image_size, image_size)
+        assert isinstance(image_size, (tuple, list)) and len(image_size) == 2
+        self.image_size = image_size
+        assert objective in {"pred_noise", "pred_x0", "pred_v"}
+        self.objective = objective
+        fn = {"linear": linear_beta_schedule, "cosine": cosine_beta_schedule,
+              "sigmoid": sigmoid_beta_schedule}.get(beta_schedule)
+        if fn is None:
+            raise ValueError(f"unknown beta schedule {beta_schedule}")
+        betas = fn(timesteps, **schedule_fn_kwargs)
+        alphas = 1.0 - betas
+        ac = torch.cumprod(alphas, dim=0)
+        ac_prev = F.pad(ac[:-1], (1, 0), value=1.0)
+        self.num_timesteps = int(betas.shape[0])
+        self.sampling_timesteps = default(sampling_timesteps, self.num_timesteps)
+        assert self.sampling_timesteps <= self.num_timesteps
+        self.is_ddim_sampling = self.sampling_timesteps < self.num_timesteps
+        self.ddim_sampling_eta = ddim_sampling_eta
+        reg = lambda name, val: self.register_buffer(name, val.to(torch.float32))  # noqa: E731
+        reg("betas", betas)
+        reg("alphas_cumprod", ac)
+        reg("alphas_cumprod_prev", ac_prev)
+        reg("sqrt_alphas_cumprod", torch.sqrt(ac))
+        reg("sqrt_one_minus_alphas_cumprod", torch.sqrt(1.0 - ac))
+        reg("log_one_minus_alphas_cumprod", torch.log(1.0 - ac))
+        reg("sqrt_recip_alphas_cumprod", torch.sqrt(1.0 / ac))
+        reg("sqrt_recipm1_alphas_cumprod", torch.sqrt(1.0 / ac - 1))
+        pv = betas * (1.0 - ac_prev) / (1.0 - ac)
+        reg("posterior_variance", pv)
+        reg("posterior_log_variance_clipped", torch.log(pv.clamp(min=1e-20)))
+        reg("posterior_mean_coef1", betas * torch.sqrt(ac_prev) / (1.0 - ac))
+        reg("posterior_mean_coef2", (1.0 - ac_prev) * torch.sqrt(alphas) / (1.0 - ac))
+        self.offset_noise_strength = offset_noise_strength
+        snr = ac / (1 - ac)
+        clipped = snr.clone()
+        if min_snr_loss_weight:
+            clipped.clamp_(max=min_snr_gamma)
+        if objective == "pred_noise":
+            reg("loss_weight", clipped / snr)
+        elif objective == "pred_x0":
+            reg("loss_weight", clipped)
+        else:
+            reg("loss_weight", clipped / (snr + 1))
+        self.normalize = normalize_to_neg_one_to_one if auto_normalize else identity
+        self.unnormalize = unnormalize_to_zero_to_one if auto_normalize else identity
+
+    @property
+    def device(self):
+        return self.betas.device
+
+    def predict_start_from_noise(self, x_t, t, noise):
+        return extract(self.sqrt_recip_alphas_cumprod, t, x_t.shape) * x_t - \
+            extract(self.sqrt_recipm1_alphas_cumprod, t, x_t.shape) * noise
+
+    def predict_noise_from_start(self, x_t, t, x0):
+        return (extract(self.sqrt_recip_alphas_cumprod, t, x_t.shape) * x_t - x0) / \
+            extract(self.sqrt_recipm1_alphas_cumprod, t, x_t.shape)
+
+    def predict_v(self, x_start, t, noise):
+        return extract(self.sqrt_alphas_cumprod, t, x_start.shape) * noise - \
+            extract(self.sqrt_one_minus_alphas_cumprod, t, x_start.shape) * x_start
+
+    def predict_start_from_v(self, x_t, t, v):
+        return extract(self.sqrt_alphas_cumprod, t, x_t.shape) * x_t - \
+            extract(self.sqrt_one_minus_alphas_cumprod, t, x_t.shape) * v
+
+    def q_posterior(self, x_start, x_t, t):
+        mean = extract(self.posterior_mean_coef1, t, x_t.shape) * x_start + \
+            extract(self.posterior_mean_coef2, t, x_t.shape) * x_t
+        return (mean, extract(self.posterior_variance, t, x_t.shape),
+                extract(self.posterior_log_variance_clipped, t, x_t.shape))
+
+    def model_predictions(self, x, t, x_self_cond=None, clip_x_start=False, rederive_pred_noise=False):
+        out = self.model(x, t, x_self_cond)
+        clip = partial(torch.clamp, min=-1.0, max=1.0) if clip_x_start else identity
+        if self.objective == "pred_noise":
+            pred_noise = out
+            x_start = clip(self.predict_start_from_noise(x, t, pred_noise))
+            if clip_x_start and rederive_pred_noise:
+                pred_noise = self.predict_noise_from_start(x, t, x_start)
+        elif self.objective == "pred_x0":
+            x_start = clip(out)
+            pred_noise = self.predict_noise_from_start(x, t, x_start)
+        else:
+            x_start = clip(self.predict_start_from_v(x, t, out))
+            pred_noise = self.predict_noise_from_start(x, t, x_start)
+        return ModelPrediction(pred_noise, x_start)
+
+    def p_mean_variance(self, x, t, x_self_cond=None, clip_denoised=True):
+        preds = self.model_predictions(x, t, x_self_cond)
+        x_start = preds.pred_x_start
+        if clip_denoised:
+            x_start.clamp_(-1.0, 1.0)
+        mean, var, logvar = self.q_posterior(x_start=x_start, x_t=x, t=t)
+        return mean, var, logvar, x_start
+
+    def p_sample_deterministic(self, x, t: int, x_self_cond=None):
+        bt = torch.full((x.shape[0],), t, device=x.device, dtype=torch.long)
+        mean, _, _, x_start = self.p_mean_variance(x=x, t=bt, x_self_cond=x_self_cond, clip_denoised=True)
+        return mean, x_start
+
+    def q_sample(self, x_start, t, noise=None):
+        noise = default(noise, lambda: torch.randn_like(x_start))
+        return extract(self.sqrt_alphas_cumprod, t, x_start.shape) * x_start + \
+            extract(self.sqrt_one_minus_alphas_cumprod, t, x_start.shape) * noise

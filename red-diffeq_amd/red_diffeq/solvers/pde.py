@@ -1,0 +1,251 @@
+"""FWIForward — drop-in for the reference forward operator (red_diffeq/solvers/pde.py:6-93).
+
+Same constructor, same ``ctx`` handling (including the in-place ``sx``/``gx`` mutation,
+pde.py:16-24), same ``forward(v) -> seis`` contract: (B,1,H,W) fp32, possibly a non-contiguous
+view, to (B, ns, ceil(nt/sample_temporal), ng') fp32, differentiable w.r.t. ``v``.
+
+The compute is the MI355X HIP path (include/red_diffeq_fwi.h): coefficient fields (K3), one
+fused stencil/source/receiver launch per time step replayed from a cached hipGraph (K1), and a
+hand-written discrete adjoint (K2 + K4) as the autograd backward — where the reference records a
+~5 MB-per-shot-step autograd tape, this keeps one fp32 wavefield per step (store-all history).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _hip
+from ..utils.data_trans import v_denormalize
+
+
+def ricker(f, dt, nt):
+    """Ricker wavelet, pde.py:26-36 (fp64; raises ValueError when nt is shorter than it)."""
+    nw = 2.2 / f / dt
+    nw = 2 * np.floor(nw / 2) + 1
+    nc = np.floor(nw / 2)
+    k = np.arange(nw)
+    alpha = (nc - k) * f * dt * np.pi
+    beta = alpha ** 2
+    w0 = (1 - beta * 2) * np.exp(-beta)
+    w = np.zeros(nt)
+    w[:len(w0)] = w0
+    return w
+
+
+def adj_sr(sx, sz, gx, gz, dx, nbc):
+    """Physical positions -> padded-grid indices, pde.py:54-59 (np.around: half to even)."""
+    isx = np.around(sx / dx) + nbc
+    isz = np.around(sz / dx) + nbc
+    igx = np.around(gx / dx) + nbc
+    igz = np.around(gz / dx) + nbc
+    return isx.astype("int"), int(isz), igx.astype("int"), int(igz)
+
+
+class FwiPlan:
+    """Owns one C-ABI plan (uploaded geometry + cached hipGraphs) for one device."""
+
+    def __init__(self, nz, nx, ctx, sample_temporal, isx, isz, igx, igz, wavelet, device):
+        self.lib = _hip.lib()
+        self.device = device
+        self._isx = np.ascontiguousarray(isx, np.int32)
+        self._igx = np.ascontiguousarray(igx, np.int32)
+        self._wav = np.ascontiguousarray(wavelet, np.float64)
+        g = _hip.FwiGeom(nz=nz, nx=nx, nbc=int(ctx["nbc"]), nt=int(ctx["nt"]), ns=len(self._isx),
+                         ng=len(self._igx), sample_temporal=int(sample_temporal),
+                         dx=float(ctx["dx"]), dt=float(ctx["dt"]), isz=int(isz), igz=int(igz),
+                         isx=self._isx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                         igx=self._igx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                         wavelet=self._wav.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        self.ns, self.ng, self.nt, self.nz, self.nx = len(self._isx), len(self._igx), int(ctx["nt"]), nz, nx
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _hip.check(self.lib.rdq_fwi_plan_create(ctypes.byref(g), ctypes.byref(h)), "rdq_fwi_plan_create")
+        self.handle = h
+        self._sizes = {}
+
+    def sizes(self, B):
+        if B not in self._sizes:
+            s = _hip.FwiSizes()
+            _hip.check(self.lib.rdq_fwi_sizes(self.handle, B, ctypes.byref(s)), "rdq_fwi_sizes")
+            self._sizes[B] = s
+        return self._sizes[B]
+
+    def set_graphs(self, enable):
+        _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.rdq_fwi_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    # ---- thin wrappers over the C ABI (all buffers torch-allocated on the plan's device) ----
+    def _f32(self, nbytes):
+        return torch.empty(int(nbytes) // 4, dtype=torch.float32, device=self.device)
+
+    def coeffs(self, v, vel_mode):
+        B = v.shape[0]
+        sz = self.sizes(B)
+        coeffs = self._f32(sz.coeffs)
+        vstat = torch.empty(int(sz.vstat), dtype=torch.uint8, device=self.device)
+        strides = (ctypes.c_int64 * 4)(*v.stride())
+        _hip.check(self.lib.rdq_fwi_coeffs(self.handle, B, _hip.ptr(v), strides, vel_mode,
+                                           _hip.ptr(coeffs), _hip.ptr(vstat), _hip.stream_of(v)),
+                   "rdq_fwi_coeffs")
+        return coeffs, vstat
+
+    def forward(self, coeffs, B, keep_history):
+        sz = self.sizes(B)
+        seis = torch.empty(B, self.ns, sz.nrec, self.ng, dtype=torch.float32, device=self.device)
+        hist = self._f32(sz.history) if keep_history else None
+        ring = None if keep_history else self._f32(sz.ring)
+        _hip.check(self.lib.rdq_fwi_forward(self.handle, B, _hip.ptr(coeffs), _hip.ptr(seis),
+                                            _hip.ptr(hist), _hip.ptr(ring), _hip.stream_of(coeffs)),
+                   "rdq_fwi_forward")
+        return seis, hist
+
+    def adjoint(self, coeffs, hist, dseis, B):
+        sz = self.sizes(B)
+        ring = self._f32(sz.ring)
+        gA = self._f32(sz.gA)
+        gk = torch.empty(int(sz.gk_part) // 8, dtype=torch.float64, device=self.device)
+        gb = self._f32(sz.gbeta)
+        _hip.check(self.lib.rdq_fwi_adjoint(self.handle, B, _hip.ptr(coeffs), _hip.ptr(hist),
+                                            _hip.ptr(dseis), _hip.ptr(ring), _hip.ptr(gA), _hip.ptr(gk),
+                                            _hip.ptr(gb), _hip.stream_of(coeffs)), "rdq_fwi_adjoint")
+        return gA, gk, gb
+
+    def finalize(self, coeffs, vstat, gA, gk, gb, B, vel_mode):
+        sz = self.sizes(B)
+        colsum = torch.empty(int(sz.colsum) // 8, dtype=torch.float64, device=self.device)
+        out = torch.empty(B, 1, self.nz, self.nx, dtype=torch.float32, device=self.device)
+        _hip.check(self.lib.rdq_fwi_grad_finalize(self.handle, B, _hip.ptr(coeffs), _hip.ptr(vstat),
+                                                  _hip.ptr(gA), _hip.ptr(gk), _hip.ptr(gb), vel_mode,
+                                                  _hip.ptr(colsum), _hip.ptr(out), _hip.stream_of(coeffs)),
+                   "rdq_fwi_grad_finalize")
+        return out
+
+
+class _FWIFunction(torch.autograd.Function):
+    """seis = FWM(v); backward = hand-written discrete adjoint (no autograd tape)."""
+
+    @staticmethod
+    def forward(ctx, v, plan, vel_mode):
+        B = v.shape[0]
+        coeffs, vstat = plan.coeffs(v, vel_mode)
+        keep = bool(ctx.needs_input_grad[0])
+        seis, hist = plan.forward(coeffs, B, keep_history=keep)
+        if keep:
+            ctx.plan, ctx.vel_mode, ctx.B = plan, vel_mode, B
+            ctx.coeffs, ctx.vstat, ctx.hist = coeffs, vstat, hist
+        return seis
+
+    @staticmethod
+    def backward(ctx, gseis):
+        gseis = gseis.contiguous()
+        plan = ctx.plan
+        gA, gk, gb = plan.adjoint(ctx.coeffs, ctx.hist, gseis, ctx.B)
+        ctx.hist = None   # release the history (largest buffer) as early as possible
+        g = plan.finalize(ctx.coeffs, ctx.vstat, gA, gk, gb, ctx.B, ctx.vel_mode)
+        return g, None, None
+
+
+class FWIForward(nn.Module):
+    """Drop-in for red_diffeq.solvers.pde.FWIForward (pde.py:6-93)."""
+
+    def __init__(self, ctx, device, sample_temporal=1, sample_spatial=1.0, normalize=True,
+                 v_denorm_func=None, s_norm_func=None, shots=None):
+        super().__init__()
+        self.device = device
+        self.normalize = normalize
+        if normalize:
+            self.v_denorm_func = v_denorm_func
+            self.s_norm_func = s_norm_func
+        self.sample_temporal = sample_temporal
+        if "sx" not in ctx.keys():
+            ctx["sx"] = np.linspace(0, ctx["n_grid"] - 1, num=ctx["ns"]) * ctx["dx"]
+        else:
+            ctx["sx"] = np.array(ctx["sx"]) * ctx["dx"]
+        if "gx" not in ctx.keys():
+            ctx["gx"] = np.linspace(0, ctx["n_grid"] - 1, num=int(sample_spatial * ctx["ng"])) * ctx["dx"]
+        else:
+            ctx["gx"] = np.array(ctx["gx"]) * ctx["dx"]
+        self.ctx = ctx
+        # shot-parallel sharding: this operator models only shots[start:stop]
+        self.shots = (0, len(ctx["sx"])) if shots is None else (int(shots[0]), int(shots[1]))
+        self._plans = {}
+
+    # --- reference helpers kept with their signatures -------------------------------------
+    def ricker(self, f, dt, nt):
+        return ricker(f, dt, nt)
+
+    def adj_sr(self, sx, sz, gx, gz, dx, nbc):
+        return adj_sr(sx, sz, gx, gz, dx, nbc)
+
+    def get_Abc(self, vp, nbc, dx):
+        """Sponge damping field of a padded velocity (pde.py:38-52), for inspection only.
+
+        The hot path never calls this: the same profile is fused into the HIP coefficient kernel
+        (rdq_fwi_coeffs).  Columns overwrite rows, so the corners take the column profile."""
+        dimrange = 1.0 * torch.unsqueeze(torch.arange(nbc, device=vp.device), dim=-1)
+        velmin, _ = torch.min(vp.view(vp.shape[0], -1), dim=-1)
+        a = (nbc - 1) * dx
+        kappa = (3.0 * velmin * np.log(10000000.0) / (2.0 * a)).unsqueeze(0).expand(nbc, -1)
+        prof = (kappa * (dimrange * dx / a) ** 2).permute(1, 0).unsqueeze(1)   # (B,1,nbc)
+        damp = torch.zeros_like(vp)
+        H, W = vp.shape[-2:]
+        damp[:, :, :nbc, :] = torch.flip(prof, dims=[-1]).unsqueeze(-1).expand(-1, -1, -1, W)
+        damp[:, :, H - nbc:, :] = prof.unsqueeze(-1).expand(-1, -1, -1, W)
+        damp[:, :, :, :nbc] = torch.flip(prof, dims=[-1]).unsqueeze(-2).expand(-1, -1, H, -1)
+        damp[:, :, :, W - nbc:] = prof.unsqueeze(-2).expand(-1, -1, H, -1)
+        return damp
+
+    # --- HIP path --------------------------------------------------------------------------
+    def _plan(self, nz, nx, device):
+        key = (nz, nx, device.index)
+        if key not in self._plans:
+            c = self.ctx
+            isx, isz, igx, igz = adj_sr(np.asarray(c["sx"]), c["sz"], np.asarray(c["gx"]), c["gz"],
+                                        c["dx"], c["nbc"])
+            isx = isx[self.shots[0]:self.shots[1]]
+            if len(isx) == 0:
+                raise ValueError("empty shot range")
+            self._plans[key] = FwiPlan(nz, nx, c, self.sample_temporal, isx, isz, igx, igz,
+                                       ricker(c["f"], c["dt"], c["nt"]), device)
+        return self._plans[key]
+
+    def _fused_denorm(self):
+        return self.normalize and self.v_denorm_func is v_denormalize
+
+    def forward(self, v):
+        _hip.require_device(v)
+        if v.dim() != 4 or v.shape[1] != 1:
+            raise ValueError(f"expected v of shape (B,1,H,W), got {tuple(v.shape)}")
+        if v.dtype != torch.float32:
+            v = v.float()
+        if self._fused_denorm():
+            vel_mode = 0                      # denormalisation fused into K3 / K4
+        else:
+            if self.normalize:
+                v = self.v_denorm_func(v)     # arbitrary user callable: autograd through torch
+            vel_mode = 1
+        plan = self._plan(v.shape[2], v.shape[3], v.device)
+        s = _FWIFunction.apply(v, plan, vel_mode)
+        return self.s_norm_func(s) if self.normalize else s
+
+    def coefficients(self, v):
+        """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""
+        _hip.require_device(v)
+        plan = self._plan(v.shape[2], v.shape[3], v.device)
+        v = v.float()
+        if self.normalize and not self._fused_denorm():
+            v = self.v_denorm_func(v)
+        coeffs, vstat = plan.coeffs(v, 0 if self._fused_denorm() else 1)
+        sz = plan.sizes(v.shape[0])
+        f = coeffs.view(6, v.shape[0], sz.Hp, sz.ld)[..., :sz.Wp]
+        return dict(zip(("alpha", "temp1", "temp2", "kappa", "beta", "v"), f.unbind(0)))

@@ -1,0 +1,283 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures in tests/golden/*.npz by running the REFERENCE implementation
+(SimingShan/red-diffeq at /root/reference) on the CPU of this container.
+
+Run:  python tests/golden/make_golden.py [name ...]
+
+This script is the only code in the repository that executes the reference.  It never runs on the
+GPU box (the reference does not exist there); the tests only read the .npz files it writes.
+Every fixture stores its inputs next to the reference outputs, so a test needs nothing else.
+"""
+import copy
+import importlib.util
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from _refimport import load_reference  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location(
+    "_synthetic", os.path.join(HERE, "..", "..", "red-diffeq_amd", "red_diffeq", "utils", "synthetic.py"))
+synthetic = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(synthetic)
+
+ref = load_reference()
+torch.set_num_threads(8)
+
+OPENFWI = dict(n_grid=70, nt=1000, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=5)
+SMALL = dict(n_grid=16, nt=160, dx=10.0, dt=0.001, nbc=8, f=15.0, sz=10, gz=10, ng=16, ns=3)
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+def vnorm(v):
+    return ref.data_trans.v_normalize(v)
+
+
+def make_fwi(ctx, **kw):
+    return ref.pde.FWIForward(copy.deepcopy(ctx), "cpu", normalize=True,
+                              v_denorm_func=ref.data_trans.v_denormalize,
+                              s_norm_func=ref.data_trans.s_normalize_none, **kw)
+
+
+def ctx_arrays(ctx):
+    return {"ctx_" + k: np.asarray(v) for k, v in ctx.items()}
+
+
+# ----------------------------------------------------------------------------------------------
+def gen_geometry():
+    """ricker (pde.py:26-36) and adj_sr (pde.py:54-59) known-answer vectors."""
+    out = {}
+    f = make_fwi(OPENFWI)
+    for i, (fq, dt, nt) in enumerate([(15.0, 1e-3, 1000), (10.0, 2e-3, 600), (25.0, 1e-3, 200)]):
+        out[f"ricker{i}_args"] = np.array([fq, dt, nt])
+        out[f"ricker{i}"] = f.ricker(fq, dt, nt)
+    cases = [(70, 1, 70, 1.0), (70, 5, 70, 1.0), (70, 8, 70, 1.0), (70, 32, 70, 1.0),
+             (70, 256, 70, 1.0), (190, 5, 190, 1.0), (70, 5, 70, 0.5), (16, 3, 16, 1.0)]
+    for i, (n_grid, ns, ng, ss) in enumerate(cases):
+        ctx = dict(OPENFWI, n_grid=n_grid, ns=ns, ng=ng)
+        fw = make_fwi(ctx, sample_spatial=ss)
+        c = fw.ctx
+        isx, isz, igx, igz = fw.adj_sr(c["sx"], c["sz"], c["gx"], c["gz"], c["dx"], c["nbc"])
+        out[f"sr{i}_args"] = np.array([n_grid, ns, ng, ss])
+        out[f"sr{i}_isx"] = isx
+        out[f"sr{i}_igx"] = igx
+        out[f"sr{i}_isz_igz"] = np.array([isz, igz])
+    # explicit sx/gx in ctx (grid units, pde.py:18-23)
+    ctx = dict(SMALL, sx=[0, 7.5, 15], gx=list(range(0, 16, 3)))
+    fw = make_fwi(ctx)
+    c = fw.ctx
+    isx, isz, igx, igz = fw.adj_sr(c["sx"], c["sz"], c["gx"], c["gz"], c["dx"], c["nbc"])
+    out["srx_isx"], out["srx_igx"], out["srx_isz_igz"] = isx, igx, np.array([isz, igz])
+    save("geometry", **out)
+
+
+def gen_damp():
+    """get_Abc sponge field (pde.py:38-52) for a small and an OpenFWI padded model."""
+    out = {}
+    for tag, ctx, nz, nx in [("small", SMALL, 16, 16), ("openfwi", OPENFWI, 70, 70),
+                             ("rect", dict(SMALL, n_grid=24), 16, 24)]:
+        v = synthetic.make_model("curvefault", nz, nx, seed=11, batch=2)
+        fw = make_fwi(ctx)
+        vpad = torch.nn.functional.pad(torch.from_numpy(v), (ctx["nbc"],) * 4, mode="replicate")
+        damp = fw.get_Abc(vpad, ctx["nbc"], ctx["dx"])
+        out[tag + "_v"] = v
+        out[tag + "_damp"] = damp.numpy()
+        out[tag + "_nbc_dx"] = np.array([ctx["nbc"], ctx["dx"]])
+    save("damp", **out)
+
+
+def run_forward(ctx, v, **kw):
+    fw = make_fwi(ctx, **kw)
+    with torch.no_grad():
+        return fw(torch.from_numpy(vnorm(v))).numpy()
+
+
+def gen_forward():
+    """Forward seismograms, FWIForward.forward (pde.py:88-93)."""
+    v = synthetic.make_model("curvefault", 16, 16, seed=3, batch=2)
+    save("fwd_small", v=v, seis=run_forward(SMALL, v), **ctx_arrays(SMALL))
+    save("fwd_small_st3", v=v, seis=run_forward(SMALL, v, sample_temporal=3, sample_spatial=0.5),
+         st=np.array(3), ss=np.array(0.5), **ctx_arrays(SMALL))
+    ctx = dict(SMALL, n_grid=24, nbc=4, nt=200, ns=4, ng=24)   # small sponge: periodic wrap matters
+    v = synthetic.make_model("curvevel", 12, 24, seed=5, batch=1)
+    save("fwd_wrap", v=v, seis=run_forward(ctx, v), **ctx_arrays(ctx))
+    v = synthetic.make_model("flatvel", 70, 70, seed=8888, batch=1)
+    ctx = dict(OPENFWI, ns=1)
+    t0 = time.time()
+    save("fwd_openfwi_ns1", v=v, seis=run_forward(ctx, v), **ctx_arrays(ctx))
+    print(f"  openfwi ns1 forward {time.time() - t0:.1f}s")
+    v = synthetic.make_model("curvevel", 70, 70, seed=8889, batch=1)
+    ctx = dict(OPENFWI, ns=5, nt=400)
+    save("fwd_openfwi_ns5_nt400", v=v, seis=run_forward(ctx, v), **ctx_arrays(ctx))
+
+
+def l1_grad(ctx, v_true, v_init, mask=None):
+    """Gradient of the reference observation loss (losses.py:14-41) through the autograd adjoint."""
+    y = torch.from_numpy(run_forward(ctx, v_true))
+    fw = make_fwi(ctx)
+    vn = torch.from_numpy(vnorm(v_init)).clone().requires_grad_(True)
+    pred = fw(vn)
+    lc = ref.losses.LossCalculator(None)
+    m = None if mask is None else torch.from_numpy(mask)
+    loss = lc.observation_loss(pred, y, mask=m)
+    loss.sum().backward()
+    return y.numpy(), loss.detach().numpy(), vn.grad.numpy()
+
+
+def smooth(v, sigma):
+    from scipy.ndimage import gaussian_filter
+    vn = gaussian_filter(vnorm(v.astype(np.float64)), sigma=sigma)
+    return ref.data_trans.v_denormalize(vn).astype(np.float32)
+
+
+def gen_grad():
+    v_true = synthetic.make_model("curvefault", 16, 16, seed=21, batch=2)
+    v_init = smooth(v_true, 2.0)
+    y, loss, g = l1_grad(SMALL, v_true, v_init)
+    save("grad_small", v_true=v_true, v_init=v_init, y=y, loss=loss, grad=g, **ctx_arrays(SMALL))
+    mask = np.ones_like(y)
+    mask[0, :, :, [2, 9]] = 0
+    mask[1, :, :, [0, 5, 15]] = 0
+    y, loss, g = l1_grad(SMALL, v_true, v_init, mask=mask)
+    save("grad_small_mask", v_true=v_true, v_init=v_init, y=y, mask=mask, loss=loss, grad=g,
+         **ctx_arrays(SMALL))
+    # flat layers: many ties for vmin (torch.min first-index rule), OpenFWI geometry, ns=1
+    v_true = synthetic.make_model("flatvel", 70, 70, seed=8888, batch=1)
+    v_init = smooth(v_true, 10.0)
+    v_init[0, 0, 0:3, :] = v_init.min()   # force ties for the minimum in the top rows
+    ctx = dict(OPENFWI, ns=1)
+    t0 = time.time()
+    y, loss, g = l1_grad(ctx, v_true, v_init)
+    print(f"  openfwi ns1 fwd+adj {time.time() - t0:.1f}s")
+    save("grad_openfwi_ns1", v_true=v_true, v_init=v_init, y=y, loss=loss, grad=g, **ctx_arrays(ctx))
+
+
+class _NoDiffusion:
+    device = torch.device("cpu")
+
+
+def run_loop(ctx, family, seed, reg, ts, lr, lam, sigma, missing=0, noise_std=0.0):
+    v_true = synthetic.make_model(family, ctx["n_grid"], ctx["n_grid"], seed=seed, batch=1)
+    y = torch.from_numpy(run_forward(ctx, v_true))
+    init = ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=sigma)
+    mu0 = torch.nn.functional.pad(init, (1, 1, 1, 1), "constant", 0)
+    eng = ref.inversion.InversionEngine(_NoDiffusion(), ref.ssim.SSIM(window_size=11), reg)
+    torch.manual_seed(1234)
+    mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), y, make_fwi(ctx), ts=ts, lr=lr,
+                            reg_lambda=lam, missing_number=missing, noise_std=noise_std,
+                            regularization=reg)
+    h = hist[0]
+    return dict(v_true=v_true, y=y.numpy(), mu0=mu0.numpy(), mu=mu.detach().numpy(),
+                total_losses=np.array(h["total_losses"]), obs_losses=np.array(h["obs_losses"]),
+                reg_losses=np.array(h["reg_losses"]), ssim=np.array(h["ssim"]),
+                mae=np.array(h["mae"]), rmse=np.array(h["rmse"]),
+                params=np.array([ts, lr, lam, sigma, missing, noise_std]), **ctx_arrays(ctx))
+
+
+def gen_loop():
+    """InversionEngine.optimize trajectories (inversion.py:26-129), TV and Tikhonov."""
+    t0 = time.time()
+    ctx = dict(OPENFWI, ns=2)
+    save("loop_tv_openfwi", reg=np.array("tv"),
+         **run_loop(ctx, "flatvel", 8888, "tv", ts=5, lr=0.03, lam=0.01, sigma=10.0))
+    print(f"  tv loop {time.time() - t0:.1f}s")
+    ctx = dict(SMALL, n_grid=16)
+    save("loop_l2_small", reg=np.array("l2"),
+         **run_loop(ctx, "curvevel", 77, "l2", ts=8, lr=0.03, lam=0.1, sigma=2.0))
+    save("loop_none_small", reg=np.array("none"),
+         **run_loop(ctx, "curvevel", 78, None, ts=8, lr=0.05, lam=0.0, sigma=2.0))
+
+
+def _unet_dim8(seed=0):
+    torch.manual_seed(seed)
+    net = ref.diffusion.Unet(dim=8, dim_mults=(1, 2, 4, 8), channels=1, flash_attn=False)
+    # perturb the unit-initialised norm gains so that the fixture pins them
+    with torch.no_grad():
+        for name, p in net.named_parameters():
+            if name.endswith(".g") or (".norm." in name and name.endswith("weight")):
+                p.mul_(1.0 + 0.2 * torch.randn_like(p))
+            if ".norm." in name and name.endswith("bias"):
+                p.add_(0.1 * torch.randn_like(p))
+    return net.eval()
+
+
+def gen_unet():
+    """lucidrains U-Net forward (models/diffusion.py:220-301) at dim=8, same topology."""
+    net = _unet_dim8()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 1, 72, 72, generator=g)
+    t = torch.tensor([17, 803])
+    with torch.no_grad():
+        out = net(x, t)
+    sd = {"sd." + k: v.numpy() for k, v in net.state_dict().items()}
+    save("unet_dim8", x=x.numpy(), t=t.numpy(), out=out.numpy(), **sd)
+
+
+def gen_red():
+    """RED-DiffEq regularizer (regularization/diffusion.py:50-155) + schedule buffers."""
+    net = _unet_dim8()
+    diff = ref.diffusion.GaussianDiffusion(net, image_size=72, timesteps=1000,
+                                           sampling_timesteps=250, objective="pred_noise").eval()
+    out = {"buf." + k: v.numpy() for k, v in diff.state_dict().items() if not k.startswith("model.")}
+    for tag, H, W, tw in [("sq", 72, 72, False), ("sqw", 72, 72, True), ("patch", 72, 192, False)]:
+        red = ref.reg_diffusion.RED_DiffEq(diff, use_time_weight=tw, sigma_x0=1e-4)
+        g = torch.Generator().manual_seed(99)
+        mu = (torch.rand(2, 1, H, W, generator=g) * 2 - 1).requires_grad_(True)
+        seed = 4242
+        gen = torch.Generator().manual_seed(seed)
+        if W > 72:
+            reg, gpm, t = red.get_reg_loss_patched(mu, generator=gen)
+        else:
+            reg, gpm, t = red.get_reg_loss(mu, generator=gen)
+        reg.sum().backward()
+        # replay the generator to record the injected draws (t first, then noise)
+        gen = torch.Generator().manual_seed(seed)
+        t2 = torch.randint(0, 1000, (2,), generator=gen, dtype=torch.long)
+        shp = (2, 1, H - 2, W - 2) if W > 72 else (2, 1, H, W)
+        noise = torch.randn(shp, generator=gen)
+        assert torch.equal(t, t2)
+        out.update({tag + "_mu": mu.detach().numpy(), tag + "_t": t.numpy(),
+                    tag + "_noise": noise.numpy(), tag + "_reg": reg.detach().numpy(),
+                    tag + "_gpm": gpm.detach().numpy(), tag + "_grad": mu.grad.numpy(),
+                    tag + "_seed": np.array(seed)})
+    save("red_dim8", **out)
+
+
+def gen_small_losses():
+    """TV / Tikhonov (regularization/benchmark.py:4-37), SSIM (utils/ssim.py), metrics."""
+    g = torch.Generator().manual_seed(7)
+    a = torch.rand(3, 1, 72, 72, generator=g) * 2 - 1
+    b = torch.rand(3, 1, 70, 70, generator=g) * 2 - 1
+    c = torch.rand(3, 1, 70, 70, generator=g) * 2 - 1
+    s = ref.ssim.SSIM(window_size=11)
+    ssim = np.array([s((b[i:i + 1] + 1) / 2, (c[i:i + 1] + 1) / 2).item() for i in range(3)])
+    mc = ref.metrics.MetricsCalculator(ref.ssim.SSIM(window_size=11))
+    vtrue = ref.data_trans.v_denormalize(c)
+    mae, rmse, ss = mc.calculate(b, vtrue)
+    save("small_losses", a=a.numpy(), b=b.numpy(), c=c.numpy(),
+         tv=ref.reg_bench.total_variation_loss(a).numpy(),
+         l2=ref.reg_bench.tikhonov_loss(a).numpy(), ssim=ssim,
+         m_mae=mae.numpy(), m_rmse=rmse.numpy(), m_ssim=ss.numpy(),
+         patches_190_70=np.array(ref.reg_diffusion.calculate_patches(190, 70)[0]),
+         overlaps_190_70=np.array(ref.reg_diffusion.calculate_patches(190, 70)[1]))
+
+
+GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
+            loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses)
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(GENS)
+    for n in names:
+        t0 = time.time()
+        GENS[n]()
+        print(f"[{n}] {time.time() - t0:.1f}s")

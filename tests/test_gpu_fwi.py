@@ -1,0 +1,221 @@
+"""Parity of the HIP FWI path (libred_diffeq_hip.so through its C ABI) against the reference's
+own outputs (tests/golden, produced by the reference) and the oracle (oracle/, CPU restatement).
+
+Bars: forward seismograms BIT-EXACT vs the reference; adjoint accumulator gA bit-exact vs the
+oracle; velocity gradient within fp32 tolerance of the reference autograd (rel-L2 < 5e-5) and
+of the oracle (rel-L2 < 1e-6); TV inversion trajectory: final-model RMSE difference < 1e-4
+(north_star tolerance)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ctx_of, load_golden, vnorm
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FWD = [("fwd_small", {}), ("fwd_small_st3", dict(sample_temporal=3, sample_spatial=0.5)), ("fwd_wrap", {}),
+       ("fwd_openfwi_ns1", {}), ("fwd_openfwi_ns5_nt400", {})]
+
+
+def make_fwi(ctx, **kw):
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize
+    return FWIForward(dict(ctx), "cuda", normalize=True, v_denorm_func=v_denormalize,
+                      s_norm_func=s_normalize_none, **kw)
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.int32), b.view(np.int32))
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+@pytest.mark.parametrize("name,kw", FWD)
+def test_forward_bitexact_vs_reference(cuda, name, kw, graphs):
+    z = load_golden(name)
+    fwi = make_fwi(ctx_of(z), **kw)
+    v = torch.from_numpy(vnorm(z["v"])).to(cuda)
+    plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+    plan.set_graphs(graphs)
+    with torch.no_grad():
+        seis = fwi(v).cpu().numpy()
+    assert bits_equal(seis, z["seis"]), np.abs(seis - z["seis"]).max()
+
+
+def test_forward_noncontiguous_view_and_history_path(cuda):
+    """mu[:, :, 1:-1, 1:-1] view (how InversionEngine calls it), with and without history."""
+    z = load_golden("fwd_small")
+    fwi = make_fwi(ctx_of(z))
+    v = torch.from_numpy(vnorm(z["v"]))
+    mu = torch.nn.functional.pad(v, (1, 1, 1, 1)).to(cuda)
+    view = mu[:, :, 1:-1, 1:-1]
+    assert not view.is_contiguous()
+    with torch.no_grad():
+        s1 = fwi(view)
+    s2 = fwi(view.clone().requires_grad_(True))     # history (store-all) path
+    assert bits_equal(s1.cpu().numpy(), z["seis"]) and bits_equal(s2.detach().cpu().numpy(), z["seis"])
+
+
+@pytest.mark.parametrize("name", ["grad_small", "grad_small_mask", "grad_openfwi_ns1"])
+def test_gradient_vs_reference_autograd(cuda, name):
+    from red_diffeq.core.losses import LossCalculator
+    z = load_golden(name)
+    fwi = make_fwi(ctx_of(z))
+    vn = torch.from_numpy(vnorm(z["v_init"])).to(cuda).requires_grad_(True)
+    y = torch.from_numpy(z["y"]).to(cuda)
+    mask = torch.from_numpy(z["mask"]).to(cuda) if "mask" in z.files else None
+    loss = LossCalculator(None).observation_loss(fwi(vn), y, mask=mask)
+    loss.sum().backward()
+    np.testing.assert_allclose(loss.detach().cpu().numpy(), z["loss"], rtol=2e-6)
+    g = vn.grad.cpu().numpy()
+    ref = z["grad"]
+    assert np.linalg.norm(g - ref) / np.linalg.norm(ref) < 5e-5
+    # and against the oracle on identical inputs: tighter (only fp64 summation order differs)
+    f = O.OracleFWI(ctx_of(z), vn.shape[0])
+    seis, c = f.forward(vnorm(z["v_init"]), keep_history=True)
+    _, ds = O.l1_loss(seis, z["y"], z["mask"] if "mask" in z.files else None)
+    go = f.finalize(c, *f.adjoint(c, ds))
+    assert np.linalg.norm(g - go) / np.linalg.norm(go) < 1e-6
+
+
+@pytest.mark.parametrize("name,kw", [("fwd_small", {}), ("fwd_small_st3", dict(sample_temporal=3, sample_spatial=0.5)),
+                                     ("fwd_wrap", {})])
+def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw):
+    z = load_golden(name)
+    ctx = ctx_of(z)
+    fwi = make_fwi(ctx, **kw)
+    vn = vnorm(z["v"])
+    v = torch.from_numpy(vn).to(cuda)
+    B = v.shape[0]
+    plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(1)
+    dseis = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
+    coeffs, vstat = plan.coeffs(v, 0)
+    seis, hist = plan.forward(coeffs, B, keep_history=True)
+    gA, gk, gb = plan.adjoint(coeffs, hist, torch.from_numpy(dseis).to(cuda), B)
+    g = plan.finalize(coeffs, vstat, gA, gk, gb, B, 0).cpu().numpy()
+    torch.cuda.synchronize()
+    f = O.OracleFWI(ctx, B, **kw)
+    _, c = f.forward(vn, keep_history=True)
+    oA, oK, ob = f.adjoint(c, dseis)
+    gA = gA.view(B, sz.Hp, sz.ld)[:, :, :sz.Wp].cpu().numpy()
+    assert bits_equal(gA, oA)
+    assert bits_equal(gb.view(B, -1).cpu().numpy(), ob)
+    gks = gk.view(B, -1).sum(1).cpu().numpy()
+    np.testing.assert_allclose(gks, oK, rtol=1e-5, atol=1e-12 + 1e-6 * np.abs(oK).max())
+    go = f.finalize(c, oA, oK, ob)
+    assert np.linalg.norm(g - go) / np.linalg.norm(go) < 1e-6
+    # coefficient fields vs the oracle: bitwise
+    cf = fwi.coefficients(v)
+    for k in ("alpha", "temp1", "temp2", "kappa", "beta"):
+        assert bits_equal(cf[k].cpu().numpy(), c[k]), k
+    vm = vstat[:4 * B].view(torch.float32).cpu().numpy()
+    assert bits_equal(vm, c["vmin"])
+
+
+def test_damp_profile_vs_reference(cuda):
+    """Sponge (get_Abc, columns overwrite rows) as kappa/dt vs the reference fixture."""
+    z = load_golden("damp")
+    for tag in ("small", "openfwi", "rect"):
+        v = z[tag + "_v"]
+        nbc, dx = z[tag + "_nbc_dx"]
+        ctx = dict(n_grid=v.shape[3], nt=200, dx=float(dx), dt=0.001, nbc=int(nbc), f=15.0, sz=10, gz=10,
+                   ng=v.shape[3], ns=2)
+        fwi = make_fwi(ctx)
+        cf = fwi.coefficients(torch.from_numpy(vnorm(v)).to(cuda))
+        kappa = cf["kappa"].cpu().numpy()
+        ref = (z[tag + "_damp"][:, 0] * np.float32(0.001)).astype(np.float32)
+        assert bits_equal(kappa, ref), tag
+
+
+def test_batch_and_dot_product_openfwi_ns8(cuda):
+    """Full OpenFWI size, 8 shots, B=2: size-independent properties — adjoint dot-product test
+    <J dv, w> = <dv, J^T w>, batch independence (model b alone == model b in the batch)."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=70, nt=1000, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=8)
+    fwi = make_fwi(ctx)
+    v = torch.from_numpy(vnorm(make_model("curvevel", 70, 70, seed=5, batch=2))).to(cuda).double()
+    v = v + 0.02 * torch.rand_like(v)
+    v[:, :, 30, 40] = v.amin(dim=(1, 2, 3)) - 0.05          # unique minimum
+    v = v.float()
+    vv = v.clone().requires_grad_(True)
+    seis = fwi(vv)
+    w = torch.randn_like(seis)
+    (seis * w).sum().backward()
+    g = vv.grad.double()
+    dv = 5e-3 * torch.randn_like(v)
+    with torch.no_grad():
+        lhs = (((fwi(v + dv).double() - fwi(v - dv).double()) / 2) * w.double()).sum()
+    rhs = (g * dv.double()).sum()
+    assert abs(lhs - rhs) / abs(rhs) < 2e-2, (lhs.item(), rhs.item())
+    with torch.no_grad():
+        s1 = fwi(v[1:2].contiguous())
+    assert torch.equal(s1[0], seis.detach()[1])
+
+
+def test_l1_and_smooth_reg_kernels(cuda):
+    from red_diffeq.core.losses import l1_misfit
+    from red_diffeq.regularization.benchmark import tikhonov_loss, total_variation_loss
+    z = load_golden("small_losses")
+    a = torch.from_numpy(z["a"]).to(cuda).requires_grad_(True)
+    tv = total_variation_loss(a)
+    np.testing.assert_allclose(tv.detach().cpu().numpy(), z["tv"], rtol=1e-6)
+    tv.sum().backward()
+    a2 = a.detach().clone().requires_grad_(True)
+    ref = (a2[:, :, :, 1:] - a2[:, :, :, :-1]).abs().flatten(1).mean(1) + \
+        (a2[:, :, 1:, :] - a2[:, :, :-1, :]).abs().flatten(1).mean(1)
+    ref.sum().backward()
+    torch.testing.assert_close(a.grad, a2.grad, rtol=1e-6, atol=1e-9)
+    b = a.detach().clone().requires_grad_(True)
+    l2 = tikhonov_loss(b)
+    np.testing.assert_allclose(l2.detach().cpu().numpy(), z["l2"], rtol=1e-6)
+    (l2 * torch.tensor([1.0, 2.0, 3.0], device=cuda)).sum().backward()
+    b2 = a.detach().clone().requires_grad_(True)
+    r2 = ((b2[:, :, :, 1:] - b2[:, :, :, :-1]) ** 2).flatten(1).mean(1) + \
+        ((b2[:, :, 1:, :] - b2[:, :, :-1, :]) ** 2).flatten(1).mean(1)
+    (r2 * torch.tensor([1.0, 2.0, 3.0], device=cuda)).sum().backward()
+    torch.testing.assert_close(b.grad, b2.grad, rtol=1e-5, atol=1e-9)
+    # L1 misfit with a mask, against the reference formula in torch fp64
+    g = torch.Generator().manual_seed(3)
+    pred = torch.randn(2, 3, 50, 7, generator=g).to(cuda).requires_grad_(True)
+    y = torch.randn(2, 3, 50, 7, generator=g).to(cuda)
+    mask = (torch.rand(2, 3, 50, 7, generator=g) > 0.3).float().to(cuda)
+    loss = l1_misfit(pred, y, mask)
+    nob = mask.flatten(1).sum(1).clamp(min=1)
+    ref = ((y - pred).abs() * mask).flatten(1).double().sum(1) / nob.double()
+    torch.testing.assert_close(loss.double(), ref.detach(), rtol=1e-6, atol=0)
+    (loss * torch.tensor([0.5, 2.0], device=cuda)).sum().backward()
+    exp = torch.sign(pred.detach() - y) * mask * (torch.tensor([0.5, 2.0], device=cuda) / nob).view(2, 1, 1, 1)
+    assert torch.equal(pred.grad, exp)
+
+
+@pytest.mark.parametrize("name", ["loop_tv_openfwi", "loop_l2_small", "loop_none_small"])
+def test_inversion_loop_vs_reference(cuda, name):
+    """InversionEngine trajectory vs the reference engine (tv / l2 / none): final model RMSE
+    difference < 1e-4 and per-iteration losses/metrics within fp32 tolerance."""
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden(name)
+    ts, lr, lam, sigma, missing, noise_std = z["params"]
+    reg = str(z["reg"])
+    reg = None if reg == "none" else reg
+
+    class _NoDiffusion:
+        device = cuda
+
+    eng = InversionEngine(_NoDiffusion(), SSIM(window_size=11), reg, show_progress=False)
+    fwi = make_fwi(ctx_of(z))
+    mu, hist = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
+                            torch.from_numpy(z["y"]).to(cuda), fwi, ts=int(ts), lr=float(lr),
+                            reg_lambda=float(lam), missing_number=int(missing), noise_std=float(noise_std),
+                            regularization=reg)
+    mu = mu.detach().cpu().numpy()
+    rmse = float(np.sqrt(np.mean((mu - z["mu"]) ** 2)))
+    assert rmse < 1e-4, rmse
+    h = hist[0]
+    for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
+        np.testing.assert_allclose(np.array(h[k], np.float64), z[k].astype(np.float64), rtol=2e-4, atol=1e-6,
+                                   err_msg=k)

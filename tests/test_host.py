@@ -1,0 +1,135 @@
+"""Host-side logic on CPU: geometry, config, schedules, patching, the C-ABI library surface and
+the no-CPU-fallback rule."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+
+
+def test_ricker_and_geometry_vs_reference():
+    from red_diffeq.solvers.pde import FWIForward, adj_sr, ricker
+    z = load_golden("geometry")
+    for i in range(3):
+        f, dt, nt = z[f"ricker{i}_args"]
+        np.testing.assert_array_equal(ricker(f, dt, int(nt)), z[f"ricker{i}"])
+    base = dict(nt=1000, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10)
+    for i in range(8):
+        n_grid, ns, ng, ss = z[f"sr{i}_args"]
+        ctx = dict(base, n_grid=int(n_grid), ns=int(ns), ng=int(ng))
+        fw = FWIForward(ctx, "cpu", sample_spatial=float(ss))
+        c = fw.ctx
+        isx, isz, igx, igz = adj_sr(c["sx"], c["sz"], c["gx"], c["gz"], c["dx"], c["nbc"])
+        np.testing.assert_array_equal(isx, z[f"sr{i}_isx"])
+        np.testing.assert_array_equal(igx, z[f"sr{i}_igx"])
+        assert [isz, igz] == list(z[f"sr{i}_isz_igz"])
+    ctx = dict(base, n_grid=16, nbc=8, ng=16, ns=3, sx=[0, 7.5, 15], gx=list(range(0, 16, 3)))
+    fw = FWIForward(ctx, "cpu")
+    c = fw.ctx
+    isx, isz, igx, igz = adj_sr(c["sx"], c["sz"], c["gx"], c["gz"], c["dx"], c["nbc"])
+    np.testing.assert_array_equal(isx, z["srx_isx"])
+    np.testing.assert_array_equal(igx, z["srx_igx"])
+
+
+def test_ricker_too_short_raises_like_reference():
+    from red_diffeq.solvers.pde import ricker
+    with pytest.raises(ValueError):
+        ricker(15.0, 1e-3, 100)   # 147-sample wavelet does not fit
+
+
+def test_oracle_geometry_matches_product():
+    from oracle import oracle as O
+    from red_diffeq.solvers.pde import ricker
+    np.testing.assert_array_equal(O.ricker(15.0, 1e-3, 1000), ricker(15.0, 1e-3, 1000))
+
+
+def test_configs_load_unchanged():
+    from red_diffeq.config import get_config, load_config, save_config
+    cfg_dir = os.path.join(ROOT, "tests", "golden", "configs")
+    c = get_config()
+    assert c.pde.nbc == 120 and c.model.dim_mults == (1, 2, 4, 8)
+    assert getattr(c.optimization, "fixed_timestep", 1) is None
+    p = os.path.join(cfg_dir, "roundtrip.yaml")
+    save_config(c, p)
+    c2 = load_config(p)
+    assert c2.pde.to_dict() == c.pde.to_dict() and list(c2.model.dim_mults) == [1, 2, 4, 8]
+    os.remove(p)
+
+
+def test_schedule_buffers_vs_reference():
+    from red_diffeq.models.diffusion import GaussianDiffusion, Unet
+    z = load_golden("red_dim8")
+    net = Unet(dim=8, dim_mults=(1, 2, 4, 8), channels=1)
+    d = GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250, objective="pred_noise")
+    sd = d.state_dict()
+    for k in z.files:
+        if k.startswith("buf."):
+            assert torch.equal(sd[k[4:]], torch.from_numpy(z[k])), k
+
+
+def test_unet_state_dict_keys_match_reference():
+    from red_diffeq.models.diffusion import Unet
+    z = load_golden("unet_dim8")
+    ref = {k[3:]: z[k].shape for k in z.files if k.startswith("sd.")}
+    net = Unet(dim=8, dim_mults=(1, 2, 4, 8), channels=1)
+    mine = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    assert mine == {k: tuple(v) for k, v in ref.items()}
+
+
+def test_calculate_patches_vs_reference():
+    from red_diffeq.regularization.diffusion import calculate_patches
+    z = load_golden("small_losses")
+    pos, ov = calculate_patches(190, 70)
+    np.testing.assert_array_equal(np.array(pos), z["patches_190_70"])
+    np.testing.assert_array_equal(np.array(ov), z["overlaps_190_70"])
+    assert calculate_patches(70, 70) == ([(0, 70)], [])
+
+
+def test_c_abi_library_exports_every_header_symbol():
+    from red_diffeq import _hip
+    lib = _hip.load_library()
+    hdr = open(os.path.join(ROOT, "include", "red_diffeq_fwi.h")).read()
+    names = set(re.findall(r"^(?:int|size_t)\s+(rdq_\w+)\(", hdr, flags=re.M))
+    assert names == set(_hip.SIGNATURES), names ^ set(_hip.SIGNATURES)
+    for n in names:
+        assert isinstance(getattr(lib, n), ctypes._CFuncPtr)
+    # host-only entry points work without a GPU
+    assert lib.rdq_l1_partial_bytes(2, 100000) == 2 * 25 * 2 * 8
+    assert lib.rdq_fwi_plan_destroy(None) == 0
+
+
+def test_c_abi_rejects_bad_geometry():
+    from red_diffeq import _hip
+    lib = _hip.load_library()
+    isx = (ctypes.c_int32 * 1)(500)   # outside the padded grid
+    igx = (ctypes.c_int32 * 1)(3)
+    wav = (ctypes.c_double * 10)()
+    g = _hip.FwiGeom(nz=4, nx=4, nbc=2, nt=10, ns=1, ng=1, sample_temporal=1, dx=10.0, dt=1e-3, isz=2, igz=2,
+                     isx=isx, igx=igx, wavelet=wav)
+    h = ctypes.c_void_p()
+    assert lib.rdq_fwi_plan_create(ctypes.byref(g), ctypes.byref(h)) == -10001
+
+
+def test_no_cpu_fallback():
+    from red_diffeq.core.losses import l1_misfit
+    from red_diffeq.regularization.benchmark import total_variation_loss
+    from red_diffeq.solvers.pde import FWIForward
+    ctx = dict(n_grid=8, nt=200, dx=10.0, dt=0.001, nbc=4, f=15.0, sz=10, gz=10, ng=8, ns=1)
+    fwi = FWIForward(ctx, "cpu", normalize=False)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        fwi(torch.zeros(1, 1, 8, 8))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        total_variation_loss(torch.zeros(1, 1, 8, 8))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        l1_misfit(torch.zeros(1, 4), torch.zeros(1, 4))
+
+
+def test_synthetic_models_in_range():
+    from red_diffeq.utils.synthetic import make_model
+    for fam in ("flatvel", "curvevel", "curvefault"):
+        v = make_model(fam, 70, 70, seed=8888, batch=2)
+        assert v.shape == (2, 1, 70, 70) and v.min() >= 1500 and v.max() <= 4500
