@@ -51,13 +51,15 @@ typedef struct rdq_fwi_plan rdq_fwi_plan;
 /* Byte sizes of the caller-owned buffers for batch B (number of velocity models). */
 typedef struct rdq_fwi_sizes_t {
     int32_t Hp, Wp, ld, nrec;  /* padded grid, row pitch (floats), recorded steps */
-    size_t coeffs;             /* float [5][B][Hp][ld]: alpha, temp1, temp2, kappa, beta */
+    size_t coeffs;             /* float [6][B][Hp][ld] alpha, temp1, temp2, kappa, beta, v; then
+                                  v_model [B][nz][nx] and the sponge amplitude ks [B] */
     size_t vstat;              /* float vmin[B] then int64 argmin[B] (row-major index into nz*nx) */
     size_t seis;               /* float [B][ns][nrec][ng] */
     size_t history;            /* float [nt+2][B][ns][Hp][ld]; slot j = P_{j-1} */
-    size_t ring;               /* float [3][B][ns][Hp][ld]: forward w/o history, or adjoint lambdas */
-    size_t gA;                 /* float [B][Hp][ld]  adjoint accumulator d(loss)/d(alpha) */
-    size_t gk_part;            /* double [B][n_adj_blocks] sponge-coefficient partial sums */
+    size_t ring;               /* float [4][B][ns][Hp][ld]: two in/out level pairs (no-grad forward,
+                                  adjoint lambdas) */
+    size_t gA;                 /* float [B][ns][Hp][ld] per-shot accumulator d(loss)/d(alpha) */
+    size_t gk_part;            /* double [B][ns][n_adj_blocks] sponge-coefficient partial sums */
     size_t gbeta;              /* float [B][ns] source-amplitude gradient */
     size_t colsum;             /* double [B][Hp][nx] replicate-fold workspace */
 } rdq_fwi_sizes_t;
@@ -68,6 +70,10 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *plan);
 int rdq_fwi_sizes(const rdq_fwi_plan *plan, int32_t B, rdq_fwi_sizes_t *out);
 /* 1 = capture each time loop into a cached hipGraph (default), 0 = direct launches. */
 int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
+/* Time steps advanced per launch by the forward / adjoint kernels (temporal blocking depth,
+ * 1..4) and the number of concurrent shot-group launch chains (1..16).  Results are identical
+ * for every setting; only speed changes. */
+int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
 
 /* Velocity input convention of rdq_fwi_coeffs / rdq_fwi_grad_finalize. */
 #define RDQ_VEL_NORMALIZED 0  /* v_norm in [-1,1], denormalised in-kernel: (v+1)/2*3000+1500 */

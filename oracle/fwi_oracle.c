@@ -157,11 +157,11 @@ void oracle_forward(const oracle_geom *g, const float *alpha, const float *temp1
 /*
  * Discrete adjoint.  Walks k = nt..1:
  *   L_k = T1*L_{k+1} - T2*L_{k+2} + (c2*N1(A*L_{k+1}) + c3*N2(A*L_{k+1})) + R^T dseis[k-1]
- *   gA(x)   += L_k(x) * (2c1*P_{k-1}(x) + c2*N1(P_{k-1}) + c3*N2(P_{k-1}))      [sum over s]
- *   gKs     += sum_x K(x) * P_{k-1}(x) * (L_{k+1}(x) - L_k(x))                  [double]
+ *   gA_s(x) += L_k(x) * (2c1*P_{k-1}(x) + c2*N1(P_{k-1}) + c3*N2(P_{k-1}))     [per shot s]
+ *   gKs     += sum_x (K(x) * P_{k-1}(x)) * (L_{k+1}(x) - L_k(x))   [fp32 terms, fp64 sum]
  *   gbeta[s]+= L_k(src_s) * w[k-1]
- * The shot loop is innermost per point so the gA order is (k descending, s ascending); the HIP
- * kernel uses the same order and agrees bit-for-bit on gA.
+ * then gA = sum_s gA_s (s ascending, fp32).  Order: k descending per shot, then shots; the HIP
+ * kernels use the same order and agree bit-for-bit on gA and gbeta.
  */
 void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1,
                     const float *temp2, const float *kappa, const float *hist, const float *dseis,
@@ -171,7 +171,7 @@ void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1
     const size_t N = (size_t)Hp * Wp, S = (size_t)g->B * ns * N;
     float *lam = (float *)calloc(3 * S, sizeof(float));
     float *q = (float *)malloc(S * sizeof(float));
-    memset(gA, 0, (size_t)g->B * N * sizeof(float));
+    float *gAs = (float *)calloc(S, sizeof(float));
     for (int b = 0; b < g->B; ++b) gKs[b] = 0.0;
     memset(gbeta, 0, (size_t)g->B * ns * sizeof(float));
     for (int k = g->nt; k >= 1; --k) {
@@ -194,7 +194,6 @@ void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1
                 for (int x = 0; x < Wp; ++x) {
                     const size_t i = (size_t)z * Wp + x, ci = b * N + i;
                     const int xm1 = wrap(x - 1, Wp), xp1 = wrap(x + 1, Wp), xm2 = wrap(x - 2, Wp), xp2 = wrap(x + 2, Wp);
-                    float ga = 0.0f;
                     for (int s = 0; s < ns; ++s) {
                         const size_t off = ((size_t)b * ns + s) * N;
                         const float *qq = q + off, *pp = P + off;
@@ -215,10 +214,10 @@ void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1
                         float lap = C2 * s1; const float lp2 = C3 * s2; lap = lap + lp2;
                         float d = C1X2 * pp[i]; d = d + lap;
                         const float c = l * d;
-                        ga = ga + c;
-                        ksum += (double)kappa[ci] * (double)pp[i] * ((double)L1[off + i] - (double)l);
+                        gAs[off + i] = gAs[off + i] + c;
+                        float kk = kappa[ci] * pp[i]; const float dl = L1[off + i] - l; kk = kk * dl;
+                        ksum += (double)kk;   /* fp32 product (as autograd), fp64 sum */
                     }
-                    gA[ci] = gA[ci] + ga;
                 }
             }
             gKs[b] += ksum;
@@ -230,7 +229,13 @@ void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1
                 gbeta[b * ns + s] = gbeta[b * ns + s] + L0[off + si] * w;
             }
     }
-    free(lam); free(q);
+    for (int b = 0; b < g->B; ++b)
+        for (size_t i = 0; i < N; ++i) {
+            float a = 0.0f;
+            for (int s = 0; s < ns; ++s) a = a + gAs[((size_t)b * ns + s) * N + i];
+            gA[b * N + i] = a;
+        }
+    free(lam); free(q); free(gAs);
 }
 
 /*

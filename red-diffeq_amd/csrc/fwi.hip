@@ -35,25 +35,25 @@ namespace {
 constexpr float C1X2 = -5.0f;                      // 2*c1, pde.py:66,69
 constexpr float C2 = (float)(4.0 / 3.0);           // pde.py:67
 constexpr float C3 = (float)(-1.0 / 12.0);         // pde.py:68
-constexpr int TX = 64;                             // tile width = one wave
-constexpr int TY = 4;                              // waves per workgroup
-constexpr int ZT = 4;                              // rows marched per thread (register queue)
-constexpr int ROWS_PER_BLOCK = TY * ZT;
 
 #define RDQ_CHECK(x)                                   \
     do {                                               \
         hipError_t e_ = (x);                           \
         if (e_ != hipSuccess) return -(int)e_;         \
     } while (0)
+#define RDQ_TRY(x)                                     \
+    do {                                               \
+        const int rc_ = (x);                           \
+        if (rc_ != 0) return rc_;                      \
+    } while (0)
 
-__device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
 // --------------------------------------------------------------------------------------- K3
 // vmin / first row-major argmin over the (unpadded) model; the padded field's first minimum
 // folds back to this cell (pde.py:41, torch.min tie rule = first index).
 __global__ __launch_bounds__(256) void k_vstat(const float *__restrict__ vn, int64_t s0, int64_t s2,
-                                               int64_t s3, int nz, int nx, int vel_mode, float *vmin,
-                                               int64_t *amin)
+                                               int64_t s3, int nz, int nx, int vel_mode, float lnk,
+                                               float two_a, float *vmin, int64_t *amin, float *ks)
 {
     const int b = blockIdx.x;
     float best = INFINITY;
@@ -81,15 +81,58 @@ __global__ __launch_bounds__(256) void k_vstat(const float *__restrict__ vn, int
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { vmin[b] = sv[0]; amin[b] = si[0]; }
+    if (threadIdx.x == 0) {
+        vmin[b] = sv[0];
+        amin[b] = si[0];
+        float k = 3.0f * sv[0]; k = k * lnk; k = k / two_a;   // kappa = 3*vmin*ln(1e7)/(2a), pde.py:43
+        ks[b] = k;
+    }
 }
+
+// Coefficient fields at one padded-grid point (pde.py:38-52, 63-71), from the model velocity
+// and the per-model sponge amplitude ks = 3*vmin*ln(1e7)/(2a).  K3 stores them for inspection and
+// for K4; the time-loop kernels regenerate them in registers (bit-identical: same function), so a
+// launch reads a 20 KB model instead of three 400 KB padded fields per shot.
+struct CoefGen {
+    const float *vmod;   // [B][nz][nx] velocity (m/s)
+    const float *ks;     // [B]
+    int nz, nx, nbc, Hp, Wp;
+    float dt, dx, a;
+};
+
+struct Coef { float v, al, t1, t2, kp; };
+
+__device__ __forceinline__ Coef gen_coef(const CoefGen &c, int b, int z, int x)
+{
+    const int iz = min(max(z - c.nbc, 0), c.nz - 1);
+    const int ix = min(max(x - c.nbc, 0), c.nx - 1);
+    Coef o;
+    o.v = c.vmod[((size_t)b * c.nz + iz) * c.nx + ix];
+    const int nbc = c.nbc;
+    int pi = -1;                                   // rows first, then columns overwrite (corners)
+    if (z < nbc) pi = nbc - 1 - z;
+    if (z >= c.Hp - nbc) pi = z - (c.Hp - nbc);
+    if (x < nbc) pi = nbc - 1 - x;
+    if (x >= c.Wp - nbc) pi = x - (c.Wp - nbc);
+    float dmp = 0.0f;
+    if (pi >= 0) { float d = (float)pi * c.dx; d = d / c.a; d = d * d; dmp = c.ks[b] * d; }
+    float al = o.v * c.dt; al = al / c.dx; al = al * al;                   // pde.py:63
+    o.al = al;
+    o.kp = dmp * c.dt;                                                      // pde.py:65
+    float t1 = C1X2 * al; t1 = t1 + 2.0f; t1 = t1 - o.kp;                   // pde.py:69
+    o.t1 = t1;
+    o.t2 = 1.0f - o.kp;                                                     // pde.py:70
+    return o;
+}
+
+__device__ __forceinline__ float beta_of(float v, float dt) { float bt = v * dt; return bt * bt; }  // pde.py:71
 
 struct CoefArgs {
     const float *vn;
     int64_t s0, s2, s3;
-    int nz, nx, nbc, Hp, Wp, ld, vel_mode;
-    float dt, dx, a, lnk, two_a;
-    const float *vmin;
+    int vel_mode, ld;
+    CoefGen cg;
+    float *vmod_out;
     float *coeffs;
     size_t cstride;  // B*Hp*ld
 };
@@ -99,212 +142,359 @@ __global__ __launch_bounds__(256) void k_coeffs(CoefArgs p)
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int z = blockIdx.y;
     const int b = blockIdx.z;
+    const CoefGen &c = p.cg;
     if (x >= p.ld) return;
-    const size_t i = ((size_t)b * p.Hp + z) * p.ld + x;
-    if (x >= p.Wp) {
+    const size_t i = ((size_t)b * c.Hp + z) * p.ld + x;
+    if (x >= c.Wp) {
         for (int f = 0; f < 6; ++f) p.coeffs[f * p.cstride + i] = 0.0f;
         return;
     }
-    const int iz = min(max(z - p.nbc, 0), p.nz - 1);
-    const int ix = min(max(x - p.nbc, 0), p.nx - 1);
-    float v = p.vn[b * p.s0 + iz * p.s2 + ix * p.s3];
-    if (p.vel_mode == 0) { v = v + 1.0f; v = v / 2.0f; v = v * 3000.0f; v = v + 1500.0f; }  // data_trans.py:15
-    // get_Abc: kappa = 3*vmin*ln(1e7)/(2a); damp1d[i] = kappa*(i*dx/a)^2; rows, then columns
-    float ks = 3.0f * p.vmin[b]; ks = ks * p.lnk; ks = ks / p.two_a;
-    const int nbc = p.nbc;
-    int pi = -1;
-    if (z < nbc) pi = nbc - 1 - z;
-    if (z >= p.Hp - nbc) pi = z - (p.Hp - nbc);
-    if (x < nbc) pi = nbc - 1 - x;
-    if (x >= p.Wp - nbc) pi = x - (p.Wp - nbc);
-    float dmp = 0.0f;
-    if (pi >= 0) { float d = (float)pi * p.dx; d = d / p.a; d = d * d; dmp = ks * d; }
-    float al = v * p.dt; al = al / p.dx; al = al * al;                      // pde.py:63
-    const float kp = dmp * p.dt;                                             // pde.py:65
-    float t1 = C1X2 * al; t1 = t1 + 2.0f; t1 = t1 - kp;                      // pde.py:69
-    float bt = v * p.dt; bt = bt * bt;                                       // pde.py:71
-    p.coeffs[i] = al;
-    p.coeffs[p.cstride + i] = t1;
-    p.coeffs[2 * p.cstride + i] = 1.0f - kp;                                 // pde.py:70
-    p.coeffs[3 * p.cstride + i] = kp;
-    p.coeffs[4 * p.cstride + i] = bt;
-    p.coeffs[5 * p.cstride + i] = v;
+    const int iz = z - c.nbc, ix = x - c.nbc;
+    if (iz >= 0 && iz < c.nz && ix >= 0 && ix < c.nx) {   // the model itself (unpadded)
+        float v = p.vn[b * p.s0 + iz * p.s2 + ix * p.s3];
+        if (p.vel_mode == 0) { v = v + 1.0f; v = v / 2.0f; v = v * 3000.0f; v = v + 1500.0f; }  // data_trans.py:15
+        p.vmod_out[((size_t)b * c.nz + iz) * c.nx + ix] = v;
+    }
 }
 
-// --------------------------------------------------------------------------------------- K1
-struct StepGeo {
-    int B, ns, Hp, Wp, ld;
-    size_t cstride;          // B*Hp*ld (coefficient field stride)
-    size_t slice;            // Hp*ld
-    int isz, igz, ng, nrec;
-    const int *isx;          // [ns]
-    const int *rcv_start;    // [Wp+1]
-    const int *rcv_list;     // receivers sorted by column
+__global__ __launch_bounds__(256) void k_coeff_fields(CoefArgs p)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int z = blockIdx.y;
+    const int b = blockIdx.z;
+    const CoefGen &c = p.cg;
+    if (x >= c.Wp) return;
+    const size_t i = ((size_t)b * c.Hp + z) * p.ld + x;
+    const Coef o = gen_coef(c, b, z, x);
+    p.coeffs[i] = o.al;
+    p.coeffs[p.cstride + i] = o.t1;
+    p.coeffs[2 * p.cstride + i] = o.t2;
+    p.coeffs[3 * p.cstride + i] = o.kp;
+    p.coeffs[4 * p.cstride + i] = beta_of(o.v, c.dt);
+    p.coeffs[5 * p.cstride + i] = o.v;
+}
+
+// --------------------------------------------------------------------------------------- K1/K2
+// Temporal blocking on a register-resident region (the MI355X design of the time loop).
+//
+// A workgroup of NW waves owns a region of 64 columns (one per lane) x NW*R rows (R consecutive
+// rows per wave, held in VGPRs) of one (model, shot) slice, and advances it T time steps per
+// launch.  Halo H = 2T on every side: after t steps the outermost 2t rows/columns are stale, the
+// interior (64-2H) x (NW*R-2H) stays exact and is the only part that is stored.  Per step:
+//   - vertical taps: the wave's own registers; the two rows above/below its slab come from the
+//     neighbouring waves through a 2 KB LDS exchange (double-buffered: one barrier per step);
+//   - horizontal taps: DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1) — no LDS traffic;
+//   - periodic wrap (torch.roll, pde.py:79) is in the region->grid map (global index mod Hp/Wp),
+//     so a tile at the domain edge simply loads wrapped rows/columns.
+// T steps per launch divide the launch count (the latency floor of the per-step design) by T and
+// cut the wavefield re-reads to two levels per launch; the extra arithmetic is the halo.
+constexpr int TB_NW = 8;                 // waves per workgroup
+constexpr int TB_R = 8;                  // rows per wave
+constexpr int TB_RH = TB_NW * TB_R;      // region rows
+constexpr int TB_MAXT = 4;
+
+__device__ __forceinline__ float dpp_shr1(float v)   // lane i <- lane i-1 (x-1); lane 0 keeps v
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                 __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_shl1(float v)   // lane i <- lane i+1 (x+1); lane 63 keeps v
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                                 __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+struct TBGeo {
+    int B, ns, Hp, Wp, ld, isz, igz, ng, nrec, st;
+    int s_off, ns_grp;                   // this launch covers shots [s_off, s_off + ns_grp)
+    size_t cstride, slice, level;        // level = B*ns*slice (one time level of all slices)
+    const int *isx, *rcv_start, *rcv_list;
 };
 
-// One forward time step for every (model, shot): P_{i+1} = T1 P_i - T2 P_{i-1} + A (c2 S1 + c3 S2)
-// (+ source, pde.py:80-81), recorded at the receivers (pde.py:82-83).  Each thread marches ZT
-// rows of one column keeping the 5 vertical taps in registers; horizontal taps are L1/L2 hits
-// of the row the wave has just loaded.
-__global__ __launch_bounds__(256) void k_fwd_step(StepGeo g, const float *__restrict__ coeffs,
-                                                  const float *__restrict__ p0,
-                                                  const float *__restrict__ p1,
-                                                  float *__restrict__ pn, float w, int rec,
-                                                  float *__restrict__ seis_k)
+struct FwdTBArgs {
+    TBGeo g;
+    const float *coeffs;                 // K3 fields: alpha, temp1, temp2 at 0, 1, 2 x cstride
+    const float *in_prev, *in_cur;       // P_{n-1}, P_n   (each [B][ns][Hp][ld])
+    float *hist;                         // history base (slot j = P_{j-1}) or nullptr
+    float *out_prev, *out_cur;           // ring path: P_{n+T-1}, P_{n+T}
+    float *seis;
+    int n0, nsteps;
+    float w[TB_MAXT];                    // wavelet samples w[n0 .. n0+nsteps-1]
+};
+
+// exchange two boundary rows each way between the NW waves of the workgroup
+struct Halo4 { float u2, u1, d1, d2; };
+
+__device__ __forceinline__ Halo4 exchange(float (*xch)[TB_NW][4][64], int buf, int w, int lane,
+                                          float top0, float top1, float bot1, float bot0)
 {
-    const int x = blockIdx.x * TX + threadIdx.x;
-    const int zb = (blockIdx.y * TY + threadIdx.y) * ZT;
-    const int bs = blockIdx.z;
-    const int b = bs / g.ns, s = bs - b * g.ns;
-    if (x >= g.Wp || zb >= g.Hp) return;
-    const int Hp = g.Hp, Wp = g.Wp, ld = g.ld;
+    xch[buf][w][0][lane] = top0;      // row 0
+    xch[buf][w][1][lane] = top1;      // row 1
+    xch[buf][w][2][lane] = bot1;      // row R-2
+    xch[buf][w][3][lane] = bot0;      // row R-1
+    __syncthreads();
+    Halo4 h;
+    const int wu = w > 0 ? w - 1 : 0, wd = w < TB_NW - 1 ? w + 1 : TB_NW - 1;
+    h.u2 = xch[buf][wu][2][lane];     // row -2 (garbage for w == 0: outside the region)
+    h.u1 = xch[buf][wu][3][lane];     // row -1
+    h.d1 = xch[buf][wd][0][lane];     // row R
+    h.d2 = xch[buf][wd][1][lane];     // row R+1
+    return h;
+}
+
+// vertical neighbour rows of row r from the slab + halo rows
+#define TB_VERT(ARR, r, H4, m2, m1, p1, p2)                                   \
+    const float m2 = (r) >= 2 ? ARR[(r) - 2] : ((r) == 1 ? H4.u1 : H4.u2);    \
+    const float m1 = (r) >= 1 ? ARR[(r) - 1] : H4.u1;                        \
+    const float p1 = (r) + 1 < TB_R ? ARR[(r) + 1] : H4.d1;                  \
+    const float p2 = (r) + 2 < TB_R ? ARR[(r) + 2] : ((r) + 2 == TB_R ? H4.d1 : H4.d2);
+
+// cheap wrap for |v| < a few n (general v handled by the loops)
+__device__ __forceinline__ int wrapn(int v, int n)
+{
+    while (v < 0) v += n;
+    while (v >= n) v -= n;
+    return v;
+}
+
+template <int T>
+__global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
+{
+    constexpr int H = 2 * T, IW = 64 - 2 * H, IH = TB_RH - 2 * H;
+    __shared__ float xch[2][TB_NW][4][64];
+    const TBGeo &g = a.g;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    const int b = blockIdx.z / g.ns_grp, s = g.s_off + (blockIdx.z - b * g.ns_grp), bs = b * g.ns + s;
+    const int ux = (int)blockIdx.x * IW - H + lane;                   // unwrapped column
+    const int gx = wrapn(ux, g.Wp);
+    const bool xin = lane >= H && lane < 64 - H && ux < g.Wp;
+    const int uz0 = (int)blockIdx.y * IH - H + w * TB_R;              // unwrapped row of r = 0
     const size_t so = (size_t)bs * g.slice;
-    const float *P1 = p1 + so;
-    const float *P0 = p0 + so;
-    float *PN = pn + so;
-    const float *AL = coeffs + (size_t)b * g.slice;
-    const float *T1 = AL + g.cstride;
-    const float *T2 = AL + 2 * g.cstride;
-    const float *BE = AL + 4 * g.cstride;
-    const int xm1 = wrapm(x - 1, Wp), xp1 = wrapm(x + 1, Wp);
-    const int xm2 = wrapm(x - 2, Wp), xp2 = wrapm(x + 2, Wp);
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    const float *T1p = AL + g.cstride, *T2p = AL + 2 * g.cstride;
     const int isx = g.isx[s];
-    float qm2 = P1[(size_t)wrapm(zb - 2, Hp) * ld + x];
-    float qm1 = P1[(size_t)wrapm(zb - 1, Hp) * ld + x];
-    float qc = P1[(size_t)zb * ld + x];
-    float qp1 = P1[(size_t)wrapm(zb + 1, Hp) * ld + x];
-    float qp2 = P1[(size_t)wrapm(zb + 2, Hp) * ld + x];
+    float A[TB_R], C1[TB_R], C2v[TB_R], P0[TB_R], P1[TB_R];
+    int rofs[TB_R];                 // wave-uniform row offsets gz*ld
+    unsigned rin = 0;               // wave-uniform: row is interior and inside the domain
+    int srow = -1, rrow = -1;       // wave-uniform: row holding the source / the receivers
 #pragma unroll
-    for (int r = 0; r < ZT; ++r) {
-        const int z = zb + r;
-        if (z >= Hp) break;
-        const float *row = P1 + (size_t)z * ld;
-        const size_t i = (size_t)z * ld + x;
-        float s1 = qm1 + qp1; s1 = s1 + row[xm1]; s1 = s1 + row[xp1];
-        float s2 = qm2 + qp2; s2 = s2 + row[xm2]; s2 = s2 + row[xp2];
-        float lap = C2 * s1; const float l2 = C3 * s2; lap = lap + l2;
-        float a1 = T1[i] * qc; const float a2 = T2[i] * P0[i]; a1 = a1 - a2;
-        const float a3 = AL[i] * lap;
-        float out = a1 + a3;
-        if (z == g.isz && x == isx) { const float add = BE[i] * w; out = out + add; }
-        PN[i] = out;
-        if (rec && z == g.igz) {
-            for (int j = g.rcv_start[x]; j < g.rcv_start[x + 1]; ++j)
-                seis_k[(size_t)bs * g.nrec * g.ng + g.rcv_list[j]] = out;
+    for (int r = 0; r < TB_R; ++r) {
+        const int uz = uz0 + r, gz = wrapn(uz, g.Hp);
+        rofs[r] = gz * g.ld;
+        const int o = rofs[r] + gx;
+        A[r] = AL[o]; C1[r] = T1p[o]; C2v[r] = T2p[o];
+        P0[r] = a.in_prev[so + o];
+        P1[r] = a.in_cur[so + o];
+        const int rr = w * TB_R + r;
+        if (rr >= H && rr < TB_RH - H && uz < g.Hp) rin |= 1u << r;
+        if (gz == g.isz) srow = r;          // (a region row maps to one grid row: one hit per wave
+        if (gz == g.igz) rrow = r;          //  unless the region wraps a tiny domain -> see below)
+    }
+    // tiny domains (region taller than Hp) can hold the source row twice: keep every hit
+    unsigned smask = 0;
+#pragma unroll
+    for (int r = 0; r < TB_R; ++r) if (wrapn(uz0 + r, g.Hp) == g.isz) smask |= 1u << r;
+    const bool scol = gx == isx;
+    const float bsrc = (smask != 0) ? a.coeffs[4 * g.cstride + (size_t)b * g.slice + (size_t)g.isz * g.ld + isx] : 0.0f;
+    const int rs = (rrow >= 0) ? g.rcv_start[gx] : 0, re = (rrow >= 0) ? g.rcv_start[gx + 1] : 0;
+    (void)srow;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        if (t >= a.nsteps) break;
+        float *cur = (t & 1) ? P0 : P1;     // P_{n+t}
+        float *prv = (t & 1) ? P1 : P0;     // P_{n+t-1}  -> overwritten with P_{n+t+1}
+        const Halo4 h4 = exchange(xch, t & 1, w, lane, cur[0], cur[1], cur[TB_R - 2], cur[TB_R - 1]);
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) {
+            TB_VERT(cur, r, h4, zm2, zm1, zp1, zp2)
+            const float c = cur[r];
+            const float xl1 = dpp_shr1(c), xr1 = dpp_shl1(c);
+            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);
+            // pde.py:79, reference evaluation order
+            float s1 = zm1 + zp1; s1 = s1 + xl1; s1 = s1 + xr1;
+            float s2 = zm2 + zp2; s2 = s2 + xl2; s2 = s2 + xr2;
+            float lap = C2 * s1; const float l2 = C3 * s2; lap = lap + l2;
+            float a1 = C1[r] * c; const float a2 = C2v[r] * prv[r]; a1 = a1 - a2;
+            const float a3 = A[r] * lap;
+            prv[r] = a1 + a3;
         }
-        if (r + 1 < ZT) {
-            qm2 = qm1; qm1 = qc; qc = qp1; qp1 = qp2;
-            qp2 = P1[(size_t)wrapm(z + 3, Hp) * ld + x];
+        if (smask) {                                                   // pde.py:80-81
+#pragma unroll
+            for (int r = 0; r < TB_R; ++r)
+                if ((smask & (1u << r)) && scol) { const float add = bsrc * a.w[t]; prv[r] = prv[r] + add; }
         }
+        const int n = a.n0 + t;
+        if (a.hist && xin) {
+            float *HS = a.hist + (size_t)(n + 2) * g.level + so + gx;
+#pragma unroll
+            for (int r = 0; r < TB_R; ++r)
+                if (rin & (1u << r)) HS[rofs[r]] = prv[r];
+        }
+        if (rrow >= 0 && (rin & (1u << rrow)) && xin && (n % g.st) == 0) {   // pde.py:82-83
+            float val = 0.0f;
+#pragma unroll
+            for (int r = 0; r < TB_R; ++r) if (r == rrow) val = prv[r];
+            float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;
+            for (int j = rs; j < re; ++j) SK[g.rcv_list[j]] = val;
+        }
+    }
+    if (a.out_cur && xin) {   // ring path: keep the last two levels
+        const bool odd = (a.nsteps & 1) != 0;   // after nsteps steps the newest level is in P0 if odd
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r)
+            if (rin & (1u << r)) {
+                const size_t o = so + rofs[r] + gx;
+                a.out_cur[o] = odd ? P0[r] : P1[r];
+                a.out_prev[o] = odd ? P1[r] : P0[r];
+            }
     }
 }
 
-// --------------------------------------------------------------------------------------- K2
-// One adjoint step for every model (shots looped inside so gA needs no atomics):
-//   L_k = T1 L_{k+1} - T2 L_{k+2} + c2 N1(A L_{k+1}) + c3 N2(A L_{k+1}) + R^T dseis[k-1]
-//   gA  += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1}))        (sum over shots, then rows)
-//   gk  += sum K P_{k-1} (L_{k+1} - L_k)       (per-workgroup partial, fixed order, fp64)
-//   gbeta[s] += L_k(src_s) w[k-1]
-__global__ __launch_bounds__(256) void k_adj_step(StepGeo g, const float *__restrict__ coeffs,
-                                                  const float *__restrict__ L1,
-                                                  const float *__restrict__ L2,
-                                                  float *__restrict__ L0,
-                                                  const float *__restrict__ P, float *__restrict__ gA,
-                                                  double *__restrict__ gk_part,
-                                                  float *__restrict__ gbeta, float w, int rec,
-                                                  const float *__restrict__ dseis_k, int nblk)
+struct AdjTBArgs {
+    TBGeo g;
+    const float *coeffs;                 // K3 fields: alpha, temp1, temp2, kappa at 0..3 x cstride
+    const float *in_l1, *in_l2;          // L_{k0+1}, L_{k0+2}
+    float *out_l1, *out_l2;              // L_{k0-nsteps+1}, L_{k0-nsteps+2}
+    const float *hist;                   // slot k = P_{k-1}
+    const float *dseis;
+    float *gA;                           // [B][ns][Hp][ld]
+    double *gk_part;                     // [B*ns][nblk]
+    float *gbeta;                        // [B*ns]
+    int k0, nsteps, nblk;
+    float w[TB_MAXT];                    // w[k0-1-t]
+};
+
+// Adjoint with the same register-region blocking, walking k = k0, k0-1, ...:
+//   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
+// and, on the interior only, the per-shot accumulators (loaded once, stored once per launch):
+//   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k),
+//   gbeta[s] += L_k(src) w[k-1].
+template <int T>
+__global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 {
-    const int x = blockIdx.x * TX + threadIdx.x;
-    const int zb = (blockIdx.y * TY + threadIdx.y) * ZT;
-    const int b = blockIdx.z;
-    const int Hp = g.Hp, Wp = g.Wp, ld = g.ld, ns = g.ns;
-    const bool act = x < Wp && zb < Hp;
-    float ksum = 0.0f;
-    if (act) {
-        const float *AL = coeffs + (size_t)b * g.slice;
-        const float *T1 = AL + g.cstride;
-        const float *T2 = AL + 2 * g.cstride;
-        const float *KA = AL + 3 * g.cstride;
-        const int xm1 = wrapm(x - 1, Wp), xp1 = wrapm(x + 1, Wp);
-        const int xm2 = wrapm(x - 2, Wp), xp2 = wrapm(x + 2, Wp);
-        float ga[ZT];
-        float t1r[ZT], t2r[ZT], kr[ZT];
+    constexpr int H = 2 * T, IW = 64 - 2 * H, IH = TB_RH - 2 * H;
+    __shared__ float xch[2][TB_NW][4][64];
+    __shared__ float pxc[2][TB_NW][4][64];
+    __shared__ double red[64 * TB_NW];
+    __shared__ float gal[TB_RH][64];   // gA_s accumulators of the region (interior used)
+    __shared__ float kal[TB_RH][64];   // sponge coefficient K of the region
+    const TBGeo &g = a.g;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.z / g.ns_grp, s = g.s_off + (blockIdx.z - b * g.ns_grp), bs = b * g.ns + s;
+    const int ux = (int)blockIdx.x * IW - H + lane;
+    const int gx = wrapn(ux, g.Wp);
+    const bool xin = lane >= H && lane < 64 - H && ux < g.Wp;
+    const int uz0 = (int)blockIdx.y * IH - H + w * TB_R;
+    const size_t so = (size_t)bs * g.slice;
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    const float *KAp = AL + 3 * g.cstride;
+    const int isx = g.isx[s];
+    float A[TB_R], L0[TB_R], L1[TB_R];   // temp1/temp2 are re-derived from A and K (bit-identical)
+    int rofs[TB_R];
+    unsigned rin = 0, pmask = 0, smask = 0, rmask = 0;   // wave-uniform row masks
 #pragma unroll
-        for (int r = 0; r < ZT; ++r) {
-            ga[r] = 0.0f;
-            const int z = min(zb + r, Hp - 1);
-            const size_t i = (size_t)z * ld + x;
-            t1r[r] = T1[i]; t2r[r] = T2[i]; kr[r] = KA[i];
+    for (int r = 0; r < TB_R; ++r) {
+        const int uz = uz0 + r, gz = wrapn(uz, g.Hp);
+        rofs[r] = gz * g.ld;
+        const int o = rofs[r] + gx;
+        A[r] = AL[o];
+        kal[w * TB_R + r][lane] = KAp[o];
+        L1[r] = a.in_l1[so + o];     // L_{k+1}
+        L0[r] = a.in_l2[so + o];     // L_{k+2}
+        const int rr = w * TB_R + r;
+        if (rr >= H && rr < TB_RH - H && uz < g.Hp) rin |= 1u << r;
+        if (rr >= H - 2 && rr < TB_RH - H + 2) pmask |= 1u << r;
+        if (gz == g.isz) smask |= 1u << r;
+        if (gz == g.igz) rmask |= 1u << r;
+        gal[rr][lane] = ((rin & (1u << r)) && xin) ? a.gA[so + o] : 0.0f;
+    }
+    const bool scol = gx == isx;
+    const int rs = rmask ? g.rcv_start[gx] : 0, re = rmask ? g.rcv_start[gx + 1] : 0;
+    double ksum = 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        if (t >= a.nsteps) break;
+        const int k = a.k0 - t;
+        float *cur = (t & 1) ? L0 : L1;     // L_{k+1}
+        float *prv = (t & 1) ? L1 : L0;     // L_{k+2} -> overwritten with L_k
+        // history P_{k-1} on the rows whose stencil the interior needs (HBM stream, issued first)
+        const float *PS = a.hist + (size_t)k * g.level + so + gx;
+        float P[TB_R];
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) P[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+        float q[TB_R];
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) q[r] = A[r] * cur[r];
+        const Halo4 h4 = exchange(xch, t & 1, w, lane, q[0], q[1], q[TB_R - 2], q[TB_R - 1]);
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) {
+            TB_VERT(q, r, h4, qm2, qm1, qp1, qp2)
+            const float qc = q[r];
+            const float xl1 = dpp_shr1(qc), xr1 = dpp_shl1(qc);
+            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);
+            float n1 = qm1 + qp1; n1 = n1 + xl1; n1 = n1 + xr1;
+            float n2 = qm2 + qp2; n2 = n2 + xl2; n2 = n2 + xr2;
+            float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;
+            const float kp = kal[w * TB_R + r][lane];
+            float t1 = C1X2 * A[r]; t1 = t1 + 2.0f; t1 = t1 - kp;     // pde.py:69
+            const float t2 = 1.0f - kp;                               // pde.py:70
+            float l = t1 * cur[r]; const float l2 = t2 * prv[r]; l = l - l2; l = l + nb;
+            prv[r] = l;
         }
-        const int zr[5] = {wrapm(zb - 2, Hp), wrapm(zb - 1, Hp), zb, wrapm(zb + 1, Hp), wrapm(zb + 2, Hp)};
-        for (int s = 0; s < ns; ++s) {
-            const size_t so = ((size_t)b * ns + s) * g.slice;
-            const float *LA = L1 + so, *LB = L2 + so, *PP = P + so;
-            float *LO = L0 + so;
-            const int isx = g.isx[s];
-            float am2 = AL[(size_t)zr[0] * ld + x], am1 = AL[(size_t)zr[1] * ld + x], ac = AL[(size_t)zr[2] * ld + x];
-            float ap1 = AL[(size_t)zr[3] * ld + x], ap2 = AL[(size_t)zr[4] * ld + x];
-            float lm2 = LA[(size_t)zr[0] * ld + x], lm1 = LA[(size_t)zr[1] * ld + x], lc = LA[(size_t)zr[2] * ld + x];
-            float lp1 = LA[(size_t)zr[3] * ld + x], lp2 = LA[(size_t)zr[4] * ld + x];
-            float pm2 = PP[(size_t)zr[0] * ld + x], pm1 = PP[(size_t)zr[1] * ld + x], pc = PP[(size_t)zr[2] * ld + x];
-            float pp1 = PP[(size_t)zr[3] * ld + x], pp2 = PP[(size_t)zr[4] * ld + x];
+        if (rmask && ((k - 1) % g.st) == 0) {   // adjoint of the receiver sampling
+            const float *DS = a.dseis + ((size_t)bs * g.nrec + (k - 1) / g.st) * g.ng;
 #pragma unroll
-            for (int r = 0; r < ZT; ++r) {
-                const int z = zb + r;
-                if (z >= Hp) break;
-                const size_t rowo = (size_t)z * ld;
-                const size_t i = rowo + x;
-                const float *ar = AL + rowo, *lr = LA + rowo, *pr = PP + rowo;
-                float n1 = am1 * lm1; n1 = n1 + ap1 * lp1; n1 = n1 + ar[xm1] * lr[xm1]; n1 = n1 + ar[xp1] * lr[xp1];
-                float n2 = am2 * lm2; n2 = n2 + ap2 * lp2; n2 = n2 + ar[xm2] * lr[xm2]; n2 = n2 + ar[xp2] * lr[xp2];
-                float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;
-                float l = t1r[r] * lc; const float l2 = t2r[r] * LB[i]; l = l - l2; l = l + nb;
-                if (rec && z == g.igz) {
-                    for (int j = g.rcv_start[x]; j < g.rcv_start[x + 1]; ++j)
-                        l = l + dseis_k[((size_t)b * ns + s) * g.nrec * g.ng + g.rcv_list[j]];
-                }
-                LO[i] = l;
-                float s1 = pm1 + pp1; s1 = s1 + pr[xm1]; s1 = s1 + pr[xp1];
-                float s2 = pm2 + pp2; s2 = s2 + pr[xm2]; s2 = s2 + pr[xp2];
+            for (int r = 0; r < TB_R; ++r)
+                if (rmask & (1u << r))
+                    for (int j = rs; j < re; ++j) prv[r] = prv[r] + DS[g.rcv_list[j]];
+        }
+        // gradient accumulators on the interior: needs the P stencil (second exchange)
+        const Halo4 hp = exchange(pxc, t & 1, w, lane, P[0], P[1], P[TB_R - 2], P[TB_R - 1]);
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) {
+            TB_VERT(P, r, hp, pm2, pm1, pp1, pp2)
+            const float pc = P[r];
+            const float xl1 = dpp_shr1(pc), xr1 = dpp_shl1(pc);
+            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);
+            if ((rin & (1u << r)) && xin) {
+                float s1 = pm1 + pp1; s1 = s1 + xl1; s1 = s1 + xr1;
+                float s2 = pm2 + pp2; s2 = s2 + xl2; s2 = s2 + xr2;
                 float lap = C2 * s1; const float lq = C3 * s2; lap = lap + lq;
                 float d = C1X2 * pc; d = d + lap;
+                const float l = prv[r];
                 const float c = l * d;
-                ga[r] = ga[r] + c;
-                const float dl = lc - l;
-                float kk = kr[r] * pc; kk = kk * dl; ksum = ksum + kk;
-                if (z == g.isz && x == isx) {
-                    const float gb = l * w;
-                    gbeta[b * ns + s] = gbeta[b * ns + s] + gb;
-                }
-                if (r + 1 < ZT) {
-                    const size_t nz3 = (size_t)wrapm(z + 3, Hp) * ld + x;
-                    am2 = am1; am1 = ac; ac = ap1; ap1 = ap2; ap2 = AL[nz3];
-                    lm2 = lm1; lm1 = lc; lc = lp1; lp1 = lp2; lp2 = LA[nz3];
-                    pm2 = pm1; pm1 = pc; pc = pp1; pp1 = pp2; pp2 = PP[nz3];
-                }
+                float &ga = gal[w * TB_R + r][lane];
+                ga = ga + c;
+                float kk = kal[w * TB_R + r][lane] * pc; const float dl = cur[r] - l; kk = kk * dl;  // fp32 term,
+                ksum += (double)kk;                                                             // fp64 sum
+                if ((smask & (1u << r)) && scol) { const float gb = l * a.w[t]; a.gbeta[bs] = a.gbeta[bs] + gb; }
             }
         }
-        float *GA = gA + (size_t)b * g.slice;
-#pragma unroll
-        for (int r = 0; r < ZT; ++r) {
-            const int z = zb + r;
-            if (z < Hp) { const size_t i = (size_t)z * ld + x; GA[i] = GA[i] + ga[r]; }
-        }
     }
-    // deterministic workgroup reduction of ksum (fixed tree), one fp64 partial per workgroup
-    __shared__ double red[TX * TY];
-    const int t = threadIdx.y * TX + threadIdx.x;
-    red[t] = (double)ksum;
+    if (xin) {
+        const bool odd = (a.nsteps & 1) != 0;   // newest level (L_{k0-nsteps+1}) is in L0 if odd
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r)
+            if (rin & (1u << r)) {
+                const size_t o = so + rofs[r] + gx;
+                a.out_l1[o] = odd ? L0[r] : L1[r];
+                a.out_l2[o] = odd ? L1[r] : L0[r];
+                a.gA[o] = gal[w * TB_R + r][lane];
+            }
+    }
+    // deterministic workgroup reduction of the sponge-coefficient partial sum
+    const int tid = threadIdx.x;
+    red[tid] = ksum;
     __syncthreads();
-    for (int w2 = TX * TY / 2; w2 > 0; w2 >>= 1) {
-        if (t < w2) red[t] += red[t + w2];
+    for (int w2 = 32 * TB_NW; w2 > 0; w2 >>= 1) {
+        if (tid < w2) red[tid] += red[tid + w2];
         __syncthreads();
     }
-    if (t == 0) {
-        const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-        gk_part[(size_t)b * nblk + blk] += red[0];
-    }
+    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + blockIdx.y * gridDim.x + blockIdx.x] += red[0];
 }
+#undef TB_VERT
 
 // --------------------------------------------------------------------------------------- K4
 struct FinArgs {
@@ -332,14 +522,16 @@ __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
     const int x0 = ix == 0 ? 0 : ix + p.nbc;
     const int x1 = ix == p.nx - 1 ? p.Wp : ix + p.nbc + 1;
     const size_t ro = (size_t)b * p.slice + (size_t)z * p.ld;
-    const float *GA = p.gA + ro;
+    const float *GA = p.gA + (size_t)b * p.ns * p.slice + (size_t)z * p.ld;   // [B][ns][Hp][ld]
     const float *V = p.coeffs + 5 * p.cstride + ro;
     const int amz = (int)(p.amin[b] / p.nx), amx = (int)(p.amin[b] - (int64_t)amz * p.nx);
     const int apz = amz == 0 ? 0 : amz + p.nbc, apx = amx == 0 ? 0 : amx + p.nbc;
     double acc = 0.0;
     for (int x = x0; x < x1; ++x) {
         float a1 = V[x] * p.dt; a1 = a1 / p.dx;
-        float t = GA[x] * (2.0f * a1); t = t / p.dx; t = t * p.dt;
+        float ga = 0.0f;
+        for (int s = 0; s < p.ns; ++s) ga = ga + GA[(size_t)s * p.slice + x];   // shots in order
+        float t = ga * (2.0f * a1); t = t / p.dx; t = t * p.dt;
         double gv = (double)t;
         if (z == p.isz) {
             for (int s = 0; s < p.ns; ++s)
@@ -351,7 +543,7 @@ __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
         }
         if (z == apz && x == apx) {
             double gk = 0.0;
-            for (int j = 0; j < p.nblk; ++j) gk += p.gk_part[(size_t)b * p.nblk + j];
+            for (int j = 0; j < p.ns * p.nblk; ++j) gk += p.gk_part[(size_t)b * p.ns * p.nblk + j];
             gv += gk / (double)p.vmin[b];
         }
         acc += gv;
@@ -511,73 +703,187 @@ struct rdq_fwi_plan {
     int Hp, Wp, ld, nrec;
     int *d_isx = nullptr, *d_rcv_start = nullptr, *d_rcv_list = nullptr;
     bool graphs = true;
+    int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
+    int chains = 1;             // independent shot groups launched as concurrent chains
     hipStream_t cap = nullptr;
+    std::vector<hipStream_t> aux;
+    std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins
     std::vector<GraphEntry> cache;
     uint64_t tick = 0;
 };
 
 namespace {
 
-StepGeo step_geo(const rdq_fwi_plan *p, int B)
+int tiles_x(int Wp, int T) { return (Wp + (64 - 4 * T) - 1) / (64 - 4 * T); }
+int tiles_y(int Hp, int T) { return (Hp + (TB_RH - 4 * T) - 1) / (TB_RH - 4 * T); }
+
+// gk_part is sized for the smallest tile interior (T = TB_MAXT): most workgroups
+int adj_blocks(const rdq_fwi_plan *p) { return tiles_x(p->Wp, TB_MAXT) * tiles_y(p->Hp, TB_MAXT); }
+
+TBGeo tb_geo(const rdq_fwi_plan *p, int B)
 {
-    StepGeo g;
+    TBGeo g;
     g.B = B; g.ns = p->g.ns; g.Hp = p->Hp; g.Wp = p->Wp; g.ld = p->ld;
+    g.isz = p->g.isz; g.igz = p->g.igz; g.ng = p->g.ng; g.nrec = p->nrec; g.st = p->g.sample_temporal;
     g.slice = (size_t)p->Hp * p->ld;
     g.cstride = (size_t)B * g.slice;
-    g.isz = p->g.isz; g.igz = p->g.igz; g.ng = p->g.ng; g.nrec = p->nrec;
+    g.level = (size_t)B * g.ns * g.slice;
     g.isx = p->d_isx; g.rcv_start = p->d_rcv_start; g.rcv_list = p->d_rcv_list;
+    g.s_off = 0; g.ns_grp = p->g.ns;
     return g;
 }
 
-int adj_blocks(const rdq_fwi_plan *p)
+// Shots split into `chains` groups, each a dependent chain of launches on its own stream, forked
+// from and joined back into `st` with events (inside graph capture this records parallel graph
+// branches).  Concurrent chains overlap each launch's fixed latency (prologue loads, store
+// drain, dispatch) with the other chains' compute.
+int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, p->g.ns)); }
+
+int ensure_aux(rdq_fwi_plan *p, int S)
 {
-    return ((p->Wp + TX - 1) / TX) * ((p->Hp + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    while ((int)p->aux.size() < S - 1) {
+        hipStream_t s;
+        RDQ_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        p->aux.push_back(s);
+    }
+    while ((int)p->evs.size() < S) {
+        hipEvent_t e;
+        RDQ_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->evs.push_back(e);
+    }
+    return 0;
 }
 
-int launch_forward(const rdq_fwi_plan *p, int B, const float *coeffs, float *seis, float *hist,
+int fork_chains(rdq_fwi_plan *p, hipStream_t st, int S)
+{
+    if (S == 1) return 0;
+    RDQ_TRY(ensure_aux(p, S));
+    RDQ_CHECK(hipEventRecord(p->evs[0], st));
+    for (int c = 1; c < S; ++c) RDQ_CHECK(hipStreamWaitEvent(p->aux[c - 1], p->evs[0], 0));
+    return 0;
+}
+
+int join_chains(rdq_fwi_plan *p, hipStream_t st, int S)
+{
+    for (int c = 1; c < S; ++c) {
+        RDQ_CHECK(hipEventRecord(p->evs[c], p->aux[c - 1]));
+        RDQ_CHECK(hipStreamWaitEvent(st, p->evs[c], 0));
+    }
+    return 0;
+}
+
+// coeffs buffer: [6][B][Hp][ld] fields, then v_model [B][nz][nx], then ks [B]
+CoefGen coef_gen(const rdq_fwi_plan *p, int B, const float *coeffs)
+{
+    CoefGen c;
+    const size_t cstride = (size_t)B * p->Hp * p->ld;
+    c.vmod = coeffs + 6 * cstride;
+    c.ks = c.vmod + (size_t)B * p->g.nz * p->g.nx;
+    c.nz = p->g.nz; c.nx = p->g.nx; c.nbc = p->g.nbc; c.Hp = p->Hp; c.Wp = p->Wp;
+    c.dt = p->g.dt; c.dx = p->g.dx;
+    c.a = (float)((double)(p->g.nbc - 1) * (double)p->g.dx);
+    return c;
+}
+
+template <class Args>
+void launch_fwd(int T, dim3 grid, hipStream_t st, const Args &a)
+{
+    const dim3 blk(64 * TB_NW);
+    switch (T) {
+    case 1: hipLaunchKernelGGL(k_fwd_tb<1>, grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(k_fwd_tb<2>, grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(k_fwd_tb<3>, grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(k_fwd_tb<4>, grid, blk, 0, st, a); break;
+    }
+}
+
+template <class Args>
+void launch_adj(int T, dim3 grid, hipStream_t st, const Args &a)
+{
+    const dim3 blk(64 * TB_NW);
+    switch (T) {
+    case 1: hipLaunchKernelGGL(k_adj_tb<1>, grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(k_adj_tb<2>, grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(k_adj_tb<3>, grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(k_adj_tb<4>, grid, blk, 0, st, a); break;
+    }
+}
+
+int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, float *hist,
                    float *ring, hipStream_t st)
 {
-    const StepGeo g = step_geo(p, B);
-    const size_t S = (size_t)B * g.ns * g.slice;   // one time level, all models and shots
-    if (hist) RDQ_CHECK(hipMemsetAsync(hist, 0, 2 * S * sizeof(float), st));
-    else RDQ_CHECK(hipMemsetAsync(ring, 0, 3 * S * sizeof(float), st));
-    const dim3 blk(TX, TY), grd((g.Wp + TX - 1) / TX, (g.Hp + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B * g.ns);
-    const int nt = p->g.nt, stt = p->g.sample_temporal;
-    for (int i = 0; i < nt; ++i) {
-        const float *p0, *p1;
-        float *pn;
-        if (hist) { p0 = hist + (size_t)i * S; p1 = hist + (size_t)(i + 1) * S; pn = hist + (size_t)(i + 2) * S; }
-        else { p0 = ring + (size_t)((i + 1) % 3) * S; p1 = ring + (size_t)((i + 2) % 3) * S; pn = ring + (size_t)(i % 3) * S; }
-        const int rec = (i % stt) == 0;
-        hipLaunchKernelGGL(k_fwd_step, grd, blk, 0, st, g, coeffs, p0, p1, pn, p->wavf[i], rec,
-                           seis + (size_t)(i / stt) * g.ng);
+    FwdTBArgs a{};
+    a.g = tb_geo(p, B);
+    const size_t L = a.g.level;
+    const int T = p->fwd_T, S = chain_count(p), ns = p->g.ns;
+    if (hist) RDQ_CHECK(hipMemsetAsync(hist, 0, 2 * L * sizeof(float), st));
+    else RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
+    a.coeffs = coeffs;
+    a.seis = seis;
+    a.hist = hist;
+    RDQ_TRY(fork_chains(p, st, S));
+    const int nt = p->g.nt;
+    for (int c = 0; c < S; ++c) {
+        a.g.s_off = c * ns / S;
+        a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
+        const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
+        const dim3 grid(tiles_x(p->Wp, T), tiles_y(p->Hp, T), B * a.g.ns_grp);
+        for (int n0 = 0, i = 0; n0 < nt; n0 += T, ++i) {
+            a.n0 = n0;
+            a.nsteps = std::min(T, nt - n0);
+            for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
+            if (hist) {
+                a.in_prev = hist + (size_t)n0 * L;          // slot n0   = P_{n0-1}
+                a.in_cur = hist + (size_t)(n0 + 1) * L;     // slot n0+1 = P_{n0}
+                a.out_prev = a.out_cur = nullptr;
+            } else {
+                const int pin = i & 1, pout = pin ^ 1;
+                a.in_prev = ring + (size_t)(2 * pin) * L;
+                a.in_cur = ring + (size_t)(2 * pin + 1) * L;
+                a.out_prev = ring + (size_t)(2 * pout) * L;
+                a.out_cur = ring + (size_t)(2 * pout + 1) * L;
+            }
+            launch_fwd(T, grid, cs, a);
+        }
     }
     RDQ_CHECK(hipGetLastError());
-    return 0;
+    return join_chains(p, st, S);
 }
 
-int launch_adjoint(const rdq_fwi_plan *p, int B, const float *coeffs, const float *hist,
+int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *hist,
                    const float *dseis, float *ring, float *gA, double *gk, float *gbeta, hipStream_t st)
 {
-    const StepGeo g = step_geo(p, B);
-    const size_t S = (size_t)B * g.ns * g.slice;
-    const int nblk = adj_blocks(p);
-    RDQ_CHECK(hipMemsetAsync(ring, 0, 3 * S * sizeof(float), st));
-    RDQ_CHECK(hipMemsetAsync(gA, 0, (size_t)B * g.slice * sizeof(float), st));
-    RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * nblk * sizeof(double), st));
-    RDQ_CHECK(hipMemsetAsync(gbeta, 0, (size_t)B * g.ns * sizeof(float), st));
-    const dim3 blk(TX, TY), grd((g.Wp + TX - 1) / TX, (g.Hp + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B);
-    const int nt = p->g.nt, stt = p->g.sample_temporal;
-    for (int k = nt; k >= 1; --k) {
-        const float *L1 = ring + (size_t)((k + 1) % 3) * S;
-        const float *L2 = ring + (size_t)((k + 2) % 3) * S;
-        float *L0 = ring + (size_t)(k % 3) * S;
-        const int rec = ((k - 1) % stt) == 0;
-        hipLaunchKernelGGL(k_adj_step, grd, blk, 0, st, g, coeffs, L1, L2, L0, hist + (size_t)k * S,
-                           gA, gk, gbeta, p->wavf[k - 1], rec, dseis + (size_t)((k - 1) / stt) * g.ng, nblk);
+    AdjTBArgs a{};
+    a.g = tb_geo(p, B);
+    const size_t L = a.g.level;
+    const int T = p->adj_T, S = chain_count(p), ns = p->g.ns;
+    const int nblk_alloc = adj_blocks(p);
+    RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
+    RDQ_CHECK(hipMemsetAsync(gA, 0, L * sizeof(float), st));
+    RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * ns * nblk_alloc * sizeof(double), st));
+    RDQ_CHECK(hipMemsetAsync(gbeta, 0, (size_t)B * ns * sizeof(float), st));
+    a.coeffs = coeffs; a.hist = hist; a.dseis = dseis; a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
+    a.nblk = nblk_alloc;
+    RDQ_TRY(fork_chains(p, st, S));
+    for (int c = 0; c < S; ++c) {
+        a.g.s_off = c * ns / S;
+        a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
+        const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
+        const dim3 grid(tiles_x(p->Wp, T), tiles_y(p->Hp, T), B * a.g.ns_grp);
+        for (int k0 = p->g.nt, i = 0; k0 >= 1; k0 -= T, ++i) {
+            a.k0 = k0;
+            a.nsteps = std::min(T, k0);
+            for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
+            const int pin = i & 1, pout = pin ^ 1;
+            a.in_l1 = ring + (size_t)(2 * pin) * L;
+            a.in_l2 = ring + (size_t)(2 * pin + 1) * L;
+            a.out_l1 = ring + (size_t)(2 * pout) * L;
+            a.out_l2 = ring + (size_t)(2 * pout + 1) * L;
+            launch_adj(T, grid, cs, a);
+        }
     }
     RDQ_CHECK(hipGetLastError());
-    return 0;
+    return join_chains(p, st, S);
 }
 
 template <class F>
@@ -668,6 +974,8 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
     if (!p) return 0;
     for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
     if (p->cap) (void)hipStreamDestroy(p->cap);
+    for (auto st : p->aux) (void)hipStreamDestroy(st);
+    for (auto e : p->evs) (void)hipEventDestroy(e);
     if (p->d_isx) (void)hipFree(p->d_isx);
     if (p->d_rcv_start) (void)hipFree(p->d_rcv_start);
     if (p->d_rcv_list) (void)hipFree(p->d_rcv_list);
@@ -682,18 +990,33 @@ int rdq_fwi_set_graphs(rdq_fwi_plan *p, int32_t enable)
     return 0;
 }
 
+int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, int32_t chains)
+{
+    if (!p || fwd_steps < 1 || fwd_steps > TB_MAXT || adj_steps < 1 || adj_steps > TB_MAXT || chains < 1 ||
+        chains > 16)
+        return RDQ_E_INVALID;
+    if (p->fwd_T != fwd_steps || p->adj_T != adj_steps || p->chains != chains) {   // graphs encode these
+        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+        p->cache.clear();
+    }
+    p->fwd_T = fwd_steps;
+    p->adj_T = adj_steps;
+    p->chains = chains;
+    return 0;
+}
+
 int rdq_fwi_sizes(const rdq_fwi_plan *p, int32_t B, rdq_fwi_sizes_t *o)
 {
     if (!p || !o || B < 1) return RDQ_E_INVALID;
     const size_t slice = (size_t)p->Hp * p->ld, ns = p->g.ns;
     o->Hp = p->Hp; o->Wp = p->Wp; o->ld = p->ld; o->nrec = p->nrec;
-    o->coeffs = 6 * (size_t)B * slice * sizeof(float);
+    o->coeffs = (6 * (size_t)B * slice + (size_t)B * p->g.nz * p->g.nx + B + 4) * sizeof(float);
     o->vstat = (size_t)B * (sizeof(float) + sizeof(int64_t)) + 16;
     o->seis = (size_t)B * ns * p->nrec * p->g.ng * sizeof(float);
     o->history = (size_t)(p->g.nt + 2) * B * ns * slice * sizeof(float);
-    o->ring = 3 * (size_t)B * ns * slice * sizeof(float);
-    o->gA = (size_t)B * slice * sizeof(float);
-    o->gk_part = (size_t)B * adj_blocks(p) * sizeof(double);
+    o->ring = 4 * (size_t)B * ns * slice * sizeof(float);
+    o->gA = (size_t)B * ns * slice * sizeof(float);
+    o->gk_part = (size_t)B * ns * adj_blocks(p) * sizeof(double);
     o->gbeta = (size_t)B * ns * sizeof(float);
     o->colsum = (size_t)B * p->Hp * p->g.nx * sizeof(double);
     return 0;
@@ -713,21 +1036,19 @@ int rdq_fwi_coeffs(const rdq_fwi_plan *p, int32_t B, const float *vn, const int6
         return RDQ_E_INVALID;
     float *vmin; int64_t *amin;
     vstat_ptrs(vstat, B, &vmin, &amin);
-    hipLaunchKernelGGL(k_vstat, dim3(B), dim3(256), 0, st, vn, strides[0], strides[2], strides[3],
-                       p->g.nz, p->g.nx, vel_mode, vmin, amin);
     CoefArgs a;
-    a.vn = vn; a.s0 = strides[0]; a.s2 = strides[2]; a.s3 = strides[3];
-    a.nz = p->g.nz; a.nx = p->g.nx; a.nbc = p->g.nbc; a.Hp = p->Hp; a.Wp = p->Wp; a.ld = p->ld;
-    a.vel_mode = vel_mode;
-    a.dt = p->g.dt; a.dx = p->g.dx;
+    a.cg = coef_gen(p, B, coeffs);
     const double ad = (double)(p->g.nbc - 1) * (double)p->g.dx;   // a = (nbc-1)*dx, pde.py:42
-    a.a = (float)ad;
-    a.two_a = (float)(2.0 * ad);
-    a.lnk = (float)std::log(10000000.0);
-    a.vmin = vmin;
+    hipLaunchKernelGGL(k_vstat, dim3(B), dim3(256), 0, st, vn, strides[0], strides[2], strides[3],
+                       p->g.nz, p->g.nx, vel_mode, (float)std::log(10000000.0), (float)(2.0 * ad), vmin, amin,
+                       const_cast<float *>(a.cg.ks));
+    a.vn = vn; a.s0 = strides[0]; a.s2 = strides[2]; a.s3 = strides[3];
+    a.vel_mode = vel_mode; a.ld = p->ld;
+    a.vmod_out = const_cast<float *>(a.cg.vmod);
     a.coeffs = coeffs;
     a.cstride = (size_t)B * p->Hp * p->ld;
     hipLaunchKernelGGL(k_coeffs, dim3((p->ld + 255) / 256, p->Hp, B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_coeff_fields, dim3((p->ld + 255) / 256, p->Hp, B), dim3(256), 0, st, a);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

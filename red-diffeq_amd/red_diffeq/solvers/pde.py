@@ -75,6 +75,10 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
+    def set_tuning(self, fwd_steps, adj_steps, chains=1):
+        _hip.check(self.lib.rdq_fwi_set_tuning(self.handle, int(fwd_steps), int(adj_steps), int(chains)),
+                   "rdq_fwi_set_tuning")
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
@@ -247,5 +251,5 @@ class FWIForward(nn.Module):
             v = self.v_denorm_func(v)
         coeffs, vstat = plan.coeffs(v, 0 if self._fused_denorm() else 1)
         sz = plan.sizes(v.shape[0])
-        f = coeffs.view(6, v.shape[0], sz.Hp, sz.ld)[..., :sz.Wp]
+        f = coeffs[:6 * v.shape[0] * sz.Hp * sz.ld].view(6, v.shape[0], sz.Hp, sz.ld)[..., :sz.Wp]
         return dict(zip(("alpha", "temp1", "temp2", "kappa", "beta", "v"), f.unbind(0)))

@@ -1,0 +1,51 @@
+"""Time the forward / adjoint time loops for every temporal-blocking depth (steps per launch).
+python tools/sweep_tb.py [--ns 8] [--B 1]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+from red_diffeq.solvers.pde import FWIForward  # noqa: E402
+from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize, v_normalize  # noqa: E402
+from red_diffeq.utils.synthetic import make_model  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--ns", type=int, default=8)
+ap.add_argument("--B", type=int, default=1)
+ap.add_argument("--nt", type=int, default=1000)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--only", type=int, default=0, help="run a single blocking depth")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+ctx = dict(n_grid=70, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=a.ns)
+fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
+v = v_normalize(torch.from_numpy(make_model("flatvel", 70, 70, batch=a.B))).to(dev)
+plan = fwi._plan(70, 70, dev)
+sz = plan.sizes(a.B)
+dseis = torch.randn(a.B, a.ns, sz.nrec, plan.ng, device=dev)
+res = []
+cfgs = [(a.only, 1)] if a.only else [(1, 1), (2, 1), (3, 1), (4, 1), (4, 2), (4, 4), (3, 2), (3, 4), (4, 8)]
+for T, C in cfgs:
+    plan.set_tuning(T, T, C)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fw, ad = [], []
+    for i in range(a.reps + 1):
+        coeffs, vstat = plan.coeffs(v, 0)
+        ev[0].record()
+        seis, hist = plan.forward(coeffs, a.B, keep_history=True)
+        ev[1].record()
+        plan.adjoint(coeffs, hist, dseis, a.B)
+        ev[2].record()
+        torch.cuda.synchronize()
+        if i:
+            fw.append(ev[0].elapsed_time(ev[1]))
+            ad.append(ev[1].elapsed_time(ev[2]))
+        del hist
+    fw, ad = sorted(fw)[len(fw) // 2], sorted(ad)[len(ad) // 2]
+    res.append({"T": T, "chains": C, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
+                "shot_ts_per_s": round(a.ns * a.nt * a.B / ((fw + ad) * 1e-3))})
+    print(json.dumps(res[-1]), flush=True)
