@@ -193,20 +193,19 @@ constexpr int TB_R = 8;                  // rows per wave
 constexpr int TB_RH = TB_NW * TB_R;      // region rows
 constexpr int TB_MAXT = 4;
 
-__device__ __forceinline__ float dpp_shr1(float v)   // lane i <- lane i-1 (x-1); lane 0 keeps v
+__device__ __forceinline__ float dpp_shr1(float v)   // lane i <- lane i-1 (x-1); lane 0 reads 0
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
-                                                                 __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
 }
-__device__ __forceinline__ float dpp_shl1(float v)   // lane i <- lane i+1 (x+1); lane 63 keeps v
+__device__ __forceinline__ float dpp_shl1(float v)   // lane i <- lane i+1 (x+1); lane 63 reads 0
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
-                                                                 __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
 }
 
 struct TBGeo {
     int B, ns, Hp, Wp, ld, isz, igz, ng, nrec, st;
     int s_off, ns_grp;                   // this launch covers shots [s_off, s_off + ns_grp)
+    int tiles_x, ntiles;                 // tile grid of this launch's blocking depth
     size_t cstride, slice, level;        // level = B*ns*slice (one time level of all slices)
     const int *isx, *rcv_start, *rcv_list;
 };
@@ -242,12 +241,42 @@ __device__ __forceinline__ Halo4 exchange(float (*xch)[TB_NW][4][64], int buf, i
     return h;
 }
 
+// the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
+__device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
+                                          int lane, const float (&fa)[4], const float (&fb)[4], Halo4 &ha,
+                                          Halo4 &hb)
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { xa[buf][w][i][lane] = fa[i]; xb[buf][w][i][lane] = fb[i]; }
+    __syncthreads();
+    const int wu = w > 0 ? w - 1 : 0, wd = w < TB_NW - 1 ? w + 1 : TB_NW - 1;
+    ha.u2 = xa[buf][wu][2][lane]; ha.u1 = xa[buf][wu][3][lane]; ha.d1 = xa[buf][wd][0][lane]; ha.d2 = xa[buf][wd][1][lane];
+    hb.u2 = xb[buf][wu][2][lane]; hb.u1 = xb[buf][wu][3][lane]; hb.d1 = xb[buf][wd][0][lane]; hb.d2 = xb[buf][wd][1][lane];
+}
+
 // vertical neighbour rows of row r from the slab + halo rows
 #define TB_VERT(ARR, r, H4, m2, m1, p1, p2)                                   \
     const float m2 = (r) >= 2 ? ARR[(r) - 2] : ((r) == 1 ? H4.u1 : H4.u2);    \
     const float m1 = (r) >= 1 ? ARR[(r) - 1] : H4.u1;                        \
     const float p1 = (r) + 1 < TB_R ? ARR[(r) + 1] : H4.d1;                  \
     const float p2 = (r) + 2 < TB_R ? ARR[(r) + 2] : ((r) + 2 == TB_R ? H4.d1 : H4.d2);
+
+// XCD-aware block -> (tile, shot) map.  Blocks are dealt round-robin over the 8 XCDs (block b
+// and b+8 share an L2); every shot of one tile gets the same (block mod 8), so the per-model
+// coefficient rows a tile reads are fetched once per XCD and re-read from that L2 by the other
+// shots of the group.  A placement guess only changes speed, never results.
+struct TileId { int tx, ty, tile, sl; bool valid; };
+
+__device__ __forceinline__ TileId decode_tile(int L, int tiles_x, int ntiles, int nsg)
+{
+    TileId t;
+    t.tile = (L / (8 * nsg)) * 8 + (L & 7);
+    t.sl = (L >> 3) % nsg;
+    t.valid = t.tile < ntiles;
+    t.ty = t.tile / tiles_x;
+    t.tx = t.tile - t.ty * tiles_x;
+    return t;
+}
 
 // cheap wrap for |v| < a few n (general v handled by the loops)
 __device__ __forceinline__ int wrapn(int v, int n)
@@ -265,11 +294,13 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
     const TBGeo &g = a.g;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-    const int b = blockIdx.z / g.ns_grp, s = g.s_off + (blockIdx.z - b * g.ns_grp), bs = b * g.ns + s;
-    const int ux = (int)blockIdx.x * IW - H + lane;                   // unwrapped column
+    const TileId ti = decode_tile(blockIdx.x, g.tiles_x, g.ntiles, g.B * g.ns_grp);
+    if (!ti.valid) return;                                            // whole workgroup: uniform
+    const int b = ti.sl / g.ns_grp, s = g.s_off + (ti.sl - b * g.ns_grp), bs = b * g.ns + s;
+    const int ux = ti.tx * IW - H + lane;                             // unwrapped column
     const int gx = wrapn(ux, g.Wp);
     const bool xin = lane >= H && lane < 64 - H && ux < g.Wp;
-    const int uz0 = (int)blockIdx.y * IH - H + w * TB_R;              // unwrapped row of r = 0
+    const int uz0 = ti.ty * IH - H + w * TB_R;                        // unwrapped row of r = 0
     const size_t so = (size_t)bs * g.slice;
     const float *AL = a.coeffs + (size_t)b * g.slice;
     const float *T1p = AL + g.cstride, *T2p = AL + 2 * g.cstride;
@@ -382,11 +413,13 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     const TBGeo &g = a.g;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.z / g.ns_grp, s = g.s_off + (blockIdx.z - b * g.ns_grp), bs = b * g.ns + s;
-    const int ux = (int)blockIdx.x * IW - H + lane;
+    const TileId ti = decode_tile(blockIdx.x, g.tiles_x, g.ntiles, g.B * g.ns_grp);
+    if (!ti.valid) return;                                            // whole workgroup: uniform
+    const int b = ti.sl / g.ns_grp, s = g.s_off + (ti.sl - b * g.ns_grp), bs = b * g.ns + s;
+    const int ux = ti.tx * IW - H + lane;
     const int gx = wrapn(ux, g.Wp);
     const bool xin = lane >= H && lane < 64 - H && ux < g.Wp;
-    const int uz0 = (int)blockIdx.y * IH - H + w * TB_R;
+    const int uz0 = ti.ty * IH - H + w * TB_R;
     const size_t so = (size_t)bs * g.slice;
     const float *AL = a.coeffs + (size_t)b * g.slice;
     const float *KAp = AL + 3 * g.cstride;
@@ -413,21 +446,35 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     const bool scol = gx == isx;
     const int rs = rmask ? g.rcv_start[gx] : 0, re = rmask ? g.rcv_start[gx + 1] : 0;
     double ksum = 0.0;
+    // history P_{k-1} on the rows whose stencil the interior needs: HBM stream, prefetched one
+    // step ahead so its latency hides under the previous step
+    float Pn[TB_R];
+    {
+        const float *PS = a.hist + (size_t)a.k0 * g.level + so + gx;
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) Pn[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if (t >= a.nsteps) break;
         const int k = a.k0 - t;
         float *cur = (t & 1) ? L0 : L1;     // L_{k+1}
         float *prv = (t & 1) ? L1 : L0;     // L_{k+2} -> overwritten with L_k
-        // history P_{k-1} on the rows whose stencil the interior needs (HBM stream, issued first)
-        const float *PS = a.hist + (size_t)k * g.level + so + gx;
         float P[TB_R];
 #pragma unroll
-        for (int r = 0; r < TB_R; ++r) P[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+        for (int r = 0; r < TB_R; ++r) P[r] = Pn[r];
+        if (t + 1 < a.nsteps) {
+            const float *PS = a.hist + (size_t)(k - 1) * g.level + so + gx;
+#pragma unroll
+            for (int r = 0; r < TB_R; ++r) Pn[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+        }
         float q[TB_R];
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) q[r] = A[r] * cur[r];
-        const Halo4 h4 = exchange(xch, t & 1, w, lane, q[0], q[1], q[TB_R - 2], q[TB_R - 1]);
+        Halo4 h4, hp;
+        const float qe[4] = {q[0], q[1], q[TB_R - 2], q[TB_R - 1]};
+        const float pe[4] = {P[0], P[1], P[TB_R - 2], P[TB_R - 1]};
+        exchange2(xch, pxc, t & 1, w, lane, qe, pe, h4, hp);
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) {
             TB_VERT(q, r, h4, qm2, qm1, qp1, qp2)
@@ -450,8 +497,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
                 if (rmask & (1u << r))
                     for (int j = rs; j < re; ++j) prv[r] = prv[r] + DS[g.rcv_list[j]];
         }
-        // gradient accumulators on the interior: needs the P stencil (second exchange)
-        const Halo4 hp = exchange(pxc, t & 1, w, lane, P[0], P[1], P[TB_R - 2], P[TB_R - 1]);
+        // gradient accumulators on the interior (P halo rows came with the same exchange)
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) {
             TB_VERT(P, r, hp, pm2, pm1, pp1, pp2)
@@ -492,7 +538,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         if (tid < w2) red[tid] += red[tid + w2];
         __syncthreads();
     }
-    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + blockIdx.y * gridDim.x + blockIdx.x] += red[0];
+    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + ti.tile] += red[0];
 }
 #undef TB_VERT
 
@@ -827,7 +873,9 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
-        const dim3 grid(tiles_x(p->Wp, T), tiles_y(p->Hp, T), B * a.g.ns_grp);
+        a.g.tiles_x = tiles_x(p->Wp, T);
+        a.g.ntiles = a.g.tiles_x * tiles_y(p->Hp, T);
+        const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
         for (int n0 = 0, i = 0; n0 < nt; n0 += T, ++i) {
             a.n0 = n0;
             a.nsteps = std::min(T, nt - n0);
@@ -869,7 +917,9 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
-        const dim3 grid(tiles_x(p->Wp, T), tiles_y(p->Hp, T), B * a.g.ns_grp);
+        a.g.tiles_x = tiles_x(p->Wp, T);
+        a.g.ntiles = a.g.tiles_x * tiles_y(p->Hp, T);
+        const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
         for (int k0 = p->g.nt, i = 0; k0 >= 1; k0 -= T, ++i) {
             a.k0 = k0;
             a.nsteps = std::min(T, k0);
