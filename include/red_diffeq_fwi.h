@@ -74,6 +74,9 @@ int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
  * 1..4) and the number of concurrent shot-group launch chains (1..16).  Results are identical
  * for every setting; only speed changes. */
 int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
+/* Kernel variant: 1 = the forward regenerates alpha/temp1/temp2 from the 20 KB model in
+ * registers instead of loading the three K3 fields (identical results). */
+int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t fwd_gen_coeffs);
 
 /* Velocity input convention of rdq_fwi_coeffs / rdq_fwi_grad_finalize. */
 #define RDQ_VEL_NORMALIZED 0  /* v_norm in [-1,1], denormalised in-kernel: (v+1)/2*3000+1500 */

@@ -212,6 +212,7 @@ struct TBGeo {
 
 struct FwdTBArgs {
     TBGeo g;
+    CoefGen cg;                          // model + sponge amplitude (GEN variant)
     const float *coeffs;                 // K3 fields: alpha, temp1, temp2 at 0, 1, 2 x cstride
     const float *in_prev, *in_cur;       // P_{n-1}, P_n   (each [B][ns][Hp][ld])
     float *hist;                         // history base (slot j = P_{j-1}) or nullptr
@@ -286,7 +287,7 @@ __device__ __forceinline__ int wrapn(int v, int n)
     return v;
 }
 
-template <int T>
+template <int T, bool GEN>
 __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
 {
     constexpr int H = 2 * T, IW = 64 - 2 * H, IH = TB_RH - 2 * H;
@@ -314,7 +315,12 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
         const int uz = uz0 + r, gz = wrapn(uz, g.Hp);
         rofs[r] = gz * g.ld;
         const int o = rofs[r] + gx;
-        A[r] = AL[o]; C1[r] = T1p[o]; C2v[r] = T2p[o];
+        if constexpr (GEN) {   // regenerate from the 20 KB model (L1-resident) instead of 3 fields
+            const Coef cf = gen_coef(a.cg, b, gz, gx);
+            A[r] = cf.al; C1[r] = cf.t1; C2v[r] = cf.t2;
+        } else {
+            A[r] = AL[o]; C1[r] = T1p[o]; C2v[r] = T2p[o];
+        }
         P0[r] = a.in_prev[so + o];
         P1[r] = a.in_cur[so + o];
         const int rr = w * TB_R + r;
@@ -751,6 +757,7 @@ struct rdq_fwi_plan {
     bool graphs = true;
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
+    bool fwd_gen = false;       // forward regenerates coefficients from the model (vs loading K3)
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;
     std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins
@@ -831,15 +838,23 @@ CoefGen coef_gen(const rdq_fwi_plan *p, int B, const float *coeffs)
     return c;
 }
 
-template <class Args>
-void launch_fwd(int T, dim3 grid, hipStream_t st, const Args &a)
+template <int TT, bool G>
+void launch_fwd1(dim3 grid, hipStream_t st, const FwdTBArgs &a)
 {
-    const dim3 blk(64 * TB_NW);
-    switch (T) {
-    case 1: hipLaunchKernelGGL(k_fwd_tb<1>, grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(k_fwd_tb<2>, grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(k_fwd_tb<3>, grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(k_fwd_tb<4>, grid, blk, 0, st, a); break;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_tb<TT, G>), grid, dim3(64 * TB_NW), 0, st, a);
+}
+
+void launch_fwd(int T, bool gen, dim3 grid, hipStream_t st, const FwdTBArgs &a)
+{
+    switch (T * 2 + (gen ? 1 : 0)) {
+    case 2: launch_fwd1<1, false>(grid, st, a); break;
+    case 3: launch_fwd1<1, true>(grid, st, a); break;
+    case 4: launch_fwd1<2, false>(grid, st, a); break;
+    case 5: launch_fwd1<2, true>(grid, st, a); break;
+    case 6: launch_fwd1<3, false>(grid, st, a); break;
+    case 7: launch_fwd1<3, true>(grid, st, a); break;
+    case 8: launch_fwd1<4, false>(grid, st, a); break;
+    default: launch_fwd1<4, true>(grid, st, a); break;
     }
 }
 
@@ -865,6 +880,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
     if (hist) RDQ_CHECK(hipMemsetAsync(hist, 0, 2 * L * sizeof(float), st));
     else RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
     a.coeffs = coeffs;
+    a.cg = coef_gen(p, B, coeffs);
     a.seis = seis;
     a.hist = hist;
     RDQ_TRY(fork_chains(p, st, S));
@@ -891,7 +907,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
                 a.out_prev = ring + (size_t)(2 * pout) * L;
                 a.out_cur = ring + (size_t)(2 * pout + 1) * L;
             }
-            launch_fwd(T, grid, cs, a);
+            launch_fwd(T, p->fwd_gen, grid, cs, a);
         }
     }
     RDQ_CHECK(hipGetLastError());
@@ -1052,6 +1068,17 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     p->fwd_T = fwd_steps;
     p->adj_T = adj_steps;
     p->chains = chains;
+    return 0;
+}
+
+int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t fwd_gen_coeffs)
+{
+    if (!p) return RDQ_E_INVALID;
+    if (p->fwd_gen != (fwd_gen_coeffs != 0)) {
+        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+        p->cache.clear();
+    }
+    p->fwd_gen = fwd_gen_coeffs != 0;
     return 0;
 }
 

@@ -40,6 +40,7 @@ SIGNATURES = {
     "rdq_fwi_sizes": (c_int32, [c_void_p, c_int32, ctypes.POINTER(FwiSizes)]),
     "rdq_fwi_set_graphs": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_tuning": (c_int32, [c_void_p, c_int32, c_int32, c_int32]),
+    "rdq_fwi_set_variant": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_coeffs": (c_int32, [c_void_p, c_int32, c_void_p, ctypes.POINTER(c_int64), c_int32,
                                  c_void_p, c_void_p, c_void_p]),
     "rdq_fwi_forward": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

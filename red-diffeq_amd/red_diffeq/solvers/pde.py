@@ -75,6 +75,9 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
+    def set_variant(self, fwd_gen_coeffs):
+        _hip.check(self.lib.rdq_fwi_set_variant(self.handle, int(bool(fwd_gen_coeffs))), "rdq_fwi_set_variant")
+
     def set_tuning(self, fwd_steps, adj_steps, chains=1):
         _hip.check(self.lib.rdq_fwi_set_tuning(self.handle, int(fwd_steps), int(adj_steps), int(chains)),
                    "rdq_fwi_set_tuning")

@@ -42,6 +42,7 @@ def test_forward_bitexact_vs_reference(cuda, name, kw, graphs, steps, chains):
     plan = fwi._plan(v.shape[2], v.shape[3], v.device)
     plan.set_graphs(graphs)
     plan.set_tuning(steps, steps, chains)
+    plan.set_variant(steps % 2 == 0)          # both coefficient sources
     with torch.no_grad():
         seis = fwi(v).cpu().numpy()                    # no-grad: ring path
     assert bits_equal(seis, z["seis"]), np.abs(seis - z["seis"]).max()

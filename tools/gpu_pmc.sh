@@ -19,4 +19,7 @@ FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
 GROUPS
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc/calib -o run -- \
+   python3 tools/pmc_calib.py > gpurun_out/pmc/calib.log 2>&1
+rc=$?; echo "pmc calib rc=$rc"; [ $rc -eq 0 ] || exit $rc
 exit 0

@@ -28,9 +28,11 @@ plan = fwi._plan(70, 70, dev)
 sz = plan.sizes(a.B)
 dseis = torch.randn(a.B, a.ns, sz.nrec, plan.ng, device=dev)
 res = []
-cfgs = [(a.only, 1)] if a.only else [(1, 1), (2, 1), (3, 1), (4, 1)]
-for T, C in cfgs:
+cfgs = [(a.only, 0)] if a.only else [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (2, 1), (3, 1), (4, 1)]
+for T, G in cfgs:
+    C = 1
     plan.set_tuning(T, T, C)
+    plan.set_variant(G)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     fw, ad = [], []
     for i in range(a.reps + 1):
@@ -46,6 +48,6 @@ for T, C in cfgs:
             ad.append(ev[1].elapsed_time(ev[2]))
         del hist
     fw, ad = sorted(fw)[len(fw) // 2], sorted(ad)[len(ad) // 2]
-    res.append({"T": T, "chains": C, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
+    res.append({"T": T, "gen": G, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
                 "shot_ts_per_s": round(a.ns * a.nt * a.B / ((fw + ad) * 1e-3))})
     print(json.dumps(res[-1]), flush=True)
