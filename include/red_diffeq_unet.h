@@ -1,0 +1,81 @@
+/*
+ * red_diffeq_unet.h — C ABI of the U-Net epsilon-predictor kernels (libred_diffeq_hip.so).
+ *
+ * Replaces the PyTorch/cuDNN arithmetic of the reference U-Net forward
+ * (SimingShan/red-diffeq red_diffeq/models/diffusion.py:78-301) and the RED regulariser's
+ * elementwise prologue/epilogue (diffusion.py:393-429, 516-519;
+ * red_diffeq/regularization/diffusion.py:63-81).  fp32 NCHW tensors, caller-owned, stream-ordered,
+ * 0 / negative error codes, deterministic (no atomics).
+ */
+#ifndef RED_DIFFEQ_UNET_H
+#define RED_DIFFEQ_UNET_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Logical conv input = the (B, cin1 + cin2, H, W) tensor formed from x (and x2) by `in_mode`:
+ *   0 RDQ_IN_PLAIN      x (B,cin1,H,W) ++ x2 (B,cin2,H,W) along channels (torch.cat, diffusion.py:293-299)
+ *   1 RDQ_IN_UPSAMPLE2  x (B,cin1,H/2,W/2) nearest-upsampled x2 (nn.Upsample, diffusion.py:79)
+ *   2 RDQ_IN_UNSHUFFLE2 x (B,cin1/4,2H,2W), channel c*4+p1*2+p2 <- x[c][2h+p1][2w+p2]
+ *                       (einops 'b c (h p1) (w p2) -> b (c p1 p2) h w', diffusion.py:82)        */
+#define RDQ_IN_PLAIN 0
+#define RDQ_IN_UPSAMPLE2 1
+#define RDQ_IN_UNSHUFFLE2 2
+
+typedef struct rdq_conv_desc {
+    int32_t B, cin1, cin2, H, W, cout, kh, kw, pad, in_mode;
+} rdq_conv_desc;
+
+/* y = conv2d(input, w, bias, stride 1, padding pad) [+ residual]   (nn.Conv2d, implicit GEMM on
+ * fp32 MFMA v_mfma_f32_16x16x4_f32).  w: [cout][cin1+cin2][kh][kw]; bias/residual nullable. */
+int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+               const float *residual, float *y, hipStream_t stream);
+
+/* GroupNorm(G) -> [x*(scale+1)+shift] -> SiLU  (Block.forward, diffusion.py:142-149).
+ * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes. */
+size_t rdq_group_norm_ws_bytes(int32_t B, int32_t C, int32_t HW, int32_t G);
+int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, const float *x, const float *gamma,
+                        const float *beta, const float *scale_shift, float *y, void *ws, hipStream_t stream);
+
+/* RMSNorm: F.normalize(x, dim=1) * g * sqrt(C) [+ residual]  (diffusion.py:84-91). */
+int rdq_rmsnorm(int32_t B, int32_t C, int32_t HW, const float *x, const float *g, const float *residual, float *y,
+                hipStream_t stream);
+
+/* y[b][o] = act_out( W[o] . act_in(x[b]) + bias[o] ); act_in: 0 none / 1 SiLU, act_out: 0 none / 1 GELU(erf). */
+int rdq_linear(int32_t B, int32_t in, int32_t out, const float *x, const float *w, const float *bias,
+               int32_t act_in, int32_t act_out, float *y, hipStream_t stream);
+
+/* SinusoidalPosEmb (diffusion.py:93-107): y[b] = [sin(t_b f), cos(t_b f)], f_i = exp(-i ln(theta)/(half-1)). */
+int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, float *y, hipStream_t stream);
+
+/* LinearAttention core (diffusion.py:182-194; dh <= 32), qkv = to_qkv(RMSNorm(x)) as (B, 3*heads*dh, n);
+ * mem_kv (2, heads, dh, nmem); out (B, heads*dh, n) before to_out.  ws: rdq_linear_attention_ws_bytes. */
+size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh);
+int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
+                         const float *mem_kv, float *out, void *ws, hipStream_t stream);
+
+/* Attention core with Attend(flash=False) (diffusion.py:209-217): softmax(q k^T dh^-1/2) v over
+ * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32, n <= 256. */
+int rdq_full_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, const float *qkv,
+                       const float *mem_kv, float *out, hipStream_t stream);
+
+/* RED prologue: x_t = sqrt(abar_t) x0 + sqrt(1-abar_t) eps  (q_sample, diffusion.py:516-519);
+ * tables are the fp32 schedule buffers, t int64 [B], n elements per sample. */
+int rdq_red_q_sample(int32_t B, int64_t n, const float *sqrt_ac, const float *sqrt_1mac, const int64_t *t,
+                     const float *x0, const float *eps, float *xt, hipStream_t stream);
+/* RED epilogue (pred_noise objective, clip_x_start + rederive_pred_noise, diffusion.py:393-419):
+ *   x0_hat = clamp(sr[t] x_t - srm1[t] eps_hat, -1, 1);  eps' = (sr[t] x_t - x0_hat) / srm1[t];
+ *   g = eps' - eps   (regularization/diffusion.py:74). */
+int rdq_red_epilogue(int32_t B, int64_t n, const float *sqrt_recip_ac, const float *sqrt_recipm1_ac,
+                     const int64_t *t, const float *xt, const float *eps_hat, const float *eps, float *g,
+                     hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RED_DIFFEQ_UNET_H */

@@ -33,7 +33,12 @@ class FwiSizes(ctypes.Structure):
                 ("colsum", c_size_t)]
 
 
-# name -> (restype, argtypes); must match include/red_diffeq_fwi.h (tests check every symbol)
+class ConvDesc(ctypes.Structure):
+    """struct rdq_conv_desc."""
+    _fields_ = [(n, c_int32) for n in ("B", "cin1", "cin2", "H", "W", "cout", "kh", "kw", "pad", "in_mode")]
+
+
+# name -> (restype, argtypes); must match include/*.h (tests check every symbol)
 SIGNATURES = {
     "rdq_fwi_plan_create": (c_int32, [ctypes.POINTER(FwiGeom), ctypes.POINTER(c_void_p)]),
     "rdq_fwi_plan_destroy": (c_int32, [c_void_p]),
@@ -56,7 +61,27 @@ SIGNATURES = {
     "rdq_smooth_reg_forward": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "rdq_smooth_reg_backward": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                           c_void_p, c_void_p]),
+    # include/red_diffeq_unet.h
+    "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p]),
+    "rdq_group_norm_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
+    "rdq_group_norm_silu": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rdq_rmsnorm": (c_int32, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rdq_linear": (c_int32, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+                             c_void_p]),
+    "rdq_sinusoidal_emb": (c_int32, [c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
+    "rdq_linear_attention_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_linear_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
+    "rdq_full_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+    "rdq_red_q_sample": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
+    "rdq_red_epilogue": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
 }
+
 
 _lib = None
 

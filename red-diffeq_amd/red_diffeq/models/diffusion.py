@@ -55,10 +55,8 @@ def unnormalize_to_zero_to_one(t):
 
 
 class _Rearrange(nn.Module):
-    """Parameter-free stand-in for einops' Rearrange at index 0 of Downsample (keeps keys)."""
-
-    def forward(self, x):
-        return ops.pixel_unshuffle2(x)
+    """Parameter-free stand-in for einops' Rearrange at index 0 of Downsample (keeps keys); the
+    pixel-unshuffle itself is folded into the following conv's gather (ops.UNSHUFFLE2)."""
 
 
 def Upsample(dim, dim_out=None):
@@ -87,11 +85,7 @@ class SinusoidalPosEmb(nn.Module):
         self.theta = theta
 
     def forward(self, x):
-        half = self.dim // 2
-        emb = math.log(self.theta) / (half - 1)
-        emb = torch.exp(torch.arange(half, device=x.device) * -emb)
-        emb = x[:, None] * emb[None, :]
-        return torch.cat((emb.sin(), emb.cos()), dim=-1)
+        return ops.sinusoidal(x, self.dim, self.theta)
 
 
 class Block(nn.Module):
@@ -103,8 +97,8 @@ class Block(nn.Module):
         self.norm = nn.GroupNorm(groups, dim_out)
         self.act = nn.SiLU()
 
-    def forward(self, x, scale_shift=None):
-        x = ops.conv2d(x, self.proj)
+    def forward(self, x, scale_shift=None, skip=None):
+        x = ops.conv2d(x, self.proj, x2=skip)          # skip: the concatenated U-Net skip (293-299)
         return ops.group_norm_affine_silu(x, self.norm, scale_shift)
 
 
@@ -116,15 +110,18 @@ class ResnetBlock(nn.Module):
         self.block2 = Block(dim_out, dim_out, groups=groups)
         self.res_conv = nn.Conv2d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
 
-    def forward(self, x, time_emb=None):
+    def forward(self, x, time_emb=None, skip=None):
+        """(reference 160-168); `skip` = the tensor the reference torch.cat's onto x first."""
         scale_shift = None
         if exists(self.mlp) and exists(time_emb):
-            te = ops.linear(F.silu(time_emb), self.mlp[1])
-            scale_shift = te[:, :, None, None].chunk(2, dim=1)
-        h = self.block1(x, scale_shift=scale_shift)
+            scale_shift = ops.linear(time_emb, self.mlp[1], act_in=1)   # Linear(SiLU(t)): (B, 2C)
+        h = self.block1(x, scale_shift=scale_shift, skip=skip)
         h = self.block2(h)
-        res = ops.conv2d(x, self.res_conv) if isinstance(self.res_conv, nn.Conv2d) else x
-        return h + res
+        if isinstance(self.res_conv, nn.Conv2d):
+            return ops.conv2d(x, self.res_conv, x2=skip, residual=h)    # h + res_conv(x), fused
+        if skip is not None:
+            x = torch.cat((x, skip), dim=1)
+        return h + x
 
 
 class LinearAttention(nn.Module):
@@ -139,6 +136,7 @@ class LinearAttention(nn.Module):
         self.to_out = nn.Sequential(nn.Conv2d(hidden, dim, 1), RMSNorm(dim))
 
     def forward(self, x):
+        """Returns LinearAttention(x) + x (the residual of Unet.forward is fused)."""
         return ops.linear_attention(x, self)
 
 
@@ -154,6 +152,7 @@ class Attention(nn.Module):
         self.to_out = nn.Conv2d(hidden, dim, 1)
 
     def forward(self, x):
+        """Returns Attention(x) + x (the residual of Unet.forward is fused)."""
         return ops.full_attention(x, self)
 
 
@@ -215,17 +214,16 @@ class Unet(nn.Module):
         return 2 ** (len(self.downs) - 1)
 
     def _time(self, time):
-        t = self.time_mlp[0](time)
-        t = ops.linear(t, self.time_mlp[1])
-        t = F.gelu(t)
+        t = ops.sinusoidal(time, self.time_mlp[0].dim, self.time_mlp[0].theta)
+        t = ops.linear(t, self.time_mlp[1], act_out=1)                  # Linear -> GELU
         return ops.linear(t, self.time_mlp[3])
 
     def _resample(self, x, m):
         if isinstance(m, nn.Conv2d):
             return ops.conv2d(x, m)
         if isinstance(m[0], nn.Upsample):
-            return ops.conv2d(ops.upsample_nearest2(x), m[1])
-        return ops.conv2d(ops.pixel_unshuffle2(x), m[1])
+            return ops.conv2d(x, m[1], mode=ops.UPSAMPLE2)               # nearest x2 folded in
+        return ops.conv2d(x, m[1], mode=ops.UNSHUFFLE2)                  # pixel-unshuffle folded in
 
     def forward(self, x, time, x_self_cond=None):
         assert all(divisible_by(d, self.downsample_factor) for d in x.shape[-2:]), \
@@ -234,28 +232,25 @@ class Unet(nn.Module):
             x_self_cond = default(x_self_cond, lambda: torch.zeros_like(x))
             x = torch.cat((x_self_cond, x), dim=1)
         x = ops.conv2d(x, self.init_conv)
-        r = x.clone()
+        r = x
         t = self._time(time)
         h = []
         for b1, b2, attn, down in self.downs:
             x = b1(x, t)
             h.append(x)
             x = b2(x, t)
-            x = attn(x) + x
+            x = attn(x)                       # attn(x) + x
             h.append(x)
             x = self._resample(x, down)
         x = self.mid_block1(x, t)
-        x = self.mid_attn(x) + x
+        x = self.mid_attn(x)
         x = self.mid_block2(x, t)
         for b1, b2, attn, up in self.ups:
-            x = torch.cat((x, h.pop()), dim=1)
-            x = b1(x, t)
-            x = torch.cat((x, h.pop()), dim=1)
-            x = b2(x, t)
-            x = attn(x) + x
+            x = b1(x, t, skip=h.pop())        # cat((x, skip)) folded into the conv gather
+            x = b2(x, t, skip=h.pop())
+            x = attn(x)
             x = self._resample(x, up)
-        x = torch.cat((x, r), dim=1)
-        x = self.final_res_block(x, t)
+        x = self.final_res_block(x, t, skip=r)
         return ops.conv2d(x, self.final_conv)
 
 

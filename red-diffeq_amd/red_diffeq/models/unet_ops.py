@@ -1,79 +1,156 @@
-"""Arithmetic of the U-Net blocks (reference red_diffeq/models/diffusion.py:78-218).
+"""Arithmetic of the U-Net blocks (reference red_diffeq/models/diffusion.py:78-218) on the HIP
+kernels of csrc/unet.hip (C ABI include/red_diffeq_unet.h).
 
-Every U-Net block calls these functions; they are the seam where the HIP kernels
-(csrc/unet.hip: MFMA implicit-GEMM conv, fused GroupNorm-affine-SiLU, attention) replace the
-PyTorch formulation.  Functions without a HIP kernel yet use PyTorch ops on the same device;
-``HIP_OPS`` lists the ones that run hand-written kernels.
+Data movement of the reference graph is folded into the kernels: skip concatenation
+(torch.cat, diffusion.py:293-299), nearest x2 upsample (79) and 2x2 pixel-unshuffle (82) into the
+conv operand gather; bias, residual adds (168, 286, 290, 297) into the conv / RMSNorm epilogues;
+the time-conditioned scale/shift (147) and SiLU into GroupNorm.  There is no PyTorch fallback:
+CPU tensors raise.
 """
+import ctypes
+import math
+
 import torch
-import torch.nn.functional as F
 
-HIP_OPS = set()
+from .. import _hip
 
-
-def pixel_unshuffle2(x):
-    """einops 'b c (h p1) (w p2) -> b (c p1 p2) h w' with p1 = p2 = 2 (diffusion.py:82)."""
-    return F.pixel_unshuffle(x, 2)
+PLAIN, UPSAMPLE2, UNSHUFFLE2 = 0, 1, 2
 
 
-def upsample_nearest2(x):
-    """nn.Upsample(scale_factor=2, mode='nearest') (diffusion.py:79)."""
-    return F.interpolate(x, scale_factor=2, mode="nearest")
+def _f(t):
+    return t.contiguous() if t is not None else None
 
 
-def conv2d(x, conv):
-    return F.conv2d(x, conv.weight, conv.bias, padding=conv.padding)
+def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
+    """nn.Conv2d(stride 1, padding conv.padding) of the logical input formed by `mode`."""
+    _hip.require_device(x)
+    x = _f(x)
+    x2 = _f(x2)
+    w = conv.weight
+    cout, cin, kh, kw = w.shape
+    B = x.shape[0]
+    if mode == UPSAMPLE2:
+        H, W = x.shape[2] * 2, x.shape[3] * 2
+    elif mode == UNSHUFFLE2:
+        H, W = x.shape[2] // 2, x.shape[3] // 2
+    else:
+        H, W = x.shape[2], x.shape[3]
+    cin1 = x.shape[1] * (4 if mode == UNSHUFFLE2 else 1)
+    cin2 = x2.shape[1] if x2 is not None else 0
+    if cin1 + cin2 != cin:
+        raise ValueError(f"conv expects {cin} input channels, got {cin1}+{cin2}")
+    pad = conv.padding[0] if isinstance(conv.padding, tuple) else int(conv.padding)
+    d = _hip.ConvDesc(B=B, cin1=cin1, cin2=cin2, H=H, W=W, cout=cout, kh=kh, kw=kw, pad=pad, in_mode=mode)
+    y = torch.empty(B, cout, H, W, device=x.device, dtype=torch.float32)
+    res = _f(residual)
+    _hip.check(_hip.lib().rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(w.contiguous()),
+                                     _hip.ptr(conv.bias), _hip.ptr(res), _hip.ptr(y), _hip.stream_of(x)),
+               "rdq_conv2d")
+    return y
 
 
-def linear(x, lin):
-    return F.linear(x, lin.weight, lin.bias)
+def linear(x, lin, act_in=0, act_out=0):
+    """act_out(Linear(act_in(x))); act 1 = SiLU on the input / GELU(erf) on the output."""
+    _hip.require_device(x)
+    x = _f(x)
+    B, fin = x.shape
+    fout = lin.weight.shape[0]
+    y = torch.empty(B, fout, device=x.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_linear(B, fin, fout, _hip.ptr(x), _hip.ptr(lin.weight), _hip.ptr(lin.bias), act_in,
+                                     act_out, _hip.ptr(y), _hip.stream_of(x)), "rdq_linear")
+    return y
+
+
+def sinusoidal(t, dim, theta=10000):
+    _hip.require_device(t)
+    t = t.to(torch.int64).contiguous()
+    y = torch.empty(t.shape[0], dim, device=t.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_sinusoidal_emb(t.shape[0], dim, float(theta), _hip.ptr(t), _hip.ptr(y),
+                                             _hip.stream_of(t)), "rdq_sinusoidal_emb")
+    return y
 
 
 def group_norm_affine_silu(x, norm, scale_shift=None):
-    """GroupNorm -> x*(scale+1)+shift -> SiLU (Block.forward, diffusion.py:142-149)."""
-    x = F.group_norm(x, norm.num_groups, norm.weight, norm.bias, norm.eps)
-    if scale_shift is not None:
-        scale, shift = scale_shift
-        x = x * (scale + 1) + shift
-    return F.silu(x)
+    """GroupNorm -> x*(scale+1)+shift -> SiLU; scale_shift: (B, 2C) (scale first, as chunk(2))."""
+    _hip.require_device(x)
+    x = _f(x)
+    B, C, H, W = x.shape
+    L = _hip.lib()
+    ws = torch.empty(max(8, int(L.rdq_group_norm_ws_bytes(B, C, H * W, norm.num_groups))), dtype=torch.uint8,
+                     device=x.device)
+    y = torch.empty_like(x)
+    ss = _f(scale_shift)
+    _hip.check(L.rdq_group_norm_silu(B, C, H * W, norm.num_groups, float(norm.eps), _hip.ptr(x), _hip.ptr(norm.weight),
+                                     _hip.ptr(norm.bias), _hip.ptr(ss), _hip.ptr(y), _hip.ptr(ws),
+                                     _hip.stream_of(x)), "rdq_group_norm_silu")
+    return y
 
 
-def rmsnorm(x, g):
-    """F.normalize(x, dim=1) * g * sqrt(C) (diffusion.py:84-91)."""
-    return F.normalize(x, dim=1) * g * x.shape[1] ** 0.5
+def rmsnorm(x, g, residual=None):
+    """F.normalize(x, dim=1) * g * sqrt(C) [+ residual]."""
+    _hip.require_device(x)
+    x = _f(x)
+    B, C, H, W = x.shape
+    y = torch.empty_like(x)
+    _hip.check(_hip.lib().rdq_rmsnorm(B, C, H * W, _hip.ptr(x), _hip.ptr(g), _hip.ptr(_f(residual)), _hip.ptr(y),
+                                      _hip.stream_of(x)), "rdq_rmsnorm")
+    return y
 
 
 def linear_attention(x, m):
-    """LinearAttention.forward (diffusion.py:182-195): softmax-feature attention with memory kv."""
-    b, c, h, w = x.shape
+    """LinearAttention.forward(x) + x (diffusion.py:182-195 and the residual at 286/297)."""
+    B, C, H, W = x.shape
     heads = m.heads
+    dh = m.to_qkv.weight.shape[0] // (3 * heads)
     xn = rmsnorm(x, m.norm.g)
-    qkv = F.conv2d(xn, m.to_qkv.weight).chunk(3, dim=1)
-    q, k, v = (t.reshape(b, heads, -1, h * w) for t in qkv)
-    mk, mv = (t.unsqueeze(0).expand(b, -1, -1, -1) for t in m.mem_kv)
-    k = torch.cat((mk, k), dim=-1)
-    v = torch.cat((mv, v), dim=-1)
-    q = q.softmax(dim=-2) * m.scale
-    k = k.softmax(dim=-1)
-    context = torch.einsum("bhdn,bhen->bhde", k, v)
-    out = torch.einsum("bhde,bhdn->bhen", context, q).reshape(b, -1, h, w)
-    out = F.conv2d(out, m.to_out[0].weight, m.to_out[0].bias)
-    return rmsnorm(out, m.to_out[1].g)
+    qkv = conv2d(xn, m.to_qkv)
+    L = _hip.lib()
+    ws = torch.empty(int(L.rdq_linear_attention_ws_bytes(B, heads, dh)), dtype=torch.uint8, device=x.device)
+    out = torch.empty(B, heads * dh, H, W, device=x.device, dtype=torch.float32)
+    _hip.check(L.rdq_linear_attention(B, heads, dh, H * W, m.mem_kv.shape[-1], float(m.scale), _hip.ptr(qkv),
+                                      _hip.ptr(m.mem_kv.contiguous()), _hip.ptr(out), _hip.ptr(ws),
+                                      _hip.stream_of(x)), "rdq_linear_attention")
+    o = conv2d(out, m.to_out[0])
+    return rmsnorm(o, m.to_out[1].g, residual=x)
 
 
 def full_attention(x, m):
-    """Attention.forward (diffusion.py:209-218) with Attend(flash=False):
-    softmax(q k^T / sqrt(d)) v over (memory kv + pixels)."""
-    b, c, h, w = x.shape
+    """Attention.forward(x) + x (diffusion.py:209-218 with Attend(flash=False), residual 290)."""
+    B, C, H, W = x.shape
     heads = m.heads
+    dh = m.to_qkv.weight.shape[0] // (3 * heads)
     xn = rmsnorm(x, m.norm.g)
-    qkv = F.conv2d(xn, m.to_qkv.weight).chunk(3, dim=1)
-    q, k, v = (t.reshape(b, heads, -1, h * w).transpose(-1, -2) for t in qkv)
-    mk, mv = (t.unsqueeze(0).expand(b, -1, -1, -1) for t in m.mem_kv)
-    k = torch.cat((mk, k), dim=-2)
-    v = torch.cat((mv, v), dim=-2)
-    scale = q.shape[-1] ** -0.5
-    attn = (torch.einsum("bhid,bhjd->bhij", q, k) * scale).softmax(dim=-1)
-    out = torch.einsum("bhij,bhjd->bhid", attn, v)
-    out = out.transpose(-1, -2).reshape(b, -1, h, w)
-    return F.conv2d(out, m.to_out.weight, m.to_out.bias)
+    qkv = conv2d(xn, m.to_qkv)
+    out = torch.empty(B, heads * dh, H, W, device=x.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_full_attention(B, heads, dh, H * W, m.mem_kv.shape[-2], _hip.ptr(qkv),
+                                             _hip.ptr(m.mem_kv.contiguous()), _hip.ptr(out), _hip.stream_of(x)),
+               "rdq_full_attention")
+    return conv2d(out, m.to_out, residual=x)
+
+
+def red_q_sample(diff, x0, t, eps):
+    """q_sample (diffusion.py:516-519) on the fp32 schedule buffers."""
+    x0, eps = _f(x0), _f(eps)
+    B = x0.shape[0]
+    xt = torch.empty_like(x0)
+    _hip.check(_hip.lib().rdq_red_q_sample(B, x0[0].numel(), _hip.ptr(diff.sqrt_alphas_cumprod),
+                                           _hip.ptr(diff.sqrt_one_minus_alphas_cumprod), _hip.ptr(t), _hip.ptr(x0),
+                                           _hip.ptr(eps), _hip.ptr(xt), _hip.stream_of(x0)), "rdq_red_q_sample")
+    return xt
+
+
+def red_epilogue(diff, xt, t, eps_hat, eps):
+    """(eps' - eps) with eps' re-derived from the clipped x0 (diffusion.py:393-419)."""
+    xt, eps_hat, eps = _f(xt), _f(eps_hat), _f(eps)
+    B = xt.shape[0]
+    g = torch.empty_like(xt)
+    _hip.check(_hip.lib().rdq_red_epilogue(B, xt[0].numel(), _hip.ptr(diff.sqrt_recip_alphas_cumprod),
+                                           _hip.ptr(diff.sqrt_recipm1_alphas_cumprod), _hip.ptr(t), _hip.ptr(xt),
+                                           _hip.ptr(eps_hat), _hip.ptr(eps), _hip.ptr(g), _hip.stream_of(xt)),
+               "rdq_red_epilogue")
+    return g
+
+
+HIP_OPS = {"conv2d", "linear", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+           "full_attention", "red_q_sample", "red_epilogue"}
+del math

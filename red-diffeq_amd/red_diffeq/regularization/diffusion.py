@@ -44,9 +44,16 @@ class RED_DiffEq:
         return self.fixed_timestep if self.fixed_timestep is not None else self.diffusion_model.num_timesteps
 
     def _eps_residual(self, x0, t, noise):
-        """(eps_hat' - eps) for padded 72x72 inputs: q_sample -> U-Net -> clip/re-derive."""
+        """(eps_hat' - eps) for padded 72x72 inputs: q_sample -> U-Net -> clip/re-derive.
+        For the pred_noise objective (the RED-DiffEq configs) the prologue / epilogue are the
+        fused HIP kernels; other objectives use GaussianDiffusion.model_predictions."""
         dm = self.diffusion_model
         with torch.no_grad():
+            if getattr(dm, "objective", None) == "pred_noise" and x0.is_cuda and not dm.self_condition:
+                from ..models import unet_ops
+                x_t = unet_ops.red_q_sample(dm, x0, t, noise)
+                eps_hat = dm.model(x_t, t, None)
+                return unet_ops.red_epilogue(dm, x_t, t, eps_hat, noise)
             x_t = dm.q_sample(x0, t=t, noise=noise)
             pred = dm.model_predictions(x_t, t=t, x_self_cond=None, clip_x_start=True,
                                         rederive_pred_noise=True)

@@ -92,7 +92,8 @@ def test_calculate_patches_vs_reference():
 def test_c_abi_library_exports_every_header_symbol():
     from red_diffeq import _hip
     lib = _hip.load_library()
-    hdr = open(os.path.join(ROOT, "include", "red_diffeq_fwi.h")).read()
+    import glob
+    hdr = "".join(open(h).read() for h in glob.glob(os.path.join(ROOT, "include", "*.h")))
     names = set(re.findall(r"^(?:int|size_t)\s+(rdq_\w+)\(", hdr, flags=re.M))
     assert names == set(_hip.SIGNATURES), names ^ set(_hip.SIGNATURES)
     for n in names:
