@@ -30,6 +30,7 @@ extern "C" {
 
 #define RDQ_E_INVALID (-10001) /* bad argument / shape */
 #define RDQ_E_NOMEM (-10002)   /* host allocation failed */
+#define RDQ_E_HANDOFF (-10003) /* a persistent kernel's neighbour hand-off timed out (results invalid) */
 
 /* Acquisition geometry, host memory.  Mirrors FWIForward's ctx after __init__ and adj_sr
  * (pde.py:16-23, 54-59): all indices already on the padded grid. */
@@ -56,8 +57,10 @@ typedef struct rdq_fwi_sizes_t {
     size_t vstat;              /* float vmin[B] then int64 argmin[B] (row-major index into nz*nx) */
     size_t seis;               /* float [B][ns][nrec][ng] */
     size_t history;            /* float [nt+2][B][ns][Hp][ld]; slot j = P_{j-1} */
-    size_t ring;               /* float [4][B][ns][Hp][ld]: two in/out level pairs (no-grad forward,
-                                  adjoint lambdas) */
+    size_t ring;               /* workspace, 32 B per grid cell: the chunked kernels use it as float
+                                  [4][B][ns][Hp][ld] (two in/out level pairs: no-grad forward,
+                                  adjoint lambdas), the persistent kernels as u64 hand-off granules
+                                  [2 parity][2 level][B][ns][Hp][ld] */
     size_t gA;                 /* float [B][ns][Hp][ld] per-shot accumulator d(loss)/d(alpha) */
     size_t gk_part;            /* double [B][ns][n_adj_blocks] sponge-coefficient partial sums */
     size_t gbeta;              /* float [B][ns] source-amplitude gradient */
@@ -77,6 +80,23 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
 /* Kernel variant: 1 = the forward regenerates alpha/temp1/temp2 from the 20 KB model in
  * registers instead of loading the three K3 fields (identical results). */
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t fwd_gen_coeffs);
+/* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
+ * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the
+ * device, with 64 x 96 regions if they fit, else 64 x 64; 12 / 8 = only that region height;
+ * 0 = always the chunked launches.  Identical results in every mode. */
+int rdq_fwi_set_persistent(rdq_fwi_plan *plan, int32_t mode);
+/* Synchronises `stream` and reports (then clears) a persistent-kernel hand-off timeout:
+ * 0, or RDQ_E_HANDOFF when some launch since the last call gave up waiting for a neighbour. */
+int rdq_fwi_status(rdq_fwi_plan *plan, hipStream_t stream);
+/* Which kernels a forward / adjoint call for batch B runs: out = {forward persistent region
+ * height in waves (0 = chunked), the same for the adjoint, forward steps per epoch/launch,
+ * adjoint steps per epoch/launch}. */
+int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[4]);
+/* Diagnostics: 1 = the persistent kernels accumulate per-wave phase times (s_memrealtime, 10 ns
+ * ticks); read_profile synchronises the device, returns and clears them:
+ * out[0..3] forward {hand-off wait, time steps, publish, waves}, out[4..7] the same for the adjoint. */
+int rdq_fwi_set_profile(rdq_fwi_plan *plan, int32_t enable);
+int rdq_fwi_read_profile(rdq_fwi_plan *plan, uint64_t out[8]);
 
 /* Velocity input convention of rdq_fwi_coeffs / rdq_fwi_grad_finalize. */
 #define RDQ_VEL_NORMALIZED 0  /* v_norm in [-1,1], denormalised in-kernel: (v+1)/2*3000+1500 */
@@ -88,8 +108,9 @@ int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t fwd_gen_coeffs);
 int rdq_fwi_coeffs(const rdq_fwi_plan *plan, int32_t B, const float *v, const int64_t strides[4],
                    int32_t vel_mode, float *coeffs, void *vstat, hipStream_t stream);
 
-/* K1: forward time loop (pde.py:74-86).  history == NULL: no-grad forward through the 3-slice
- * `ring`; otherwise every P_j is kept in `history` for the adjoint (ring unused). */
+/* K1: forward time loop (pde.py:74-86).  history == NULL: no-grad forward; otherwise every P_j
+ * is kept in `history` for the adjoint.  `ring` is the workspace (required when the persistent
+ * kernel runs; the chunked history path does not touch it). */
 int rdq_fwi_forward(const rdq_fwi_plan *plan, int32_t B, const float *coeffs, float *seis,
                     float *history, float *ring, hipStream_t stream);
 

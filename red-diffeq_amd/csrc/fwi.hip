@@ -242,6 +242,24 @@ __device__ __forceinline__ Halo4 exchange(float (*xch)[TB_NW][4][64], int buf, i
     return h;
 }
 
+template <int NW>
+__device__ __forceinline__ Halo4 exchange_nw(float (*xch)[NW][4][64], int buf, int w, int lane, float top0,
+                                             float top1, float bot1, float bot0)
+{
+    xch[buf][w][0][lane] = top0;
+    xch[buf][w][1][lane] = top1;
+    xch[buf][w][2][lane] = bot1;
+    xch[buf][w][3][lane] = bot0;
+    __syncthreads();
+    Halo4 h;
+    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
+    h.u2 = xch[buf][wu][2][lane];
+    h.u1 = xch[buf][wu][3][lane];
+    h.d1 = xch[buf][wd][0][lane];
+    h.d2 = xch[buf][wd][1][lane];
+    return h;
+}
+
 // the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
 __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
                                           int lane, const float (&fa)[4], const float (&fb)[4], Halo4 &ha,
@@ -546,6 +564,490 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     }
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + ti.tile] += red[0];
 }
+
+// --------------------------------------------------------------------------------------- K1/K2
+// Persistent variants: ONE launch runs the whole time loop.  Every workgroup keeps its region
+// (coefficients + two wavefield levels) in VGPRs for all nt steps; after each epoch of T steps it
+// publishes the H-wide border of its interior (the only cells any other region's halo reads) and
+// reloads its own halo ring from the neighbours' publications.  The hand-off is the
+// data-is-the-flag form (8-byte {tag, value} granules, write-through `sc1` stores, `sc1` loads
+// re-read until every tag matches: cdna_hip_programming.md §6 G16, R2), so there is no flag, no
+// fence and no kernel boundary between epochs — the per-launch prologue, store drain and launch gap
+// of the chunked path (≈7.5 µs per forward launch at OpenFWI size) become one hand-off per epoch.
+// Needs every workgroup of the launch resident at once: the host checks the grid against the
+// occupancy query and uses the chunked kernels otherwise; every spin is bounded (a timeout sets
+// the plan's status word, reported by rdq_fwi_status, and the kernel still runs to completion).
+//
+// The time step is VALU-issue-bound (wave64 fp32 VALU = 4 cycles), so the kernels are written
+// to keep per-cell instructions at the stencil's own: row predicates are wave-uniform bits, the
+// per-lane ones are three loop-invariant masks, and every history / granule access is a buffer
+// instruction (scalar base + one lane offset + one uniform row offset: no 64-bit address VALU).
+// Region height is a template parameter (NW waves x 8 rows): 12 waves -> 64 x 96 regions, one
+// workgroup per CU at OpenFWI size (28 tiles x 8 shots = 224 <= 256 CUs).
+//
+// Granule buffer (inside the caller's `ring`): [2 epoch parity][2 level][B][ns][Hp][ld] u64,
+// zeroed before each launch; tag = epoch index (>= 1) so a zeroed granule never matches.
+constexpr int CP_SC1 = 16;                           // buffer cache policy: sc1 (write-through / L1 bypass)
+constexpr unsigned long long PT_TIMEOUT_TICKS = 20000000ull;   // 200 ms of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int bytes = 0x7fffffff)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+constexpr int OOB = (int)0x80000000u;               // buffer offset beyond every range: store dropped
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, int voff, int soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gran_put(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v)
+{
+    u32x2 x;
+    x.x = __float_as_uint(v);
+    x.y = tag;
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, CP_SC1);
+}
+__device__ __forceinline__ u32x2 gran_get(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, CP_SC1);
+}
+
+// padded-grid row of region row uz (periodic wrap, pde.py:79); |uz| < 2 Hp
+__device__ __forceinline__ int wrap_row(int uz, int Hp)
+{
+    uz = uz < 0 ? uz + Hp : uz;
+    return uz >= Hp ? uz - Hp : uz;
+}
+
+// Region geometry of the persistent kernels (flat locals so every block-/wave-uniform value stays
+// provably uniform: SGPRs and scalar branches, never waterfall loops).  Row classes are
+// wave-uniform bit masks; lane classes: xin (own interior column), bx (interior column within H of
+// the tile's x edge, or a one-tile-wide grid), cx (column within H of the own interior: the
+// T-step dependence cone).
+#define PT_REGION_INIT(NW_)                                                                         \
+    constexpr int R = TB_R, RH = (NW_) * TB_R, H = 2 * T, IW = 64 - 2 * H, IH = RH - 2 * H;        \
+    const int lane = threadIdx.x & 63;                                                              \
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                \
+    const TileId ti = decode_tile(blockIdx.x, g.tiles_x, g.ntiles, g.B * g.ns_grp);                 \
+    if (!ti.valid) return;                                                                          \
+    const int b = __builtin_amdgcn_readfirstlane(ti.sl / g.ns_grp);                                 \
+    const int s = __builtin_amdgcn_readfirstlane(g.s_off + (ti.sl - b * g.ns_grp));                 \
+    const int bs = b * g.ns + s;                                                                    \
+    const int tx = __builtin_amdgcn_readfirstlane(ti.tx), ty = __builtin_amdgcn_readfirstlane(ti.ty); \
+    const int tile = __builtin_amdgcn_readfirstlane(ti.tile);                                       \
+    const int ux = tx * IW - H + lane;                                                              \
+    const int gx = wrapn(ux, g.Wp);                                                                 \
+    const bool xin = lane >= H && lane < 64 - H && ux < g.Wp;                                       \
+    const int vw = min(IW, g.Wp - tx * IW), vh = min(IH, g.Hp - ty * IH);                           \
+    const bool bx = g.tiles_x == 1 || lane - H < H || lane - H >= vw - H;                           \
+    const bool cx = lane - H < vw + H;                                                              \
+    const int uz0 = ty * IH - H + w * R;                                                            \
+    unsigned rin = 0, rby = 0, rcy = 0;                                                             \
+    _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                 \
+        const int rr = w * R + r, ly = rr - H;                                                      \
+        if (rr >= H && rr < RH - H && uz0 + r < g.Hp) rin |= 1u << r;                               \
+        if (g.ntiles == g.tiles_x || ly < H || ly >= vh - H) rby |= 1u << r;                        \
+        if (ly < vh + H) rcy |= 1u << r;                                                            \
+    }                                                                                               \
+    const size_t so = (size_t)bs * g.slice;                                                         \
+    const int vo4 = gx * 4, vo8 = gx * 8;                                                           \
+    const bool hx = !xin && cx, xb = xin && bx;
+#define PT_ROFS(r) (wrap_row(uz0 + (r), g.Hp) * g.ld)
+
+// Reload the halo cells of two levels V0/V1 from the granule slot GR (level 1 at +lev_bytes),
+// zero the dead cells.  `live` turns false once this wave gave up (timeout / another's timeout).
+#define PT_SWEEP(GR, TAG, V0, V1)                                                                   \
+    {                                                                                               \
+        unsigned long long t0_ = 0;                                                                 \
+        for (unsigned pass_ = 0; live; ++pass_) {                                                   \
+            bool ok_ = true;                                                                        \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
+                const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                      \
+                if (!rowin_ && !rowcy_) continue;                                                   \
+                if (rowin_ ? hx : cx) {                                                             \
+                    const int sof_ = PT_ROFS(r) * 8;                                                \
+                    const u32x2 x0_ = gran_get(GR, vo8, sof_);                                      \
+                    const u32x2 x1_ = gran_get(GR, vo8, sof_ + lev_bytes);                          \
+                    ok_ = ok_ && x0_.y == (TAG) && x1_.y == (TAG);                                  \
+                    V0[r] = __uint_as_float(x0_.x);                                                 \
+                    V1[r] = __uint_as_float(x1_.x);                                                 \
+                }                                                                                   \
+            }                                                                                       \
+            if (__all(ok_)) break;                                                                  \
+            if (pass_ == 0) t0_ = __builtin_amdgcn_s_memrealtime();                                 \
+            if ((pass_ & 15) == 15) {                                                               \
+                if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)   \
+                    live = false;                                                                   \
+                else if (__builtin_amdgcn_s_memrealtime() - t0_ > PT_TIMEOUT_TICKS) {               \
+                    __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   \
+                    live = false;                                                                   \
+                }                                                                                   \
+            }                                                                                       \
+            __builtin_amdgcn_s_sleep(1);                                                            \
+        }                                                                                           \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
+            const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                          \
+            if (rowin_ ? (!xin && !cx) : (!rowcy_ || !cx)) { V0[r] = 0.0f; V1[r] = 0.0f; }          \
+        }                                                                                           \
+    }
+
+// publish the own-interior border cells of two levels
+#define PT_PUBLISH(GR, TAG, V0, V1)                                                                 \
+    _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                 \
+        if (!((rin >> r) & 1u)) continue;                                                           \
+        if (((rby >> r) & 1u) ? xin : xb) {                                                         \
+            const int sof_ = PT_ROFS(r) * 8;                                                        \
+            gran_put(GR, vo8, sof_, (TAG), V0[r]);                                                  \
+            gran_put(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                                      \
+        }                                                                                           \
+    }
+
+#define PT_PROF(ACC)                                                                                \
+    if (a.prof) { const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); ACC += now_ - tm; tm = now_; }
+
+// Re-materialise a wave-uniform value inside the time loop: stops the compiler from hoisting the
+// per-row compares on it out of the loop as live 64-bit lane masks (which spill to VGPR lanes and
+// cost v_readlane pairs in every step).
+#define LAUNDER(x) asm volatile("" : "+s"(x))
+
+struct FwdPtArgs {
+    TBGeo g;
+    const float *coeffs;                 // alpha, temp1, temp2 at 0, 1, 2 x cstride; beta at 4
+    const float *wav;                    // [nt] fp32 wavelet
+    float *hist;                         // history base (slot j = P_{j-1}) or nullptr (no-grad)
+    float *seis;
+    unsigned long long *gran;
+    unsigned *status;
+    unsigned long long *prof;            // nullable: [0] hand-off, [1] steps, [2] publish (10 ns ticks), [3] waves
+    int nt;
+};
+
+// one forward step P_{n+1} = temp1 P_n - temp2 P_{n-1} + alpha N(P_n) (+ source), pde.py:79-81
+#define FWD_STEP(CUR, PRV)                                                                          \
+    {                                                                                               \
+        const Halo4 h4 = exchange_nw<NW>(xch, n & 1, w, lane, CUR[0], CUR[1], CUR[R - 2], CUR[R - 1]); \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
+            TB_VERT(CUR, r, h4, zm2, zm1, zp1, zp2)                                                 \
+            const float c = CUR[r];                                                                 \
+            const float xl1 = dpp_shr1(c), xr1 = dpp_shl1(c);                                       \
+            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                                   \
+            float s1 = zm1 + zp1; s1 = s1 + xl1; s1 = s1 + xr1;                                     \
+            float s2 = zm2 + zp2; s2 = s2 + xl2; s2 = s2 + xr2;                                     \
+            float lap = C2 * s1; const float l2 = C3 * s2; lap = lap + l2;                          \
+            float a1 = C1[r] * c; const float a2 = C2v[r] * PRV[r]; a1 = a1 - a2;                   \
+            const float a3 = A[r] * lap;                                                            \
+            PRV[r] = a1 + a3;                                                                       \
+        }                                                                                           \
+        if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
+            unsigned sm_ = smask;                                                                   \
+            LAUNDER(sm_);                                                                           \
+            /* x + (-0) == x bit for bit: the other lanes add -0 instead of branching */            \
+            const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if ((sm_ >> r) & 1u) PRV[r] = PRV[r] + add;                                         \
+        }                                                                                           \
+        if (a.hist && (t + 2 < T || e + 1 == nep)) {   /* own cells only: hv = OOB elsewhere */     \
+            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PRV[r], hv[r], 0);            \
+        }                                                                                           \
+        if (rrow >= 0 && (n % g.st) == 0) {                                                         \
+            float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;                           \
+            int rr_ = rrow;                                                                         \
+            LAUNDER(rr_);                                                                           \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if (r == rr_ && rec) SK[rcv0] = PRV[r];                                             \
+            if (rmulti) {                                /* several receivers in one column */      \
+                float v_ = 0.0f;                                                                    \
+                _Pragma("unroll") for (int r = 0; r < R; ++r) if (r == rr_) v_ = PRV[r];            \
+                for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = v_;                           \
+            }                                                                                       \
+        }                                                                                           \
+    }
+
+template <int T, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
+{
+    __shared__ float xch[2][NW][4][64];
+    const TBGeo &g = a.g;
+    PT_REGION_INIT(NW)
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    float A[R], C1[R], C2v[R], P0[R], P1[R];
+    unsigned smask = 0;
+    int rrow = -1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int gz = wrap_row(uz0 + r, g.Hp);
+        const int o = gz * g.ld + gx;
+        A[r] = AL[o]; C1[r] = AL[g.cstride + o]; C2v[r] = AL[2 * g.cstride + o];
+        P0[r] = 0.0f; P1[r] = 0.0f;                       // P_{-1} = P_0 = 0 (pde.py:74-75)
+        if (gz == g.isz) smask |= 1u << r;
+        if (gz == g.igz && ((rin >> r) & 1u)) rrow = r;
+    }
+    const int isx = g.isx[s];
+    const bool scol = gx == isx;
+    const float bsrc = (smask != 0) ? AL[4 * g.cstride + (size_t)g.isz * g.ld + isx] : 0.0f;
+
+    int rs = 0, re = 0, rcv0 = -1;
+    if (rrow >= 0) {
+        rs = g.rcv_start[gx]; re = g.rcv_start[gx + 1];
+        rcv0 = rs < re ? g.rcv_list[rs] : -1;             // the (usually only) receiver of this column
+    }
+    const bool rec = rrow >= 0 && xin && rcv0 >= 0;
+    const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
+    const size_t L = g.level;
+    const int lev_bytes = (int)(L * 8);
+    const int slice_bytes = (int)(g.slice * 4);
+    int hv[R];                                            // history store offset of (row, lane), OOB if not own
+#pragma unroll
+    for (int r = 0; r < R; ++r) hv[r] = (((rin >> r) & 1u) && xin) ? (PT_ROFS(r) + gx) * 4 : OOB;
+    const int nep = (a.nt + T - 1) / T;
+    bool live = true;
+    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (int e = 0; e < nep; ++e) {
+        const int n0 = e * T;
+        if (e > 0) {
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * (e & 1)) * L + so);
+            PT_SWEEP(GR, (unsigned)e, P0, P1)
+        }
+        float wv[T];                                      // wavelet samples of this epoch
+#pragma unroll
+        for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + t, a.nt - 1)];
+        // The previous epoch's last two levels are stored only now, after the hand-off: on gfx9
+        // vmcnt also counts stores, so stores still in flight would hold up every hand-off load.
+        if (e > 0 && a.hist) {
+            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n0 + 1) * L + so, slice_bytes);
+#pragma unroll
+            for (int r = 0; r < R; ++r) bstore(HR, P1[r], hv[r], 0);            // P_{n0}
+            if (T >= 2) {
+                const __amdgpu_buffer_rsrc_t HQ = rsrc_of(a.hist + (size_t)n0 * L + so, slice_bytes);
+#pragma unroll
+                for (int r = 0; r < R; ++r) bstore(HQ, P0[r], hv[r], 0);        // P_{n0-1}
+            }
+        }
+        PT_PROF(tsw)
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int n = n0 + t;
+            if (n >= a.nt) break;
+            if (t & 1) FWD_STEP(P0, P1)
+            else FWD_STEP(P1, P0)
+        }
+        if (T & 1) {   // keep "P1 = newest" at every epoch boundary
+#pragma unroll
+            for (int r = 0; r < R; ++r) { const float tmp = P0[r]; P0[r] = P1[r]; P1[r] = tmp; }
+        }
+        PT_PROF(tst)
+        if (e + 1 < nep) {
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
+            PT_PUBLISH(GR, (unsigned)(e + 1), P0, P1)
+        }
+        PT_PROF(tpb)
+    }
+    if (a.prof && lane == 0) {
+        atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+    }
+}
+#undef FWD_STEP
+
+struct AdjPtArgs {
+    TBGeo g;
+    const float *coeffs;                 // alpha, temp1, temp2, kappa at 0..3 x cstride
+    const float *wav;
+    const float *hist;                   // slot k = P_{k-1}
+    const float *dseis;
+    float *gA;                           // [B][ns][Hp][ld]
+    double *gk_part;                     // [B*ns][nblk]
+    float *gbeta;                        // [B*ns]
+    unsigned long long *gran;
+    unsigned *status;
+    unsigned long long *prof;            // nullable, as FwdPtArgs
+    int nt, nblk;
+};
+
+// P_{k-1} (history slot K) rows uz0-2 .. uz0+9 into PD
+#define ADJ_PLOAD(PD, K)                                                                            \
+    {                                                                                               \
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(K) * L + so);                   \
+        _Pragma("unroll") for (int i = 0; i < PR; ++i) PD[i] = bload(HR, pv[i], 0);                \
+    }
+
+// one adjoint step k; CUR = L_{k+1}, PRV = L_{k+2} -> L_k, P = P_{k-1} rows -2..9
+#define ADJ_STEP(CUR, PRV, P, PN)                                                                   \
+    {                                                                                               \
+        if (grad && k > 1 && (t + 1 < T || e + 1 == nep)) ADJ_PLOAD(PN, k - 1)                     \
+        const float dcur = dn;                                                                      \
+        if (rmask) dn = DLOAD(k - 1);                                                               \
+        float q[R];                                                                                 \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) q[r] = A[r] * CUR[r];                         \
+        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0], q[1], q[R - 2], q[R - 1]);      \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
+            TB_VERT(q, r, h4, qm2, qm1, qp1, qp2)                                                   \
+            const float qc = q[r];                                                                  \
+            const float xl1 = dpp_shr1(qc), xr1 = dpp_shl1(qc);                                     \
+            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                                   \
+            float n1 = qm1 + qp1; n1 = n1 + xl1; n1 = n1 + xr1;                                     \
+            float n2 = qm2 + qp2; n2 = n2 + xl2; n2 = n2 + xr2;                                     \
+            float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;                           \
+            float l = T1v[r] * CUR[r]; const float l2 = T2v[r] * PRV[r]; l = l - l2; l = l + nb;    \
+            PRV[r] = l;                                                                             \
+        }                                                                                           \
+        if (rmask && ((k - 1) % g.st) == 0) {        /* uniform: receiver row waves */             \
+            unsigned rm_ = rmask;                                                                   \
+            LAUNDER(rm_);                                                                           \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if ((rm_ >> r) & 1u) PRV[r] = PRV[r] + dcur;     /* -0 on lanes without a receiver */ \
+            if (rmulti) {                                /* several receivers in one column */      \
+                const float *DS = DSb + (size_t)((k - 1) / g.st) * g.ng;                            \
+                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
+                    if ((rm_ >> r) & 1u)                                                            \
+                        for (int jj = rs + 1; jj < re; ++jj) PRV[r] = PRV[r] + DS[g.rcv_list[jj]];  \
+            }                                                                                       \
+        }                                                                                           \
+        if (grad) {                                                                                 \
+            unsigned rin_ = rin;                                                                    \
+            LAUNDER(rin_);                                                                          \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
+                if (!full && !((rin_ >> r) & 1u)) continue;                                        \
+                const float pc = P[r + 2];                                                          \
+                const float xl1 = dpp_shr1(pc), xr1 = dpp_shl1(pc);                                 \
+                const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                               \
+                float s1 = P[r + 1] + P[r + 3]; s1 = s1 + xl1; s1 = s1 + xr1;                       \
+                float s2 = P[r] + P[r + 4]; s2 = s2 + xl2; s2 = s2 + xr2;                           \
+                float lap = C2 * s1; const float lq = C3 * s2; lap = lap + lq;                      \
+                float d = C1X2 * pc; d = d + lap;                                                   \
+                const float l = PRV[r];                                                             \
+                const float c = l * d;                                                              \
+                GA[r] = GA[r] + c;                                                                  \
+                float kk = KP[r] * pc; const float dl = CUR[r] - l; kk = kk * dl;                   \
+                if (xin) ksum += (double)kk;                                                        \
+            }                                                                                       \
+            if (smask) {                             /* gbeta: the source cell's lane only */      \
+                unsigned sm_ = smask;                                                               \
+                LAUNDER(sm_);                                                                       \
+                const float wk = wv[t];                                                             \
+                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
+                    if ((sm_ >> r) & 1u) { const float gb = scol ? PRV[r] * wk : -0.0f; gbacc = gbacc + gb; } \
+            }                                                                                       \
+        }                                                                                           \
+    }
+
+// Adjoint, persistent.  Per step k = nt..1:
+//   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
+//   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k),
+//   gbeta[s] += L_k(src) w[k-1]        (interior cells; accumulators in registers for all nt steps)
+// P_{k-1} comes from the history: each wave loads its interior rows +-2 (12 rows) one step ahead
+// into alternating register arrays (no copies, so the wait lands at the gradient, not at the
+// step's start) and needs no LDS exchange for it.
+template <int T, int NW>
+__global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
+{
+    constexpr int PR = TB_R + 4;
+    __shared__ float xch[2][NW][4][64];
+    __shared__ double red[64 * NW];
+    const TBGeo &g = a.g;
+    PT_REGION_INIT(NW)
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    float A[R], T1v[R], T2v[R], KP[R], L0[R], L1[R], GA[R];
+    unsigned smask = 0, rmask = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int gz = wrap_row(uz0 + r, g.Hp);
+        const int o = gz * g.ld + gx;
+        A[r] = AL[o]; T1v[r] = AL[g.cstride + o]; T2v[r] = AL[2 * g.cstride + o]; KP[r] = AL[3 * g.cstride + o];
+        L0[r] = 0.0f; L1[r] = 0.0f;                       // L_{nt+1} = L_{nt+2} = 0
+        GA[r] = 0.0f;
+        if (gz == g.isz && ((rin >> r) & 1u)) smask |= 1u << r;
+        if (gz == g.igz) rmask |= 1u << r;
+    }
+    const bool scol = xin && gx == g.isx[s];
+    const bool full = rin == 0xFFu;
+    int rs = 0, re = 0, rcv0 = -1;
+    if (rmask) {
+        rs = g.rcv_start[gx]; re = g.rcv_start[gx + 1];
+        rcv0 = rs < re ? g.rcv_list[rs] : -1;
+    }
+    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.ng;
+#define DLOAD(KK) ((rcv0 >= 0 && (KK) >= 1 && (((KK) - 1) % g.st) == 0) ? DSb[(size_t)(((KK) - 1) / g.st) * g.ng + rcv0] : -0.0f)
+    const bool rmulti = __any(re - rs > 1);
+    const bool grad = rin != 0;                           // uniform: this wave has interior rows
+    double ksum = 0.0;
+    float gbacc = 0.0f;
+    const size_t L = g.level;
+    const int lev_bytes = (int)(L * 8);
+    float PA[PR], PB[PR];
+    int pv[PR];                                           // P row (uz0 - 2 + i) offset of this lane
+#pragma unroll
+    for (int i = 0; i < PR; ++i) { PA[i] = 0.0f; PB[i] = 0.0f; pv[i] = (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4; }
+    if (grad) ADJ_PLOAD(PA, a.nt)
+    float dn = rmask ? DLOAD(a.nt) : 0.0f;
+    const int nep = (a.nt + T - 1) / T;
+    bool live = true;
+    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (int e = 0; e < nep; ++e) {
+        if (e > 0) {
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * (e & 1)) * L + so);
+            PT_SWEEP(GR, (unsigned)e, L0, L1)
+            // this epoch's first P is loaded only now: loads in flight would hold up the hand-off
+            // loads (in-order vmcnt)
+            if (grad) ADJ_PLOAD(PA, a.nt - e * T)
+        }
+        float wv[T];                                      // w[k-1] of this epoch's steps
+#pragma unroll
+        for (int t = 0; t < T; ++t) wv[t] = a.wav[max(a.nt - (e * T + t) - 1, 0)];
+        PT_PROF(tsw)
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int j = e * T + t;
+            if (j >= a.nt) break;
+            const int k = a.nt - j;
+            if (t & 1) ADJ_STEP(L0, L1, PB, PA)
+            else ADJ_STEP(L1, L0, PA, PB)
+        }
+        if (T & 1) {   // keep "L1 = newest, PA = next step's P" at every epoch boundary
+#pragma unroll
+            for (int r = 0; r < R; ++r) { const float tmp = L0[r]; L0[r] = L1[r]; L1[r] = tmp; }
+#pragma unroll
+            for (int i = 0; i < PR; ++i) { const float tmp = PA[i]; PA[i] = PB[i]; PB[i] = tmp; }
+        }
+        PT_PROF(tst)
+        if (e + 1 < nep) {
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
+            PT_PUBLISH(GR, (unsigned)(e + 1), L0, L1)
+        }
+        PT_PROF(tpb)
+    }
+#undef DLOAD
+    if (a.prof && lane == 0) {
+        atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+    }
+    if (xin) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if ((rin >> r) & 1u) a.gA[so + (size_t)PT_ROFS(r) + gx] = GA[r];
+    }
+    if (smask && scol) a.gbeta[bs] = gbacc;
+    // deterministic workgroup reduction of the sponge-coefficient partial sum
+    const int tid = threadIdx.x;
+    red[tid] = ksum;
+    __syncthreads();
+    for (int w2 = 512; w2 > 0; w2 >>= 1) {
+        if (tid < w2 && tid + w2 < 64 * NW) red[tid] += red[tid + w2];
+        __syncthreads();
+    }
+    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
+}
+#undef ADJ_STEP
+#undef ADJ_PLOAD
+#undef PT_SWEEP
+#undef PT_PUBLISH
+#undef PT_PROF
+#undef PT_ROFS
+#undef PT_REGION_INIT
+#undef LAUNDER
 #undef TB_VERT
 
 // --------------------------------------------------------------------------------------- K4
@@ -754,7 +1256,13 @@ struct rdq_fwi_plan {
     std::vector<float> wavf;
     int Hp, Wp, ld, nrec;
     int *d_isx = nullptr, *d_rcv_start = nullptr, *d_rcv_list = nullptr;
+    float *d_wav = nullptr;     // fp32 wavelet [nt] (persistent kernels)
+    unsigned *d_status = nullptr;   // hand-off timeout word (rdq_fwi_status)
+    unsigned long long *d_prof = nullptr;   // phase counters (rdq_fwi_set_profile): fwd [0..3], adj [4..7]
     bool graphs = true;
+    int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves)
+    int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
+    int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = false;       // forward regenerates coefficients from the model (vs loading K3)
@@ -868,6 +1376,129 @@ void launch_adj(int T, dim3 grid, hipStream_t st, const Args &a)
     case 3: hipLaunchKernelGGL(k_adj_tb<3>, grid, blk, 0, st, a); break;
     default: hipLaunchKernelGGL(k_adj_tb<4>, grid, blk, 0, st, a); break;
     }
+}
+
+// Workgroups of a persistent kernel the device holds at once (occupancy query x CUs).
+template <class K>
+int resident_capacity(K kernel, int nthreads, int &cache)
+{
+    if (cache) return cache;
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, nthreads, 0) != hipSuccess) return -1;
+    cache = cus * nb;
+    return cache;
+}
+
+template <int NW>
+int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
+{
+    int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
+    switch (T) {
+    case 1: return adj ? resident_capacity(k_adj_pt<1, NW>, 64 * NW, c[1]) : resident_capacity(k_fwd_pt<1, NW>, 64 * NW, c[1]);
+    case 2: return adj ? resident_capacity(k_adj_pt<2, NW>, 64 * NW, c[2]) : resident_capacity(k_fwd_pt<2, NW>, 64 * NW, c[2]);
+    case 3: return adj ? resident_capacity(k_adj_pt<3, NW>, 64 * NW, c[3]) : resident_capacity(k_fwd_pt<3, NW>, 64 * NW, c[3]);
+    default: return adj ? resident_capacity(k_adj_pt<4, NW>, 64 * NW, c[4]) : resident_capacity(k_fwd_pt<4, NW>, 64 * NW, c[4]);
+    }
+}
+
+// grid of a persistent launch covering every shot of B models at depth T with NW-wave regions
+unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW)
+{
+    const int ih = NW * TB_R - 4 * T;
+    const int nt_ = tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih);
+    return (unsigned)((nt_ + 7) / 8 * 8) * (unsigned)B * (unsigned)p->g.ns;
+}
+
+// region height (waves) of the persistent kernel for this call, 0 = not resident -> chunked.
+// Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).
+int persistent_nw(rdq_fwi_plan *p, int B, bool adj)
+{
+    if (!p->persist) return 0;
+    const int T = adj ? p->adj_T : p->fwd_T;
+    const int want = p->persist;   // 1 = auto, 8 / 12 = forced
+    if (want == 1 || want == 12) {
+        const int c = capacity_nw<12>(p, adj, T);
+        if (c > 0 && pt_grid(p, B, T, 12) <= (unsigned)c) return 12;
+    }
+    if (want == 1 || want == 8) {
+        const int c = capacity_nw<8>(p, adj, T);
+        if (c > 0 && pt_grid(p, B, T, 8) <= (unsigned)c) return 8;
+    }
+    return 0;
+}
+
+template <int NW>
+void launch_fwd_pt(int T, dim3 grid, hipStream_t st, const FwdPtArgs &a)
+{
+    const dim3 blk(64 * NW);
+    switch (T) {
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<1, NW>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<2, NW>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<3, NW>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW>), grid, blk, 0, st, a); break;
+    }
+}
+
+template <int NW>
+void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
+{
+    const dim3 blk(64 * NW);
+    switch (T) {
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW>), grid, blk, 0, st, a); break;
+    }
+}
+
+int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, float *seis, float *hist, float *ring,
+                      hipStream_t st)
+{
+    FwdPtArgs a{};
+    a.g = tb_geo(p, B);
+    const int T = p->fwd_T;
+    const size_t L = a.g.level;
+    if (hist) RDQ_CHECK(hipMemsetAsync(hist, 0, 2 * L * sizeof(float), st));
+    RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(unsigned long long), st));
+    const int ih = NW * TB_R - 4 * T;
+    a.g.tiles_x = tiles_x(p->Wp, T);
+    a.g.ntiles = a.g.tiles_x * ((p->Hp + ih - 1) / ih);
+    a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
+    a.gran = reinterpret_cast<unsigned long long *>(ring);
+    a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof;
+    const dim3 grid(pt_grid(p, B, T, NW));
+    if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
+    else launch_fwd_pt<8>(T, grid, st, a);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, const float *hist, const float *dseis,
+                      float *ring, float *gA, double *gk, float *gbeta, hipStream_t st)
+{
+    AdjPtArgs a{};
+    a.g = tb_geo(p, B);
+    const int T = p->adj_T;
+    const size_t L = a.g.level;
+    const int nblk_alloc = adj_blocks(p);
+    RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(unsigned long long), st));
+    RDQ_CHECK(hipMemsetAsync(gA, 0, L * sizeof(float), st));
+    RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * p->g.ns * nblk_alloc * sizeof(double), st));
+    RDQ_CHECK(hipMemsetAsync(gbeta, 0, (size_t)B * p->g.ns * sizeof(float), st));
+    const int ih = NW * TB_R - 4 * T;
+    a.g.tiles_x = tiles_x(p->Wp, T);
+    a.g.ntiles = a.g.tiles_x * ((p->Hp + ih - 1) / ih);
+    a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.dseis = dseis;
+    a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
+    a.gran = reinterpret_cast<unsigned long long *>(ring);
+    a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + 4 : nullptr;
+    const dim3 grid(pt_grid(p, B, T, NW));
+    if (NW == 12) launch_adj_pt<12>(T, grid, st, a);
+    else launch_adj_pt<8>(T, grid, st, a);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
 }
 
 int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, float *hist,
@@ -1030,6 +1661,10 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
     if (e == hipSuccess) e = hipMemcpy(p->d_isx, p->isx.data(), sizeof(int) * geom->ns, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_rcv_start, start.data(), sizeof(int) * (p->Wp + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_rcv_list, order.data(), sizeof(int) * geom->ng, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_wav, sizeof(float) * geom->nt);
+    if (e == hipSuccess) e = hipMemcpy(p->d_wav, p->wavf.data(), sizeof(float) * geom->nt, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_status, 256);
+    if (e == hipSuccess) e = hipMemset(p->d_status, 0, 256);
     if (e != hipSuccess) { rdq_fwi_plan_destroy(p); return -(int)e; }
     *out = p;
     return 0;
@@ -1045,6 +1680,9 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
     if (p->d_isx) (void)hipFree(p->d_isx);
     if (p->d_rcv_start) (void)hipFree(p->d_rcv_start);
     if (p->d_rcv_list) (void)hipFree(p->d_rcv_list);
+    if (p->d_wav) (void)hipFree(p->d_wav);
+    if (p->d_status) (void)hipFree(p->d_status);
+    if (p->d_prof) (void)hipFree(p->d_prof);
     delete p;
     return 0;
 }
@@ -1082,6 +1720,66 @@ int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t fwd_gen_coeffs)
     return 0;
 }
 
+int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
+{
+    if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12)) return RDQ_E_INVALID;
+    if (p->persist != mode) {
+        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+        p->cache.clear();
+    }
+    p->persist = mode;
+    return 0;
+}
+
+int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[4])
+{
+    if (!p || !out || B < 1) return RDQ_E_INVALID;
+    out[0] = persistent_nw(p, B, false);
+    out[1] = persistent_nw(p, B, true);
+    out[2] = p->fwd_T;
+    out[3] = p->adj_T;
+    return 0;
+}
+
+int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
+{
+    if (!p) return RDQ_E_INVALID;
+    for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);   // graphs bake the pointer in
+    p->cache.clear();
+    if (enable && !p->d_prof) {
+        RDQ_CHECK(hipMalloc(&p->d_prof, 8 * sizeof(unsigned long long)));
+        RDQ_CHECK(hipMemset(p->d_prof, 0, 8 * sizeof(unsigned long long)));
+    } else if (!enable && p->d_prof) {
+        RDQ_CHECK(hipFree(p->d_prof));
+        p->d_prof = nullptr;
+    }
+    return 0;
+}
+
+int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[8])
+{
+    if (!p || !out) return RDQ_E_INVALID;
+    if (!p->d_prof) { for (int i = 0; i < 8; ++i) out[i] = 0; return 0; }
+    RDQ_CHECK(hipDeviceSynchronize());
+    RDQ_CHECK(hipMemcpy(out, p->d_prof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    RDQ_CHECK(hipMemset(p->d_prof, 0, 8 * sizeof(unsigned long long)));
+    return 0;
+}
+
+int rdq_fwi_status(rdq_fwi_plan *p, hipStream_t st)
+{
+    if (!p) return RDQ_E_INVALID;
+    unsigned v = 0;
+    RDQ_CHECK(hipMemcpyAsync(&v, p->d_status, sizeof(v), hipMemcpyDeviceToHost, st));
+    RDQ_CHECK(hipStreamSynchronize(st));
+    if (v) {
+        RDQ_CHECK(hipMemsetAsync(p->d_status, 0, sizeof(v), st));
+        RDQ_CHECK(hipStreamSynchronize(st));
+        return RDQ_E_HANDOFF;
+    }
+    return 0;
+}
+
 int rdq_fwi_sizes(const rdq_fwi_plan *p, int32_t B, rdq_fwi_sizes_t *o)
 {
     if (!p || !o || B < 1) return RDQ_E_INVALID;
@@ -1091,7 +1789,7 @@ int rdq_fwi_sizes(const rdq_fwi_plan *p, int32_t B, rdq_fwi_sizes_t *o)
     o->vstat = (size_t)B * (sizeof(float) + sizeof(int64_t)) + 16;
     o->seis = (size_t)B * ns * p->nrec * p->g.ng * sizeof(float);
     o->history = (size_t)(p->g.nt + 2) * B * ns * slice * sizeof(float);
-    o->ring = 4 * (size_t)B * ns * slice * sizeof(float);
+    o->ring = 4 * (size_t)B * ns * slice * sizeof(unsigned long long);
     o->gA = (size_t)B * ns * slice * sizeof(float);
     o->gk_part = (size_t)B * ns * adj_blocks(p) * sizeof(double);
     o->gbeta = (size_t)B * ns * sizeof(float);
@@ -1135,6 +1833,11 @@ int rdq_fwi_forward(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, floa
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !seis || (!hist && !ring) || B < 1) return RDQ_E_INVALID;
+    if (const int nw = persistent_nw(p, B, false)) {
+        if (!ring) return RDQ_E_INVALID;   // the persistent kernel's hand-off granules live in `ring`
+        return run_cached(p, (hist ? 3 : 4) + 16 * nw, B, {coeffs, seis, hist, ring}, st,
+                          [&](hipStream_t s) { return launch_forward_pt(p, B, nw, coeffs, seis, hist, ring, s); });
+    }
     return run_cached(p, hist ? 0 : 1, B, {coeffs, seis, hist, ring}, st,
                       [&](hipStream_t s) { return launch_forward(p, B, coeffs, seis, hist, ring, s); });
 }
@@ -1144,6 +1847,10 @@ int rdq_fwi_adjoint(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, cons
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !hist || !dseis || !ring || !gA || !gk || !gbeta || B < 1) return RDQ_E_INVALID;
+    if (const int nw = persistent_nw(p, B, true))
+        return run_cached(p, 5 + 16 * nw, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
+            return launch_adjoint_pt(p, B, nw, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
+        });
     return run_cached(p, 2, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
         return launch_adjoint(p, B, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
     });

@@ -1,0 +1,191 @@
+// loop.hip — the inversion loop's serial tail on the MI355X (C ABI: include/red_diffeq_loop.h).
+//
+// K11 fused Adam + clamp: one pass over mu (B x 72 x 72) instead of the ~8 foreach launches of
+//     torch.optim.Adam plus the clamp (reference red_diffeq/core/inversion.py:87-90).
+// K12 fused metrics: MAE, RMSE and SSIM of every model from 32 x 32 output tiles (LDS-staged
+//     halo-5 input tile, separable 11-tap Gaussian on the five SSIM moments), per-tile partial sums
+//     reduced in a fixed order by a second launch; results stay on the device, so the loop needs
+//     no per-iteration host sync (reference red_diffeq/core/metrics.py:13-46, utils/ssim.py:19-65).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "red_diffeq_loop.h"
+
+namespace {
+
+#define RDQ_CHECK(x)                                   \
+    do {                                               \
+        hipError_t e_ = (x);                           \
+        if (e_ != hipSuccess) return -(int)e_;         \
+    } while (0)
+constexpr int RDQ_E_INVALID = -10001;
+
+__global__ __launch_bounds__(256) void k_adam(int64_t n, float *__restrict__ p, const float *__restrict__ g,
+                                              float *__restrict__ m, float *__restrict__ v, float beta1, float beta2,
+                                              float eps, float step_size, float bc2_sqrt, int clamp, float lo, float hi)
+{
+    const float w = 1.0f - beta1, omb2 = 1.0f - beta2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        float mi = m[i];
+        mi = (fabsf(w) < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.0f - w);   // torch lerp
+        float vi = v[i] * beta2;
+        vi = vi + omb2 * gi * gi;                                                      // addcmul
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        float pi = p[i] + step_size * (mi / denom);                                    // addcdiv
+        if (clamp) pi = fminf(fmaxf(pi, lo), hi);
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi;
+    }
+}
+
+// ---------------------------------------------------------------------------------------- K12
+constexpr int MT = 32, WIN = 11, HALO = WIN / 2, IT = MT + 2 * HALO;   // 42 x 42 input tile
+constexpr int NPART = 5;   // |d|, d^2, ssim-map sum (+2 spare for alignment)
+
+struct MetArgs {
+    int B, H, W, tiles_x, ntiles;
+    const float *pred;
+    int64_t s0, s2, s3;
+    const float *tru;
+    double *part;          // [B][ntiles][NPART]
+    float *out;            // [3][B]
+    float win[WIN];        // 1-D Gaussian (fp32, normalised as in ssim.py:gaussian)
+};
+
+__global__ __launch_bounds__(256) void k_metrics_tile(MetArgs a)
+{
+    __shared__ float xa[IT][IT], xb[IT][IT];
+    __shared__ float hz[5][IT][MT];
+    __shared__ double red[2][256];
+    __shared__ double rsm[256];
+    const int b = blockIdx.y, tile = blockIdx.x;
+    const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+    const int y0 = ty * MT - HALO, x0 = tx * MT - HALO;
+    const int tid = threadIdx.x;
+    double sad = 0.0, ssq = 0.0;
+    for (int i = tid; i < IT * IT; i += 256) {
+        const int r = i / IT, c = i - r * IT;
+        const int y = y0 + r, x = x0 + c;
+        float p = 0.0f, t = 0.0f;
+        if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
+            const float pv = a.pred[b * a.s0 + y * a.s2 + x * a.s3];
+            const float tv = a.tru[((size_t)b * a.H + y) * a.W + x];
+            p = (pv + 1.0f) / 2.0f;                    // metrics.py: (x + 1) / 2
+            t = (tv + 1.0f) / 2.0f;
+            // MAE / RMSE on the tile's own outputs (normalised units)
+            if (r >= HALO && r < HALO + MT && c >= HALO && c < HALO + MT) {
+                const float d = pv - tv;
+                sad += (double)fabsf(d);
+                ssq += (double)(d * d);
+            }
+        }
+        xa[r][c] = p;
+        xb[r][c] = t;
+    }
+    __syncthreads();
+    // horizontal pass: 5 moments on IT rows x MT output columns
+    for (int i = tid; i < IT * MT; i += 256) {
+        const int r = i / MT, c = i - r * MT;
+        float s1 = 0.f, s2 = 0.f, s11 = 0.f, s22 = 0.f, s12 = 0.f;
+#pragma unroll
+        for (int k = 0; k < WIN; ++k) {
+            const float u = xa[r][c + k], v = xb[r][c + k], w = a.win[k];
+            s1 += w * u; s2 += w * v; s11 += w * (u * u); s22 += w * (v * v); s12 += w * (u * v);
+        }
+        hz[0][r][c] = s1; hz[1][r][c] = s2; hz[2][r][c] = s11; hz[3][r][c] = s22; hz[4][r][c] = s12;
+    }
+    __syncthreads();
+    double sm = 0.0;
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    for (int i = tid; i < MT * MT; i += 256) {
+        const int r = i / MT, c = i - r * MT;
+        const int y = ty * MT + r, x = tx * MT + c;
+        if (y >= a.H || x >= a.W) continue;
+        float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+        for (int k = 0; k < WIN; ++k) {
+            const float w = a.win[k];
+            m1 += w * hz[0][r + k][c]; m2 += w * hz[1][r + k][c]; e11 += w * hz[2][r + k][c];
+            e22 += w * hz[3][r + k][c]; e12 += w * hz[4][r + k][c];
+        }
+        const float mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
+        const float s1 = e11 - mu1_sq, s2 = e22 - mu2_sq, s12 = e12 - mu12;
+        const float v = ((2.0f * mu12 + C1) * (2.0f * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2));
+        sm += (double)v;
+    }
+    red[0][tid] = sad; red[1][tid] = ssq; rsm[tid] = sm;
+    __syncthreads();
+    for (int w2 = 128; w2 > 0; w2 >>= 1) {
+        if (tid < w2) { red[0][tid] += red[0][tid + w2]; red[1][tid] += red[1][tid + w2]; rsm[tid] += rsm[tid + w2]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        double *o = a.part + ((size_t)b * a.ntiles + tile) * NPART;
+        o[0] = red[0][0]; o[1] = red[1][0]; o[2] = rsm[0];
+    }
+}
+
+__global__ void k_metrics_final(MetArgs a)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int t = 0; t < a.ntiles; ++t) {
+        const double *o = a.part + ((size_t)b * a.ntiles + t) * NPART;
+        s0 += o[0]; s1 += o[1]; s2 += o[2];
+    }
+    const double n = (double)a.H * a.W;
+    a.out[b] = (float)(s0 / n);
+    a.out[a.B + b] = (float)std::sqrt(s1 / n);
+    a.out[2 * a.B + b] = (float)(s2 / n);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rdq_adam_step(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq, float beta1,
+                  float beta2, float eps, float step_size, float bc2_sqrt, int32_t clamp, float lo, float hi,
+                  hipStream_t stream)
+{
+    if (n < 1 || !param || !grad || !exp_avg || !exp_avg_sq) return RDQ_E_INVALID;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, stream, n, param, grad, exp_avg, exp_avg_sq, beta1,
+                       beta2, eps, step_size, bc2_sqrt, clamp, lo, hi);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+size_t rdq_metrics_ws_bytes(int32_t B, int32_t H, int32_t W)
+{
+    if (B < 1 || H < 1 || W < 1) return 0;
+    const size_t nt = (size_t)((H + MT - 1) / MT) * ((W + MT - 1) / MT);
+    return (size_t)B * nt * NPART * sizeof(double);
+}
+
+int rdq_metrics(int32_t B, int32_t H, int32_t W, const float *pred, const int64_t strides[4], const float *true_norm,
+                float *out, void *ws, hipStream_t stream)
+{
+    if (B < 1 || H < 1 || W < 1 || !pred || !strides || !true_norm || !out || !ws) return RDQ_E_INVALID;
+    MetArgs a;
+    a.B = B; a.H = H; a.W = W;
+    a.tiles_x = (W + MT - 1) / MT;
+    a.ntiles = a.tiles_x * ((H + MT - 1) / MT);
+    a.pred = pred; a.s0 = strides[0]; a.s2 = strides[2]; a.s3 = strides[3];
+    a.tru = true_norm; a.part = (double *)ws; a.out = out;
+    // ssim.py:gaussian: float32 exp(-(x - 5)^2 / (2 sigma^2)), normalised by its float32 sum
+    float g[WIN], sum = 0.0f;
+    for (int k = 0; k < WIN; ++k) { g[k] = (float)std::exp(-(double)((k - HALO) * (k - HALO)) / (2.0 * 1.5 * 1.5)); }
+    for (int k = 0; k < WIN; ++k) sum += g[k];
+    for (int k = 0; k < WIN; ++k) a.win[k] = g[k] / sum;
+    hipLaunchKernelGGL(k_metrics_tile, dim3(a.ntiles, B), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_metrics_final, dim3((B + 63) / 64), dim3(64), 0, stream, a);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -46,6 +46,11 @@ SIGNATURES = {
     "rdq_fwi_set_graphs": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_tuning": (c_int32, [c_void_p, c_int32, c_int32, c_int32]),
     "rdq_fwi_set_variant": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_set_persistent": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_status": (c_int32, [c_void_p, c_void_p]),
+    "rdq_fwi_set_profile": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_launch_info": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_int32)]),
+    "rdq_fwi_read_profile": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "rdq_fwi_coeffs": (c_int32, [c_void_p, c_int32, c_void_p, ctypes.POINTER(c_int64), c_int32,
                                  c_void_p, c_void_p, c_void_p]),
     "rdq_fwi_forward": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -80,6 +85,12 @@ SIGNATURES = {
                                    c_void_p]),
     "rdq_red_epilogue": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
+    # include/red_diffeq_loop.h
+    "rdq_adam_step": (c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float,
+                                c_float, c_int32, c_float, c_float, c_void_p]),
+    "rdq_metrics_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_metrics": (c_int32, [c_int32, c_int32, c_int32, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p, c_void_p,
+                              c_void_p]),
 }
 
 

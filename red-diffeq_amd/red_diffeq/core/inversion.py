@@ -19,9 +19,10 @@ from tqdm.auto import tqdm
 
 from ..regularization.base import RegularizationMethod
 from ..utils.data_trans import add_noise_to_seismic, missing_trace
+from ..utils.data_trans import v_normalize
 from ..utils.ssim import SSIM
+from .fused import CosineLR, FusedAdamClamp, metrics as fused_metrics
 from .losses import LossCalculator
-from .metrics import MetricsCalculator
 
 
 class _GradAllReduce(torch.autograd.Function):
@@ -84,11 +85,15 @@ class InversionEngine:
         B = mu.shape[0]
         mu = mu.float().clone().detach().to(self.device).requires_grad_(True)
         mu_true = mu_true.float().to(self.device)
-        optimizer = torch.optim.Adam([mu], lr=lr)
-        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=ts, eta_min=0.0)
-        metrics_calc = MetricsCalculator(self.ssim_loss)
+        # K11: Adam + clamp in one HIP pass; the cosine schedule is a host scalar (no sync)
+        optimizer = FusedAdamClamp(mu, lr=lr, clamp=(-1.0, 1.0))
+        scheduler = CosineLR(lr, T_max=ts, eta_min=0.0)
+        true_norm = v_normalize(mu_true).contiguous()           # metrics.py:24, loop-invariant
         loss_calc = LossCalculator(self.regularization_method)
-        hist = {k: [] for k in ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")}
+        keys = ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")
+        # per-iteration histories stay on the device; ONE copy to the host after the loop (the
+        # reference syncs six times per iteration, inversion.py:97-111)
+        hist_dev = torch.zeros(ts, len(keys), B, dtype=torch.float32, device=self.device)
 
         y = add_noise_to_seismic(y, noise_std, noise_type=noise_type, generator=None)
         y, mask = missing_trace(y, missing_number, return_mask=True, generator=None)
@@ -109,7 +114,7 @@ class InversionEngine:
             mask = None
 
         pbar = tqdm(range(ts), desc="Optimizing", unit="step", disable=not self.show_progress)
-        for _ in pbar:
+        for it in pbar:
             if regularization == "diffusion":
                 noise_x0 = torch.randn(mu.shape, device=mu.device, dtype=mu.dtype)
                 x0_pred = mu + self.regularization_method.sigma_x0 * noise_x0
@@ -123,32 +128,31 @@ class InversionEngine:
             reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
             total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
 
-            optimizer.zero_grad(set_to_none=True)
+            optimizer.zero_grad()
             total_loss.sum().backward()
-            optimizer.step()
-            with torch.no_grad():
-                mu.data.clamp_(-1, 1)
-            scheduler.step()
+            optimizer.step()                       # + clamp_(-1, 1), inversion.py:87-90
+            optimizer.lr = scheduler.step()
 
-            mae, rmse, ssim = metrics_calc.calculate(mu[:, :, 1:-1, 1:-1], mu_true)
-            obs_log = loss_obs.detach()
-            if sharded:
-                obs_log = obs_log.clone()
-                dist.all_reduce(obs_log, group=process_group)
-            tot_log = obs_log + reg_lambda * reg_loss.detach()
-            hist["total_losses"].append(tot_log.cpu().numpy())
-            hist["obs_losses"].append(obs_log.cpu().numpy())
-            hist["reg_losses"].append(reg_loss.detach().cpu().numpy())
-            hist["ssim"].append(ssim.cpu().numpy())
-            hist["mae"].append(mae.cpu().numpy())
-            hist["rmse"].append(rmse.cpu().numpy())
+            with torch.no_grad():
+                row = hist_dev[it]
+                row[3:6] = fused_metrics(mu[:, :, 1:-1, 1:-1], true_norm)[[2, 0, 1]]   # ssim, mae, rmse
+                obs_log = loss_obs.detach()
+                if sharded:
+                    obs_log = obs_log.clone()
+                    dist.all_reduce(obs_log, group=process_group)
+                row[0] = obs_log + reg_lambda * reg_loss.detach()
+                row[1] = obs_log
+                row[2] = reg_loss.detach()
             if self.show_progress:
-                post = {"MAE": float(hist["mae"][-1].mean()), "RMSE": float(hist["rmse"][-1].mean()),
-                        "SSIM": float(hist["ssim"][-1].mean())}
+                h = row.cpu().numpy()
+                post = {"MAE": float(h[4].mean()), "RMSE": float(h[5].mean()), "SSIM": float(h[3].mean())}
                 if time_tensor is not None:
                     post["t"] = int(round(time_tensor.float().mean().item()))
                 pbar.set_postfix(post)
 
-        n = len(hist["total_losses"])
-        results = [{k: [hist[k][t][i] for t in range(n)] for k in hist} for i in range(B)]
+        check = getattr(fwi_forward, "check", None)   # persistent-kernel hand-off status (one sync)
+        if callable(check):
+            check()
+        H = hist_dev.cpu().numpy()
+        results = [{k: [H[t, j, i] for t in range(ts)] for j, k in enumerate(keys)} for i in range(B)]
         return mu[:, :, 1:-1, 1:-1], results

@@ -78,6 +78,36 @@ class FwiPlan:
     def set_variant(self, fwd_gen_coeffs):
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, int(bool(fwd_gen_coeffs))), "rdq_fwi_set_variant")
 
+    def set_persistent(self, enable):
+        _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, int(bool(enable))), "rdq_fwi_set_persistent")
+
+    def status(self, stream=None):
+        """Synchronise and raise if a persistent launch's neighbour hand-off timed out."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        _hip.check(self.lib.rdq_fwi_status(self.handle, ctypes.c_void_p(stream)), "rdq_fwi_status")
+
+    def launch_info(self, B):
+        """{'fwd_persistent', 'adj_persistent', 'fwd_T', 'adj_T'} of a call with batch B."""
+        out = (ctypes.c_int32 * 4)()
+        _hip.check(self.lib.rdq_fwi_launch_info(self.handle, int(B), out), "rdq_fwi_launch_info")
+        return {"fwd_persistent": bool(out[0]), "adj_persistent": bool(out[1]), "fwd_T": int(out[2]),
+                "adj_T": int(out[3])}
+
+    def set_profile(self, enable):
+        _hip.check(self.lib.rdq_fwi_set_profile(self.handle, int(bool(enable))), "rdq_fwi_set_profile")
+
+    def read_profile(self):
+        """Per-wave average phase times (us) of the persistent kernels since the last read."""
+        out = (ctypes.c_uint64 * 8)()
+        _hip.check(self.lib.rdq_fwi_read_profile(self.handle, out), "rdq_fwi_read_profile")
+        res = {}
+        for name, o in (("fwd", 0), ("adj", 4)):
+            n = max(int(out[o + 3]), 1)
+            res[name] = {"wait_us": out[o] / n / 100.0, "steps_us": out[o + 1] / n / 100.0,
+                         "publish_us": out[o + 2] / n / 100.0, "waves": int(out[o + 3])}
+        return res
+
     def set_tuning(self, fwd_steps, adj_steps, chains=1):
         _hip.check(self.lib.rdq_fwi_set_tuning(self.handle, int(fwd_steps), int(adj_steps), int(chains)),
                    "rdq_fwi_set_tuning")
@@ -110,7 +140,7 @@ class FwiPlan:
         sz = self.sizes(B)
         seis = torch.empty(B, self.ns, sz.nrec, self.ng, dtype=torch.float32, device=self.device)
         hist = self._f32(sz.history) if keep_history else None
-        ring = None if keep_history else self._f32(sz.ring)
+        ring = self._f32(sz.ring)
         _hip.check(self.lib.rdq_fwi_forward(self.handle, B, _hip.ptr(coeffs), _hip.ptr(seis),
                                             _hip.ptr(hist), _hip.ptr(ring), _hip.stream_of(coeffs)),
                    "rdq_fwi_forward")
@@ -244,6 +274,12 @@ class FWIForward(nn.Module):
         plan = self._plan(v.shape[2], v.shape[3], v.device)
         s = _FWIFunction.apply(v, plan, vel_mode)
         return self.s_norm_func(s) if self.normalize else s
+
+    def check(self):
+        """Raise if a persistent kernel's neighbour hand-off timed out since the last check
+        (synchronises the current stream)."""
+        for plan in self._plans.values():
+            plan.status()
 
     def coefficients(self, v):
         """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""

@@ -31,22 +31,27 @@ def bits_equal(a, b):
     return a.shape == b.shape and np.array_equal(a.view(np.int32), b.view(np.int32))
 
 
-@pytest.mark.parametrize("graphs,steps,chains", [(True, 1, 1), (True, 2, 1), (True, 3, 2), (True, 4, 1), (True, 4, 3),
-                                                 (False, 3, 2)])
+@pytest.mark.parametrize("graphs,steps,chains,persist", [
+    (True, 1, 1, True), (True, 2, 1, True), (True, 3, 1, True), (True, 4, 1, True), (False, 4, 1, True),
+    (True, 1, 1, False), (True, 3, 2, False), (True, 4, 3, False), (False, 3, 2, False)])
 @pytest.mark.parametrize("name,kw", FWD)
-def test_forward_bitexact_vs_reference(cuda, name, kw, graphs, steps, chains):
-    """Every temporal-blocking depth (time steps per launch) and both launch modes."""
+def test_forward_bitexact_vs_reference(cuda, name, kw, graphs, steps, chains, persist):
+    """Every temporal-blocking depth, persistent (one launch, epoch hand-offs) and chunked
+    (one launch per T steps) kernels, graph and direct launches."""
     z = load_golden(name)
     fwi = make_fwi(ctx_of(z), **kw)
     v = torch.from_numpy(vnorm(z["v"])).to(cuda)
     plan = fwi._plan(v.shape[2], v.shape[3], v.device)
     plan.set_graphs(graphs)
     plan.set_tuning(steps, steps, chains)
-    plan.set_variant(steps % 2 == 0)          # both coefficient sources
+    plan.set_persistent(persist)
+    plan.set_variant(steps % 2 == 0)          # both coefficient sources (chunked kernels)
     with torch.no_grad():
         seis = fwi(v).cpu().numpy()                    # no-grad: ring path
+    plan.status()
     assert bits_equal(seis, z["seis"]), np.abs(seis - z["seis"]).max()
     seis_h = fwi(v.clone().requires_grad_(True)).detach().cpu().numpy()   # store-all history path
+    plan.status()
     assert bits_equal(seis_h, z["seis"])
 
 
@@ -86,10 +91,11 @@ def test_gradient_vs_reference_autograd(cuda, name):
     assert np.linalg.norm(g - go) / np.linalg.norm(go) < 1e-6
 
 
-@pytest.mark.parametrize("steps,chains", [(1, 1), (2, 2), (3, 1), (4, 3)])
+@pytest.mark.parametrize("steps,chains,persist", [(1, 1, True), (2, 1, True), (3, 1, True), (4, 1, True),
+                                                  (2, 2, False), (3, 1, False), (4, 3, False)])
 @pytest.mark.parametrize("name,kw", [("fwd_small", {}), ("fwd_small_st3", dict(sample_temporal=3, sample_spatial=0.5)),
                                      ("fwd_wrap", {}), ("fwd_openfwi_ns5_nt400", {})])
-def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains):
+def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains, persist):
     z = load_golden(name)
     ctx = ctx_of(z)
     fwi = make_fwi(ctx, **kw)
@@ -98,6 +104,7 @@ def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains):
     B = v.shape[0]
     plan = fwi._plan(v.shape[2], v.shape[3], v.device)
     plan.set_tuning(steps, steps, chains)
+    plan.set_persistent(persist)
     sz = plan.sizes(B)
     rng = np.random.default_rng(1)
     dseis = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
@@ -105,7 +112,7 @@ def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains):
     seis, hist = plan.forward(coeffs, B, keep_history=True)
     gA, gk, gb = plan.adjoint(coeffs, hist, torch.from_numpy(dseis).to(cuda), B)
     g = plan.finalize(coeffs, vstat, gA, gk, gb, B, 0).cpu().numpy()
-    torch.cuda.synchronize()
+    plan.status()
     f = O.OracleFWI(ctx, B, **kw)
     _, c = f.forward(vn, keep_history=True)
     oA, oK, ob = f.adjoint(c, dseis)
@@ -125,6 +132,50 @@ def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains):
         assert bits_equal(cf[k].cpu().numpy(), c[k]), k
     vm = vstat[:4 * B].view(torch.float32).cpu().numpy()
     assert bits_equal(vm, c["vmin"])
+
+
+@pytest.mark.parametrize("steps", [1, 3, 4])
+def test_persistent_partial_edge_tiles_vs_oracle(cuda, steps):
+    """Persistent kernels on a grid whose last tile column/row is narrower than the halo
+    (Hp = 2*48 + 4, Wp = 2*48 + 8 at T = 4): forward bit-exact, adjoint gA/gbeta bit-exact vs the
+    oracle, persistent == chunked."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=84, nt=160, dx=10.0, dt=0.001, nbc=10, f=15.0, sz=10, gz=10, ng=84, ns=3)
+    vphys = make_model("curvefault", 80, 84, seed=21, batch=2)
+    vn = vnorm(vphys)
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vn).to(cuda)
+    plan = fwi._plan(80, 84, v.device)
+    plan.set_tuning(steps, steps, 1)
+    B = 2
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(5)
+    dseis = torch.from_numpy(rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)).to(cuda)
+    out = {}
+    for persist in (True, False):
+        plan.set_persistent(persist)
+        coeffs, vstat = plan.coeffs(v, 0)
+        seis, hist = plan.forward(coeffs, B, keep_history=True)
+        gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+        plan.status()
+        out[persist] = (seis.cpu().numpy(), gA.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy(),
+                        gb.cpu().numpy(), gk.view(B, -1).sum(1).cpu().numpy())
+    for a, b in zip(out[True], out[False]):
+        if a.dtype == np.float32:
+            assert bits_equal(a, b)
+        else:
+            np.testing.assert_allclose(a, b, rtol=1e-12)
+    f = O.OracleFWI(dict(ctx), B)
+    so, c = f.forward(vn, keep_history=True)
+    assert bits_equal(out[True][0], so)
+    oA, oK, ob = f.adjoint(c, dseis.cpu().numpy())
+    gAs = out[True][1]
+    gA = gAs[:, 0].copy()
+    for s in range(1, plan.ns):
+        gA = gA + gAs[:, s]
+    assert bits_equal(gA, oA)
+    assert bits_equal(out[True][2].reshape(B, -1), ob)
+    np.testing.assert_allclose(out[True][3], oK, rtol=1e-7)
 
 
 def test_damp_profile_vs_reference(cuda):

@@ -134,3 +134,17 @@ def test_synthetic_models_in_range():
     for fam in ("flatvel", "curvevel", "curvefault"):
         v = make_model(fam, 70, 70, seed=8888, batch=2)
         assert v.shape == (2, 1, 70, 70) and v.min() >= 1500 and v.max() <= 4500
+
+
+def test_cosine_lr_matches_torch_scheduler():
+    """Host-side CosineAnnealingLR restatement used by the fused loop (inversion.py:81)."""
+    from red_diffeq.core.fused import CosineLR
+    for T, steps in ((300, 310), (7, 40)):
+        p = torch.zeros(1, requires_grad=True)
+        opt = torch.optim.SGD([p], lr=0.03)
+        sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=T, eta_min=0.0)
+        mine = CosineLR(0.03, T_max=T)
+        for _ in range(steps):
+            opt.step()
+            sch.step()
+            assert mine.step() == opt.param_groups[0]["lr"]

@@ -19,6 +19,8 @@ ap.add_argument("--B", type=int, default=1)
 ap.add_argument("--nt", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only", type=int, default=0, help="run a single blocking depth")
+ap.add_argument("--chunked", action="store_true", help="also time the chunked (launch per T steps) kernels")
+ap.add_argument("--profile", action="store_true", help="phase counters of the persistent kernels")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = dict(n_grid=70, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=a.ns)
@@ -28,11 +30,13 @@ plan = fwi._plan(70, 70, dev)
 sz = plan.sizes(a.B)
 dseis = torch.randn(a.B, a.ns, sz.nrec, plan.ng, device=dev)
 res = []
-cfgs = [(a.only, 0)] if a.only else [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (2, 1), (3, 1), (4, 1)]
+# (T, persistent)
+cfgs = [(a.only, 1)] if a.only else [(1, 1), (2, 1), (3, 1), (4, 1)]
+if a.chunked:
+    cfgs += [(T, 0) for T in (2, 3, 4)]
 for T, G in cfgs:
-    C = 1
-    plan.set_tuning(T, T, C)
-    plan.set_variant(G)
+    plan.set_tuning(T, T, 1)
+    plan.set_persistent(G)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     fw, ad = [], []
     for i in range(a.reps + 1):
@@ -47,7 +51,17 @@ for T, G in cfgs:
             fw.append(ev[0].elapsed_time(ev[1]))
             ad.append(ev[1].elapsed_time(ev[2]))
         del hist
+    plan.status()
     fw, ad = sorted(fw)[len(fw) // 2], sorted(ad)[len(ad) // 2]
-    res.append({"T": T, "gen": G, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
+    res.append({"T": T, "persistent": G, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
                 "shot_ts_per_s": round(a.ns * a.nt * a.B / ((fw + ad) * 1e-3))})
+    if a.profile and G:
+        plan.set_profile(1)
+        coeffs, vstat = plan.coeffs(v, 0)
+        seis, hist = plan.forward(coeffs, a.B, keep_history=True)
+        plan.adjoint(coeffs, hist, dseis, a.B)
+        prof = plan.read_profile()
+        plan.set_profile(0)
+        del hist
+        res[-1]["profile_us_per_wave"] = {k: {kk: round(vv, 1) for kk, vv in d.items()} for k, d in prof.items()}
     print(json.dumps(res[-1]), flush=True)
