@@ -102,6 +102,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
+    from red_diffeq.core.fused import CosineLR, FusedAdamClamp
     from red_diffeq.core.inversion import grad_all_reduce
     from red_diffeq.core.losses import l1_misfit
     from red_diffeq.regularization.benchmark import total_variation_loss
@@ -120,8 +121,8 @@ def main():
         y = fwi(v_normalize(vt).to(dev))                         # observed data, local shots
     mu0 = torch.cat([prepare_initial_model(vt[i:i + 1], "smoothed", sigma=10.0) for i in range(B)])
     mu = torch.nn.functional.pad(mu0, (1, 1, 1, 1)).to(dev).requires_grad_(True)
-    opt = torch.optim.Adam([mu], lr=0.03)
-    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=300, eta_min=0.0)
+    opt = FusedAdamClamp(mu, lr=0.03, clamp=(-1.0, 1.0))       # K11: Adam + clamp, one pass
+    sched = CosineLR(0.03, T_max=300, eta_min=0.0)
     nobs = torch.full((B,), float(ns_tot * nt * 70), device=dev) if world > 1 else None
     lam = 0.01
 
@@ -130,12 +131,10 @@ def main():
         if world > 1:
             v_in = grad_all_reduce(v_in)
         loss = l1_misfit(fwi(v_in), y, None, nobs) + lam * total_variation_loss(mu)
-        opt.zero_grad(set_to_none=True)
+        opt.zero_grad()
         loss.sum().backward()
-        opt.step()
-        with torch.no_grad():
-            mu.data.clamp_(-1, 1)
-        sched.step()
+        opt.step()                                              # + clamp_(-1, 1)
+        opt.lr = sched.step()
 
     for _ in range(a.warmup):
         step()

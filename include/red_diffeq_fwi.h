@@ -77,9 +77,15 @@ int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
  * 1..4) and the number of concurrent shot-group launch chains (1..16).  Results are identical
  * for every setting; only speed changes. */
 int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
-/* Kernel variant: 1 = the forward regenerates alpha/temp1/temp2 from the 20 KB model in
- * registers instead of loading the three K3 fields (identical results). */
-int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t fwd_gen_coeffs);
+/* Kernel variant flags (default 0):
+ *   RDQ_VARIANT_FWD_GEN    the chunked forward regenerates alpha/temp1/temp2 from the 20 KB model in
+ *                          registers instead of loading the three K3 fields (identical results);
+ *   RDQ_VARIANT_ADJ_EXACT  the persistent adjoint keeps the oracle's exact fp32 operation order (gA
+ *                          bit-identical to oracle/fwi_oracle.c) instead of contracting into FMAs and
+ *                          accumulating the sponge term per cell in fp32 (faster; within 1e-6). */
+#define RDQ_VARIANT_FWD_GEN 1
+#define RDQ_VARIANT_ADJ_EXACT 2
+int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the
  * device, with 64 x 96 regions if they fit, else 64 x 64; 12 / 8 = only that region height;
@@ -97,6 +103,9 @@ int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[4]);
  * out[0..3] forward {hand-off wait, time steps, publish, waves}, out[4..7] the same for the adjoint. */
 int rdq_fwi_set_profile(rdq_fwi_plan *plan, int32_t enable);
 int rdq_fwi_read_profile(rdq_fwi_plan *plan, uint64_t out[8]);
+/* Per-wave records of the last read_profile: out[(block * 16 + wave) * 3 + {0,1,2}] = {hand-off,
+ * steps, publish} ticks of the forward (adj = 0) or adjoint (adj = 1) kernel. */
+int rdq_fwi_profile_waves(rdq_fwi_plan *plan, int32_t adj, uint64_t *out, size_t count);
 
 /* Velocity input convention of rdq_fwi_coeffs / rdq_fwi_grad_finalize. */
 #define RDQ_VEL_NORMALIZED 0  /* v_norm in [-1,1], denormalised in-kernel: (v+1)/2*3000+1500 */

@@ -587,7 +587,10 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 //
 // Granule buffer (inside the caller's `ring`): [2 epoch parity][2 level][B][ns][Hp][ld] u64,
 // zeroed before each launch; tag = epoch index (>= 1) so a zeroed granule never matches.
-constexpr int CP_SC1 = 16;                           // buffer cache policy: sc1 (write-through / L1 bypass)
+constexpr int CP_SC1 = 16;
+constexpr size_t PROF_RAW = 8;                        // per-wave records after the 4 summary words
+constexpr size_t PROF_WAVES = 4096 * 16;              // blocks x waves recorded
+constexpr size_t PROF_WORDS = PROF_RAW + PROF_WAVES * 3;   // per kernel (fwd, then adj)                           // buffer cache policy: sc1 (write-through / L1 bypass)
 constexpr unsigned long long PT_TIMEOUT_TICKS = 20000000ull;   // 200 ms of s_memrealtime (100 MHz)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int bytes = 0x7fffffff)
@@ -849,6 +852,10 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+        if (blockIdx.x < PROF_WAVES / 16) {
+            unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
+            raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
+        }
     }
 }
 #undef FWD_STEP
@@ -891,9 +898,14 @@ struct AdjPtArgs {
             const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                                   \
             float n1 = qm1 + qp1; n1 = n1 + xl1; n1 = n1 + xr1;                                     \
             float n2 = qm2 + qp2; n2 = n2 + xl2; n2 = n2 + xr2;                                     \
-            float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;                           \
-            float l = T1v[r] * CUR[r]; const float l2 = T2v[r] * PRV[r]; l = l - l2; l = l + nb;    \
-            PRV[r] = l;                                                                             \
+            if constexpr (FMA) {                                                                    \
+                const float nb = __builtin_fmaf(C3, n2, C2 * n1);                                   \
+                PRV[r] = __builtin_fmaf(T1v[r], CUR[r], __builtin_fmaf(-T2v[r], PRV[r], nb));       \
+            } else {                                                                                \
+                float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;                       \
+                float l = T1v[r] * CUR[r]; const float l2 = T2v[r] * PRV[r]; l = l - l2; l = l + nb; \
+                PRV[r] = l;                                                                         \
+            }                                                                                       \
         }                                                                                           \
         if (rmask && ((k - 1) % g.st) == 0) {        /* uniform: receiver row waves */             \
             unsigned rm_ = rmask;                                                                   \
@@ -917,13 +929,20 @@ struct AdjPtArgs {
                 const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                               \
                 float s1 = P[r + 1] + P[r + 3]; s1 = s1 + xl1; s1 = s1 + xr1;                       \
                 float s2 = P[r] + P[r + 4]; s2 = s2 + xl2; s2 = s2 + xr2;                           \
-                float lap = C2 * s1; const float lq = C3 * s2; lap = lap + lq;                      \
-                float d = C1X2 * pc; d = d + lap;                                                   \
                 const float l = PRV[r];                                                             \
-                const float c = l * d;                                                              \
-                GA[r] = GA[r] + c;                                                                  \
-                float kk = KP[r] * pc; const float dl = CUR[r] - l; kk = kk * dl;                   \
-                if (xin) ksum += (double)kk;                                                        \
+                if constexpr (FMA) {                                                                \
+                    const float lap = __builtin_fmaf(C3, s2, C2 * s1);                              \
+                    const float d = __builtin_fmaf(C1X2, pc, lap);                                  \
+                    GA[r] = __builtin_fmaf(l, d, GA[r]);                                            \
+                    GK[r] = __builtin_fmaf(pc, CUR[r] - l, GK[r]);   /* x K at the end */          \
+                } else {                                                                            \
+                    float lap = C2 * s1; const float lq = C3 * s2; lap = lap + lq;                  \
+                    float d = C1X2 * pc; d = d + lap;                                               \
+                    const float c = l * d;                                                          \
+                    GA[r] = GA[r] + c;                                                              \
+                    float kk = KP[r] * pc; const float dl = CUR[r] - l; kk = kk * dl;               \
+                    if (xin) ksum += (double)kk;                                                    \
+                }                                                                                   \
             }                                                                                       \
             if (smask) {                             /* gbeta: the source cell's lane only */      \
                 unsigned sm_ = smask;                                                               \
@@ -942,7 +961,7 @@ struct AdjPtArgs {
 // P_{k-1} comes from the history: each wave loads its interior rows +-2 (12 rows) one step ahead
 // into alternating register arrays (no copies, so the wait lands at the gradient, not at the
 // step's start) and needs no LDS exchange for it.
-template <int T, int NW>
+template <int T, int NW, bool FMA>
 __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 {
     constexpr int PR = TB_R + 4;
@@ -951,7 +970,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    float A[R], T1v[R], T2v[R], KP[R], L0[R], L1[R], GA[R];
+    float A[R], T1v[R], T2v[R], KP[R], L0[R], L1[R], GA[R], GK[R];
     unsigned smask = 0, rmask = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -959,7 +978,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         const int o = gz * g.ld + gx;
         A[r] = AL[o]; T1v[r] = AL[g.cstride + o]; T2v[r] = AL[2 * g.cstride + o]; KP[r] = AL[3 * g.cstride + o];
         L0[r] = 0.0f; L1[r] = 0.0f;                       // L_{nt+1} = L_{nt+2} = 0
-        GA[r] = 0.0f;
+        GA[r] = 0.0f; GK[r] = 0.0f;
         if (gz == g.isz && ((rin >> r) & 1u)) smask |= 1u << r;
         if (gz == g.igz) rmask |= 1u << r;
     }
@@ -1023,6 +1042,10 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 #undef DLOAD
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+        if (blockIdx.x < PROF_WAVES / 16) {
+            unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
+            raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
+        }
     }
     if (xin) {
 #pragma unroll
@@ -1030,6 +1053,13 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             if ((rin >> r) & 1u) a.gA[so + (size_t)PT_ROFS(r) + gx] = GA[r];
     }
     if (smask && scol) a.gbeta[bs] = gbacc;
+    if constexpr (FMA) {   // gk = sum K * (sum_k P (L_{k+1} - L_k)) over the own cells
+        if (xin) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if ((rin >> r) & 1u) ksum += (double)KP[r] * (double)GK[r];
+        }
+    }
     // deterministic workgroup reduction of the sponge-coefficient partial sum
     const int tid = threadIdx.x;
     red[tid] = ksum;
@@ -1068,20 +1098,20 @@ struct FinArgs {
 // replicate ix (F.pad replicate backward).  g_vpad is formed per point exactly as autograd
 // chains it: alpha = (v*dt/dx)^2 -> ((gA*(2*a1))/dx)*dt; beta = (v*dt)^2 at the sources;
 // the sponge term sum(gK*K)/vmin lands on the first argmin of the padded field.
+// One workgroup per padded row (z, b): every padded cell's d(loss)/d(v_pad) (fp64) into LDS, all
+// cells in parallel; then the replicate-pad fold along x: interior columns take their own cell,
+// the two edge columns sum their nbc+1-wide strips (one wave each, fixed-order shuffle tree).
+constexpr int FIN_MAXW = 4096;
 __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
 {
-    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
-    const int z = blockIdx.y, b = blockIdx.z;
-    if (ix >= p.nx) return;
-    const int x0 = ix == 0 ? 0 : ix + p.nbc;
-    const int x1 = ix == p.nx - 1 ? p.Wp : ix + p.nbc + 1;
+    __shared__ double gv_s[FIN_MAXW];
+    const int z = blockIdx.x, b = blockIdx.y;
     const size_t ro = (size_t)b * p.slice + (size_t)z * p.ld;
     const float *GA = p.gA + (size_t)b * p.ns * p.slice + (size_t)z * p.ld;   // [B][ns][Hp][ld]
     const float *V = p.coeffs + 5 * p.cstride + ro;
     const int amz = (int)(p.amin[b] / p.nx), amx = (int)(p.amin[b] - (int64_t)amz * p.nx);
     const int apz = amz == 0 ? 0 : amz + p.nbc, apx = amx == 0 ? 0 : amx + p.nbc;
-    double acc = 0.0;
-    for (int x = x0; x < x1; ++x) {
+    for (int x = threadIdx.x; x < p.Wp; x += blockDim.x) {
         float a1 = V[x] * p.dt; a1 = a1 / p.dx;
         float ga = 0.0f;
         for (int s = 0; s < p.ns; ++s) ga = ga + GA[(size_t)s * p.slice + x];   // shots in order
@@ -1100,12 +1130,23 @@ __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
             for (int j = 0; j < p.ns * p.nblk; ++j) gk += p.gk_part[(size_t)b * p.ns * p.nblk + j];
             gv += gk / (double)p.vmin[b];
         }
-        acc += gv;
+        gv_s[x] = gv;
     }
-    p.colsum[((size_t)b * p.Hp + z) * p.nx + ix] = acc;
+    __syncthreads();
+    double *CS = p.colsum + ((size_t)b * p.Hp + z) * p.nx;
+    for (int ix = 1 + threadIdx.x; ix < p.nx - 1; ix += blockDim.x) CS[ix] = gv_s[ix + p.nbc];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {   // wave 0: columns [0, nbc] -> ix 0; wave 1: [nbc+nx-1, Wp) -> ix nx-1
+        const int x0 = w == 0 ? 0 : p.nbc + p.nx - 1, x1 = w == 0 ? p.nbc + 1 : p.Wp;
+        double acc = 0.0;
+        for (int x = x0 + lane; x < x1; x += 64) acc += gv_s[x];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+        if (lane == 0) {
+            if (p.nx == 1) { if (w == 0) { double t2 = acc; for (int x = p.nbc + 1; x < p.Wp; ++x) t2 += gv_s[x]; CS[0] = t2; } }
+            else CS[w == 0 ? 0 : p.nx - 1] = acc;
+        }
+    }
 }
-
-// Stage 2: sum the replicated rows, scale by d(v)/d(v_norm) = 1500 (data_trans.py:15).
 __global__ __launch_bounds__(256) void k_fin_cols(FinArgs p)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1258,7 +1299,8 @@ struct rdq_fwi_plan {
     int *d_isx = nullptr, *d_rcv_start = nullptr, *d_rcv_list = nullptr;
     float *d_wav = nullptr;     // fp32 wavelet [nt] (persistent kernels)
     unsigned *d_status = nullptr;   // hand-off timeout word (rdq_fwi_status)
-    unsigned long long *d_prof = nullptr;   // phase counters (rdq_fwi_set_profile): fwd [0..3], adj [4..7]
+    unsigned long long *d_prof = nullptr;   // phase counters (rdq_fwi_set_profile): fwd, then adj
+    std::vector<unsigned long long> prof_host;
     bool graphs = true;
     int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves)
     int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
@@ -1266,6 +1308,7 @@ struct rdq_fwi_plan {
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = false;       // forward regenerates coefficients from the model (vs loading K3)
+    bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;
     std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins
@@ -1396,10 +1439,10 @@ int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
 {
     int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
     switch (T) {
-    case 1: return adj ? resident_capacity(k_adj_pt<1, NW>, 64 * NW, c[1]) : resident_capacity(k_fwd_pt<1, NW>, 64 * NW, c[1]);
-    case 2: return adj ? resident_capacity(k_adj_pt<2, NW>, 64 * NW, c[2]) : resident_capacity(k_fwd_pt<2, NW>, 64 * NW, c[2]);
-    case 3: return adj ? resident_capacity(k_adj_pt<3, NW>, 64 * NW, c[3]) : resident_capacity(k_fwd_pt<3, NW>, 64 * NW, c[3]);
-    default: return adj ? resident_capacity(k_adj_pt<4, NW>, 64 * NW, c[4]) : resident_capacity(k_fwd_pt<4, NW>, 64 * NW, c[4]);
+    case 1: return adj ? resident_capacity(k_adj_pt<1, NW, false>, 64 * NW, c[1]) : resident_capacity(k_fwd_pt<1, NW>, 64 * NW, c[1]);
+    case 2: return adj ? resident_capacity(k_adj_pt<2, NW, false>, 64 * NW, c[2]) : resident_capacity(k_fwd_pt<2, NW>, 64 * NW, c[2]);
+    case 3: return adj ? resident_capacity(k_adj_pt<3, NW, false>, 64 * NW, c[3]) : resident_capacity(k_fwd_pt<3, NW>, 64 * NW, c[3]);
+    default: return adj ? resident_capacity(k_adj_pt<4, NW, false>, 64 * NW, c[4]) : resident_capacity(k_fwd_pt<4, NW>, 64 * NW, c[4]);
     }
 }
 
@@ -1441,15 +1484,15 @@ void launch_fwd_pt(int T, dim3 grid, hipStream_t st, const FwdPtArgs &a)
     }
 }
 
-template <int NW>
+template <int NW, bool F>
 void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
 {
     const dim3 blk(64 * NW);
     switch (T) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, F>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, F>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, F>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F>), grid, blk, 0, st, a); break;
     }
 }
 
@@ -1493,10 +1536,10 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, const
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.dseis = dseis;
     a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
-    a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + 4 : nullptr;
+    a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + PROF_WORDS : nullptr;
     const dim3 grid(pt_grid(p, B, T, NW));
-    if (NW == 12) launch_adj_pt<12>(T, grid, st, a);
-    else launch_adj_pt<8>(T, grid, st, a);
+    if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
+    else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -1709,14 +1752,16 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     return 0;
 }
 
-int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t fwd_gen_coeffs)
+int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
-    if (!p) return RDQ_E_INVALID;
-    if (p->fwd_gen != (fwd_gen_coeffs != 0)) {
+    if (!p || (flags & ~3)) return RDQ_E_INVALID;
+    const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0, fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0;
+    if (p->fwd_gen != gen || p->adj_fma != fma) {
         for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
         p->cache.clear();
     }
-    p->fwd_gen = fwd_gen_coeffs != 0;
+    p->fwd_gen = gen;
+    p->adj_fma = fma;
     return 0;
 }
 
@@ -1747,8 +1792,8 @@ int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
     for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);   // graphs bake the pointer in
     p->cache.clear();
     if (enable && !p->d_prof) {
-        RDQ_CHECK(hipMalloc(&p->d_prof, 8 * sizeof(unsigned long long)));
-        RDQ_CHECK(hipMemset(p->d_prof, 0, 8 * sizeof(unsigned long long)));
+        RDQ_CHECK(hipMalloc(&p->d_prof, 2 * PROF_WORDS * sizeof(unsigned long long)));
+        RDQ_CHECK(hipMemset(p->d_prof, 0, 2 * PROF_WORDS * sizeof(unsigned long long)));
     } else if (!enable && p->d_prof) {
         RDQ_CHECK(hipFree(p->d_prof));
         p->d_prof = nullptr;
@@ -1761,8 +1806,20 @@ int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[8])
     if (!p || !out) return RDQ_E_INVALID;
     if (!p->d_prof) { for (int i = 0; i < 8; ++i) out[i] = 0; return 0; }
     RDQ_CHECK(hipDeviceSynchronize());
-    RDQ_CHECK(hipMemcpy(out, p->d_prof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    RDQ_CHECK(hipMemset(p->d_prof, 0, 8 * sizeof(unsigned long long)));
+    p->prof_host.resize(2 * PROF_WORDS);
+    RDQ_CHECK(hipMemcpy(p->prof_host.data(), p->d_prof, 2 * PROF_WORDS * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost));
+    RDQ_CHECK(hipMemset(p->d_prof, 0, 2 * PROF_WORDS * sizeof(unsigned long long)));
+    for (int i = 0; i < 4; ++i) { out[i] = p->prof_host[i]; out[4 + i] = p->prof_host[PROF_WORDS + i]; }
+    return 0;
+}
+
+int rdq_fwi_profile_waves(rdq_fwi_plan *p, int32_t adj, uint64_t *out, size_t count)
+{
+    if (!p || !out || (adj != 0 && adj != 1)) return RDQ_E_INVALID;
+    const size_t n = std::min(count, PROF_WAVES * 3);
+    for (size_t i = 0; i < n; ++i)
+        out[i] = p->prof_host.empty() ? 0 : p->prof_host[(adj ? PROF_WORDS : 0) + PROF_RAW + i];
     return 0;
 }
 
@@ -1872,7 +1929,8 @@ int rdq_fwi_grad_finalize(const rdq_fwi_plan *p, int32_t B, const float *coeffs,
     a.slice = (size_t)p->Hp * p->ld; a.cstride = (size_t)B * a.slice;
     a.coeffs = coeffs; a.gA = gA; a.gbeta = gbeta; a.vmin = vmin; a.amin = amin; a.gk_part = gk;
     a.isx = p->d_isx; a.colsum = colsum; a.out = out;
-    hipLaunchKernelGGL(k_fin_rows, dim3((p->g.nx + 63) / 64, p->Hp, B), dim3(64), 0, st, a);
+    if (p->Wp > FIN_MAXW) return RDQ_E_INVALID;
+    hipLaunchKernelGGL(k_fin_rows, dim3(p->Hp, B), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_fin_cols, dim3((p->g.nz * p->g.nx + 255) / 256, B), dim3(256), 0, st, a);
     RDQ_CHECK(hipGetLastError());
     return 0;

@@ -75,8 +75,11 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
-    def set_variant(self, fwd_gen_coeffs):
-        _hip.check(self.lib.rdq_fwi_set_variant(self.handle, int(bool(fwd_gen_coeffs))), "rdq_fwi_set_variant")
+    def set_variant(self, fwd_gen_coeffs=False, adj_exact=False):
+        """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
+        the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction."""
+        flags = (1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0)
+        _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_persistent(self, enable):
         _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, int(bool(enable))), "rdq_fwi_set_persistent")
@@ -107,6 +110,13 @@ class FwiPlan:
             res[name] = {"wait_us": out[o] / n / 100.0, "steps_us": out[o + 1] / n / 100.0,
                          "publish_us": out[o + 2] / n / 100.0, "waves": int(out[o + 3])}
         return res
+
+    def profile_waves(self, adj):
+        """(blocks*16, 3) per-wave {hand-off, steps, publish} us of the last read_profile()."""
+        n = 4096 * 16 * 3
+        out = (ctypes.c_uint64 * n)()
+        _hip.check(self.lib.rdq_fwi_profile_waves(self.handle, int(bool(adj)), out, n), "rdq_fwi_profile_waves")
+        return np.frombuffer(out, dtype=np.uint64).reshape(-1, 3).astype(np.float64) / 100.0
 
     def set_tuning(self, fwd_steps, adj_steps, chains=1):
         _hip.check(self.lib.rdq_fwi_set_tuning(self.handle, int(fwd_steps), int(adj_steps), int(chains)),

@@ -88,7 +88,9 @@ def test_gradient_vs_reference_autograd(cuda, name):
     seis, c = f.forward(vnorm(z["v_init"]), keep_history=True)
     _, ds = O.l1_loss(seis, z["y"], z["mask"] if "mask" in z.files else None)
     go = f.finalize(c, *f.adjoint(c, ds))
-    assert np.linalg.norm(g - go) / np.linalg.norm(go) < 1e-6
+    # default persistent adjoint contracts into FMAs (RDQ_VARIANT_ADJ_EXACT off): fp32-level only
+    err = np.linalg.norm(g - go) / np.linalg.norm(go)
+    assert err < 5e-6, err
 
 
 @pytest.mark.parametrize("steps,chains,persist", [(1, 1, True), (2, 1, True), (3, 1, True), (4, 1, True),
@@ -105,6 +107,7 @@ def test_adjoint_accumulators_bitexact_vs_oracle(cuda, name, kw, steps, chains, 
     plan = fwi._plan(v.shape[2], v.shape[3], v.device)
     plan.set_tuning(steps, steps, chains)
     plan.set_persistent(persist)
+    plan.set_variant(adj_exact=True)           # the oracle's exact fp32 order (bitwise gA)
     sz = plan.sizes(B)
     rng = np.random.default_rng(1)
     dseis = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
@@ -152,6 +155,7 @@ def test_persistent_partial_edge_tiles_vs_oracle(cuda, steps):
     rng = np.random.default_rng(5)
     dseis = torch.from_numpy(rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)).to(cuda)
     out = {}
+    plan.set_variant(adj_exact=True)
     for persist in (True, False):
         plan.set_persistent(persist)
         coeffs, vstat = plan.coeffs(v, 0)
@@ -176,6 +180,17 @@ def test_persistent_partial_edge_tiles_vs_oracle(cuda, steps):
     assert bits_equal(gA, oA)
     assert bits_equal(out[True][2].reshape(B, -1), ob)
     np.testing.assert_allclose(out[True][3], oK, rtol=1e-7)
+    # the default (FMA-contracted) persistent adjoint: fp32 tolerance
+    plan.set_variant(adj_exact=False)
+    plan.set_persistent(True)
+    coeffs, vstat = plan.coeffs(v, 0)
+    seis, hist = plan.forward(coeffs, B, keep_history=True)
+    gA2, gk2, gb2 = plan.adjoint(coeffs, hist, dseis, B)
+    plan.status()
+    gAs2 = gA2.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy().sum(1)
+    assert np.linalg.norm(gAs2 - oA) / np.linalg.norm(oA) < 2e-6
+    np.testing.assert_allclose(gb2.cpu().numpy().reshape(B, -1), ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
+    np.testing.assert_allclose(gk2.view(B, -1).sum(1).cpu().numpy(), oK, rtol=2e-5)
 
 
 def test_damp_profile_vs_reference(cuda):

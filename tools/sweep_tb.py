@@ -31,7 +31,7 @@ sz = plan.sizes(a.B)
 dseis = torch.randn(a.B, a.ns, sz.nrec, plan.ng, device=dev)
 res = []
 # (T, persistent)
-cfgs = [(a.only, 1)] if a.only else [(1, 1), (2, 1), (3, 1), (4, 1)]
+cfgs = [(a.only, 1)] if a.only else [(2, 1), (3, 1), (4, 1)]
 if a.chunked:
     cfgs += [(T, 0) for T in (2, 3, 4)]
 for T, G in cfgs:
@@ -61,7 +61,32 @@ for T, G in cfgs:
         seis, hist = plan.forward(coeffs, a.B, keep_history=True)
         plan.adjoint(coeffs, hist, dseis, a.B)
         prof = plan.read_profile()
+        import numpy as np
+        for name, adj in (("fwd", 0), ("adj", 1)):
+            wv = plan.profile_waves(adj)
+            live = wv[wv.sum(1) > 0]
+            ids = np.nonzero(wv.sum(1) > 0)[0]
+            tot = live.sum(1)
+            st = live[:, 1]
+            slow = ids[np.argsort(st)[-6:]]
+            prof[name]["steps_us_min_med_max"] = [round(float(np.min(st)), 1), round(float(np.median(st)), 1),
+                                                  round(float(np.max(st)), 1)]
+            prof[name]["total_us_min_max"] = [round(float(tot.min()), 1), round(float(tot.max()), 1)]
+            prof[name]["slowest_block_wave"] = [(int(i) // 16, int(i) % 16) for i in slow]
+            # per block: hand-off wait summed over its waves; the critical-path blocks wait least
+            blk = {}
+            for i, v in zip(ids, live[:, 0]):
+                blk.setdefault(int(i) // 16, []).append(v)
+            bw = sorted((float(np.mean(v)), b) for b, v in blk.items())
+            prof[name]["least_waiting_blocks"] = [(b, round(v, 1)) for v, b in bw[:8]]
+            prof[name]["most_waiting_blocks"] = [(b, round(v, 1)) for v, b in bw[-4:]]
+            # steps by wave index
+            byw = {}
+            for i, v in zip(ids, st):
+                byw.setdefault(int(i) % 16, []).append(v)
+            prof[name]["steps_us_by_wave"] = {k: round(float(np.mean(v)), 1) for k, v in sorted(byw.items())}
         plan.set_profile(0)
         del hist
-        res[-1]["profile_us_per_wave"] = {k: {kk: round(vv, 1) for kk, vv in d.items()} for k, d in prof.items()}
+        res[-1]["profile_us_per_wave"] = {k: {kk: (round(vv, 1) if isinstance(vv, float) else vv)
+                                              for kk, vv in d.items()} for k, d in prof.items()}
     print(json.dumps(res[-1]), flush=True)
