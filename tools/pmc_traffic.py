@@ -30,7 +30,7 @@ def main():
     w = per_dispatch(wdir, "WRITE_SIZE", kname)
     fetch = statistics.median(f) * f_fetch
     write = statistics.median(w) * f_write
-    out = {"kernel": kname, "dispatches": [len(f), len(w)], "fetch_factor": round(f_fetch, 4),
+    out = {"kernel": kname.rstrip(",") + ">", "dispatches": [len(f), len(w)], "fetch_factor": round(f_fetch, 4),
            "write_factor": round(f_write, 4), "fetch_bytes": fetch, "write_bytes": write,
            "traffic_bytes_per_launch": fetch + write,
            "note": "median per dispatch; FETCH_SIZE/WRITE_SIZE (KB) x calibration factor measured on "
