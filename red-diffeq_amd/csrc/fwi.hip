@@ -810,15 +810,16 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    // Wavelet samples of an epoch are loaded BEFORE its hand-off sweep, which ends the loop body:
+    // the sweep waits vmcnt(0) on every path into the next epoch (and the prologue waits
+    // explicitly), so no step ever waits on a load - a load inside the epoch would be waited for
+    // behind the in-order vmcnt of the history stores.
+    float wv[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
+    __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
-        if (e > 0) {
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * (e & 1)) * L + so);
-            PT_SWEEP(GR, (unsigned)e, P0, P1)
-        }
-        float wv[T];                                      // wavelet samples of this epoch
-#pragma unroll
-        for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + t, a.nt - 1)];
         // The previous epoch's last two levels are stored only now, after the hand-off: on gfx9
         // vmcnt also counts stores, so stores still in flight would hold up every hand-off load.
         if (e > 0 && a.hist) {
@@ -845,11 +846,17 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         }
         PT_PROF(tst)
         if (e + 1 < nep) {
+            const unsigned tag = (unsigned)(e + 1);
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
-            PT_PUBLISH(GR, (unsigned)(e + 1), P0, P1)
+            PT_PUBLISH(GR, tag, P0, P1)
+#pragma unroll
+            for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
+            PT_PROF(tpb)
+            PT_SWEEP(GR, tag, P0, P1)
+            __builtin_amdgcn_s_waitcnt(0x0F70);           // also on the gave-up path (no loads left)
         }
-        PT_PROF(tpb)
     }
+    PT_PROF(tsw)
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
         if (blockIdx.x < PROF_WAVES / 16) {
@@ -885,9 +892,8 @@ struct AdjPtArgs {
 // one adjoint step k; CUR = L_{k+1}, PRV = L_{k+2} -> L_k, P = P_{k-1} rows -2..9
 #define ADJ_STEP(CUR, PRV, P, PN)                                                                   \
     {                                                                                               \
-        if (grad && k > 1 && (t + 1 < T || e + 1 == nep)) ADJ_PLOAD(PN, k - 1)                     \
-        const float dcur = dn;                                                                      \
-        if (rmask) dn = DLOAD(k - 1);                                                               \
+        if (t + 1 < T) ADJ_PLOAD(PN, k - 1)         /* every wave (OOB offsets off the interior) */ \
+        const float dcur = dv[t];                                                                   \
         float q[R];                                                                                 \
         _Pragma("unroll") for (int r = 0; r < R; ++r) q[r] = A[r] * CUR[r];                         \
         const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0], q[1], q[R - 2], q[R - 1]);      \
@@ -990,7 +996,15 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         rcv0 = rs < re ? g.rcv_list[rs] : -1;
     }
     const float *DSb = a.dseis + (size_t)bs * g.nrec * g.ng;
-#define DLOAD(KK) ((rcv0 >= 0 && (KK) >= 1 && (((KK) - 1) % g.st) == 0) ? DSb[(size_t)(((KK) - 1) / g.st) * g.ng + rcv0] : -0.0f)
+    const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
+    // dseis[k-1] of this lane's receiver; -0 (x + -0 == x bitwise) where there is none.  An
+    // unconditional buffer load (OOB offset: no memory access) keeps every wave's vmcnt count equal.
+#define DLOAD(KK)                                                                                   \
+    ({                                                                                              \
+        const bool ok_ = rcv0 >= 0 && (KK) >= 1 && (((KK) - 1) % g.st) == 0;                        \
+        const float v_ = bload(DSR, ok_ ? (((KK) - 1) / g.st * g.ng + rcv0) * 4 : OOB, 0);          \
+        ok_ ? v_ : -0.0f;                                                                           \
+    })
     const bool rmulti = __any(re - rs > 1);
     const bool grad = rin != 0;                           // uniform: this wave has interior rows
     double ksum = 0.0;
@@ -1000,24 +1014,27 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     float PA[PR], PB[PR];
     int pv[PR];                                           // P row (uz0 - 2 + i) offset of this lane
 #pragma unroll
-    for (int i = 0; i < PR; ++i) { PA[i] = 0.0f; PB[i] = 0.0f; pv[i] = (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4; }
-    if (grad) ADJ_PLOAD(PA, a.nt)
-    float dn = rmask ? DLOAD(a.nt) : 0.0f;
+    for (int i = 0; i < PR; ++i) {
+        PA[i] = 0.0f; PB[i] = 0.0f;
+        pv[i] = grad ? (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4 : OOB;   // OOB: no memory access
+    }
+    // Per-epoch inputs (the first step's history slice P, the receiver residuals dseis[k-1] and the
+    // wavelet w[k-1] of the epoch's T steps) are loaded BEFORE the epoch's hand-off sweep, which
+    // ends the loop body: the sweep waits vmcnt(0) on every path into the next epoch (the prologue
+    // waits explicitly), so inside an epoch the only loads in flight are the one-step-ahead
+    // history prefetches and a step waits only for its own P.
+    float wv[T], dv[T];
+    ADJ_PLOAD(PA, a.nt)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        wv[t] = a.wav[max(a.nt - t - 1, 0)];
+        dv[t] = DLOAD(a.nt - t);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
     for (int e = 0; e < nep; ++e) {
-        if (e > 0) {
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * (e & 1)) * L + so);
-            PT_SWEEP(GR, (unsigned)e, L0, L1)
-            // this epoch's first P is loaded only now: loads in flight would hold up the hand-off
-            // loads (in-order vmcnt)
-            if (grad) ADJ_PLOAD(PA, a.nt - e * T)
-        }
-        float wv[T];                                      // w[k-1] of this epoch's steps
-#pragma unroll
-        for (int t = 0; t < T; ++t) wv[t] = a.wav[max(a.nt - (e * T + t) - 1, 0)];
-        PT_PROF(tsw)
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int j = e * T + t;
@@ -1034,10 +1051,21 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         }
         PT_PROF(tst)
         if (e + 1 < nep) {
+            const unsigned tag = (unsigned)(e + 1);
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
-            PT_PUBLISH(GR, (unsigned)(e + 1), L0, L1)
+            PT_PUBLISH(GR, tag, L0, L1)
+            const int kn = a.nt - (e + 1) * T;            // first step k of the next epoch
+            ADJ_PLOAD(PA, kn)
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                wv[t] = a.wav[max(kn - t - 1, 0)];
+                dv[t] = DLOAD(kn - t);
+            }
+            PT_PROF(tpb)
+            PT_SWEEP(GR, tag, L0, L1)
+            __builtin_amdgcn_s_waitcnt(0x0F70);           // also on the gave-up path (no loads left)
+            PT_PROF(tsw)
         }
-        PT_PROF(tpb)
     }
 #undef DLOAD
     if (a.prof && lane == 0) {
@@ -1446,28 +1474,47 @@ int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
     }
 }
 
-// grid of a persistent launch covering every shot of B models at depth T with NW-wave regions
-unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW)
+// tiles (padded to the 8-XCD deal) of one (model, shot) slice at depth T with NW-wave regions
+unsigned pt_tiles_padded(const rdq_fwi_plan *p, int T, int NW)
 {
     const int ih = NW * TB_R - 4 * T;
     const int nt_ = tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih);
-    return (unsigned)((nt_ + 7) / 8 * 8) * (unsigned)B * (unsigned)p->g.ns;
+    return (unsigned)((nt_ + 7) / 8 * 8);
+}
+
+// Shots per persistent launch: every slice of one launch must be resident at once, so a survey
+// larger than the chip (e.g. 32 OpenFWI shots = 4 x 224 workgroups) runs as ceil(ns / per) launches
+// over consecutive shot groups of near-equal size; 0 = not even one shot of all B models fits.
+int pt_shots_per_launch(const rdq_fwi_plan *p, int B, int T, int NW, int cap)
+{
+    if (cap <= 0) return 0;
+    const unsigned per = (unsigned)cap / (pt_tiles_padded(p, T, NW) * (unsigned)B);
+    if (per < 1) return 0;
+    const int groups = (p->g.ns + (int)per - 1) / (int)per;
+    return (p->g.ns + groups - 1) / groups;
+}
+
+// grid of a persistent launch covering `nsg` shots of B models
+unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg)
+{
+    return pt_tiles_padded(p, T, NW) * (unsigned)B * (unsigned)nsg;
 }
 
 // region height (waves) of the persistent kernel for this call, 0 = not resident -> chunked.
-// Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).
-int persistent_nw(rdq_fwi_plan *p, int B, bool adj)
+// Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).  `per` = shots
+// per launch (the survey runs as ceil(ns / per) launches).
+int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
 {
     if (!p->persist) return 0;
     const int T = adj ? p->adj_T : p->fwd_T;
     const int want = p->persist;   // 1 = auto, 8 / 12 = forced
     if (want == 1 || want == 12) {
-        const int c = capacity_nw<12>(p, adj, T);
-        if (c > 0 && pt_grid(p, B, T, 12) <= (unsigned)c) return 12;
+        const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw<12>(p, adj, T));
+        if (k > 0) { if (per) *per = k; return 12; }
     }
     if (want == 1 || want == 8) {
-        const int c = capacity_nw<8>(p, adj, T);
-        if (c > 0 && pt_grid(p, B, T, 8) <= (unsigned)c) return 8;
+        const int k = pt_shots_per_launch(p, B, T, 8, capacity_nw<8>(p, adj, T));
+        if (k > 0) { if (per) *per = k; return 8; }
     }
     return 0;
 }
@@ -1496,7 +1543,7 @@ void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
     }
 }
 
-int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, float *seis, float *hist, float *ring,
+int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coeffs, float *seis, float *hist, float *ring,
                       hipStream_t st)
 {
     FwdPtArgs a{};
@@ -1511,14 +1558,20 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, float
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof;
-    const dim3 grid(pt_grid(p, B, T, NW));
-    if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
-    else launch_fwd_pt<8>(T, grid, st, a);
-    RDQ_CHECK(hipGetLastError());
+    // consecutive shot groups, one resident launch each (granules live at per-slice offsets, so
+    // one zeroing serves every group)
+    for (int s0 = 0; s0 < p->g.ns; s0 += per) {
+        a.g.s_off = s0;
+        a.g.ns_grp = std::min(per, p->g.ns - s0);
+        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
+        else launch_fwd_pt<8>(T, grid, st, a);
+        RDQ_CHECK(hipGetLastError());
+    }
     return 0;
 }
 
-int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, const float *hist, const float *dseis,
+int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coeffs, const float *hist, const float *dseis,
                       float *ring, float *gA, double *gk, float *gbeta, hipStream_t st)
 {
     AdjPtArgs a{};
@@ -1537,10 +1590,14 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, const float *coeffs, const
     a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + PROF_WORDS : nullptr;
-    const dim3 grid(pt_grid(p, B, T, NW));
-    if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
-    else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }
-    RDQ_CHECK(hipGetLastError());
+    for (int s0 = 0; s0 < p->g.ns; s0 += per) {
+        a.g.s_off = s0;
+        a.g.ns_grp = std::min(per, p->g.ns - s0);
+        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
+        else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }
+        RDQ_CHECK(hipGetLastError());
+    }
     return 0;
 }
 
@@ -1890,10 +1947,11 @@ int rdq_fwi_forward(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, floa
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !seis || (!hist && !ring) || B < 1) return RDQ_E_INVALID;
-    if (const int nw = persistent_nw(p, B, false)) {
+    int per = 0;
+    if (const int nw = persistent_nw(p, B, false, &per)) {
         if (!ring) return RDQ_E_INVALID;   // the persistent kernel's hand-off granules live in `ring`
         return run_cached(p, (hist ? 3 : 4) + 16 * nw, B, {coeffs, seis, hist, ring}, st,
-                          [&](hipStream_t s) { return launch_forward_pt(p, B, nw, coeffs, seis, hist, ring, s); });
+                          [&](hipStream_t s) { return launch_forward_pt(p, B, nw, per, coeffs, seis, hist, ring, s); });
     }
     return run_cached(p, hist ? 0 : 1, B, {coeffs, seis, hist, ring}, st,
                       [&](hipStream_t s) { return launch_forward(p, B, coeffs, seis, hist, ring, s); });
@@ -1904,9 +1962,10 @@ int rdq_fwi_adjoint(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, cons
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !hist || !dseis || !ring || !gA || !gk || !gbeta || B < 1) return RDQ_E_INVALID;
-    if (const int nw = persistent_nw(p, B, true))
+    int per = 0;
+    if (const int nw = persistent_nw(p, B, true, &per))
         return run_cached(p, 5 + 16 * nw, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
-            return launch_adjoint_pt(p, B, nw, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
+            return launch_adjoint_pt(p, B, nw, per, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
         });
     return run_cached(p, 2, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
         return launch_adjoint(p, B, coeffs, hist, dseis, ring, gA, gk, gbeta, s);

@@ -193,6 +193,49 @@ def test_persistent_partial_edge_tiles_vs_oracle(cuda, steps):
     np.testing.assert_allclose(gk2.view(B, -1).sum(1).cpu().numpy(), oK, rtol=2e-5)
 
 
+def test_persistent_shot_groups_openfwi_ns20(cuda):
+    """A survey larger than one resident launch (OpenFWI grid, 20 shots: 8 fit at once) runs as
+    consecutive persistent launches over shot groups: forward and adjoint accumulators bit-exact
+    vs the chunked kernels (exact-order adjoint), the FMA adjoint within fp32 tolerance."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=70, nt=200, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=20)
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vnorm(make_model("curvefault", 70, 70, seed=3, batch=1))).to(cuda)
+    plan = fwi._plan(70, 70, v.device)
+    plan.set_tuning(4, 4, 1)
+    B = 1
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(7)
+    dseis = torch.from_numpy(rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)).to(cuda)
+    out = {}
+    plan.set_variant(adj_exact=True)
+    for persist in (True, False):
+        plan.set_persistent(persist)
+        info = plan.launch_info(B)
+        assert info["fwd_persistent"] == persist and info["adj_persistent"] == persist
+        coeffs, vstat = plan.coeffs(v, 0)
+        seis, hist = plan.forward(coeffs, B, keep_history=True)
+        gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+        plan.status()
+        out[persist] = (seis.cpu().numpy(), gA.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy(),
+                        gb.cpu().numpy(), gk.view(B, -1).sum(1).cpu().numpy())
+        del hist
+    for a, b in zip(out[True], out[False]):
+        if a.dtype == np.float32:
+            assert bits_equal(a, b)
+        else:
+            np.testing.assert_allclose(a, b, rtol=1e-12)
+    plan.set_variant(adj_exact=False)
+    plan.set_persistent(True)
+    coeffs, vstat = plan.coeffs(v, 0)
+    seis, hist = plan.forward(coeffs, B, keep_history=True)
+    gA2, gk2, gb2 = plan.adjoint(coeffs, hist, dseis, B)
+    plan.status()
+    ref = out[False][1].sum(1)
+    got = gA2.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy().sum(1)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-6
+
+
 def test_damp_profile_vs_reference(cuda):
     """Sponge (get_Abc, columns overwrite rows) as kappa/dt vs the reference fixture."""
     z = load_golden("damp")
