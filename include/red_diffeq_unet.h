@@ -32,9 +32,12 @@ typedef struct rdq_conv_desc {
 } rdq_conv_desc;
 
 /* y = conv2d(input, w, bias, stride 1, padding pad) [+ residual]   (nn.Conv2d, implicit GEMM on
- * fp32 MFMA v_mfma_f32_16x16x4_f32).  w: [cout][cin1+cin2][kh][kw]; bias/residual nullable. */
+ * fp32 MFMA v_mfma_f32_16x16x4_f32).  w: [cout][cin1+cin2][kh][kw]; bias/residual nullable.
+ * ws (nullable) holds split-K partial slabs: rdq_conv2d_ws_bytes(d) bytes let the kernel split the
+ * reduction over enough workgroups to fill the chip; a smaller (or null) ws splits less (or not). */
+size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
-               const float *residual, float *y, hipStream_t stream);
+               const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
 /* GroupNorm(G) -> [x*(scale+1)+shift] -> SiLU  (Block.forward, diffusion.py:142-149).
  * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes. */
@@ -54,13 +57,15 @@ int rdq_linear(int32_t B, int32_t in, int32_t out, const float *x, const float *
 int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, float *y, hipStream_t stream);
 
 /* LinearAttention core (diffusion.py:182-194; dh <= 32), qkv = to_qkv(RMSNorm(x)) as (B, 3*heads*dh, n);
- * mem_kv (2, heads, dh, nmem); out (B, heads*dh, n) before to_out.  ws: rdq_linear_attention_ws_bytes. */
-size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh);
+ * mem_kv (2, heads, dh, nmem); out (B, heads*dh, n) before to_out.  ws: rdq_linear_attention_ws_bytes
+ * (k-softmax statistics + per-256-token context partials, combined in a fixed order). */
+size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem);
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
                          const float *mem_kv, float *out, void *ws, hipStream_t stream);
 
 /* Attention core with Attend(flash=False) (diffusion.py:209-217): softmax(q k^T dh^-1/2) v over
- * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32, n <= 256. */
+ * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32; K/V of one
+ * head staged in LDS (n + nmem <= ~1500). */
 int rdq_full_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, const float *qkv,
                        const float *mem_kv, float *out, hipStream_t stream);
 

@@ -250,7 +250,9 @@ __device__ __forceinline__ Halo4 exchange_nw(float (*xch)[NW][4][64], int buf, i
     xch[buf][w][1][lane] = top1;
     xch[buf][w][2][lane] = bot1;
     xch[buf][w][3][lane] = bot0;
+#ifndef RDQ_EXP_NOBARRIER        // timing experiments only (tools/exp_variants.sh): wrong results
     __syncthreads();
+#endif
     Halo4 h;
     const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
     h.u2 = xch[buf][wu][2][lane];
@@ -587,6 +589,16 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 //
 // Granule buffer (inside the caller's `ring`): [2 epoch parity][2 level][B][ns][Hp][ld] u64,
 // zeroed before each launch; tag = epoch index (>= 1) so a zeroed granule never matches.
+// timing-experiment knockouts (0 in the product build; tools/exp_variants.sh builds the others)
+#ifndef RDQ_EXP_SWEEP_ONCE
+#define RDQ_EXP_SWEEP_ONCE 0
+#endif
+#ifndef RDQ_EXP_NOPLOAD
+#define RDQ_EXP_NOPLOAD 0
+#endif
+#ifndef RDQ_EXP_NOSTORE
+#define RDQ_EXP_NOSTORE 0
+#endif
 constexpr int CP_SC1 = 16;
 constexpr size_t PROF_RAW = 8;                        // per-wave records after the 4 summary words
 constexpr size_t PROF_WAVES = 4096 * 16;              // blocks x waves recorded
@@ -680,7 +692,7 @@ __device__ __forceinline__ int wrap_row(int uz, int Hp)
                     V1[r] = __uint_as_float(x1_.x);                                                 \
                 }                                                                                   \
             }                                                                                       \
-            if (__all(ok_)) break;                                                                  \
+            if (RDQ_EXP_SWEEP_ONCE || __all(ok_)) break;                                            \
             if (pass_ == 0) t0_ = __builtin_amdgcn_s_memrealtime();                                 \
             if ((pass_ & 15) == 15) {                                                               \
                 if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)   \
@@ -753,7 +765,7 @@ struct FwdPtArgs {
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
                 if ((sm_ >> r) & 1u) PRV[r] = PRV[r] + add;                                         \
         }                                                                                           \
-        if (a.hist && (t + 2 < T || e + 1 == nep)) {   /* own cells only: hv = OOB elsewhere */     \
+        if (!RDQ_EXP_NOSTORE && a.hist && (t + 2 < T || e + 1 == nep)) {   /* own cells only */    \
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
             _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PRV[r], hv[r], 0);            \
         }                                                                                           \
@@ -884,7 +896,7 @@ struct AdjPtArgs {
 
 // P_{k-1} (history slot K) rows uz0-2 .. uz0+9 into PD
 #define ADJ_PLOAD(PD, K)                                                                            \
-    {                                                                                               \
+    if (!RDQ_EXP_NOPLOAD) {                                                                         \
         const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(K) * L + so);                   \
         _Pragma("unroll") for (int i = 0; i < PR; ++i) PD[i] = bload(HR, pv[i], 0);                \
     }

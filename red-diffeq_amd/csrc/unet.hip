@@ -31,112 +31,163 @@ namespace {
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 // ------------------------------------------------------------------------------------ conv2d
-constexpr int CBM = 64;   // output pixels per workgroup tile
-constexpr int CBN = 64;   // output channels per workgroup tile
-constexpr int CKC = 16;   // K (= cin*kh*kw) per LDS stage
+// Implicit GEMM on the fp32 matrix cores: D[cout][pixel] = W[cout][k] x A[k][pixel], k = (ci, ky, kx).
+// A workgroup (4 waves) owns a 64 (cout) x 32 (pixel) output tile; wave w the couts 16w..16w+15 as
+// two 16x16 MFMA tiles (v_mfma_f32_16x16x4_f32: exact f32 products, one VGPR per operand per lane;
+// lane l supplies A[m = l&15][k = l>>4] and B[k = l>>4][n = l&15], D[m = (l>>4)*4 + r][n = l&15]).
+// K is staged 32 deep through double-buffered LDS (one barrier per stage; the next stage's
+// global loads are in flight during the current stage's MFMAs).  Row pitches make every operand
+// read conflict-free: Ws[n][k] pitch 36 (16 n x 4 k -> 64 distinct banks), As[k][p] pitch 48.
+// The U-Net's data movement is folded into the A gather (channel concat of skips, nearest x2
+// upsample, 2x2 pixel-unshuffle).  Small-M layers (B = 1 at 18x18 / 9x9: K up to 6912) split K over
+// blockIdx.z into fp32 partial slabs summed in a fixed order by k_conv_reduce (deterministic).
+constexpr int IG_BN = 64, IG_BM = 32, IG_BK = 32;
+constexpr int IG_LDW = IG_BK + 4, IG_LDA = IG_BM + 16;
 
-struct ConvArgs {
+struct IgArgs {
     rdq_conv_desc d;
     const float *x, *x2, *w, *bias, *res;
-    float *y;
+    float *y;                 // S == 1: output (+ bias + residual)
+    float *part;              // S > 1: partial slabs [S][B][cout][HW]
+    int K, M, HW, nsteps, per_split, S;
 };
 
-__device__ __forceinline__ float conv_in(const ConvArgs &a, int b, int ci, int ih, int iw)
+// A[k][pixel] of the logical input (zero padding outside the image)
+template <int KH, int MODE>
+__device__ __forceinline__ float ig_gather(const IgArgs &a, bool pv, int b, int oh, int ow, int k)
 {
+    if (!pv || k >= a.K) return 0.0f;
     const rdq_conv_desc &d = a.d;
-    if (ih < 0 || iw < 0 || ih >= d.H || iw >= d.W) return 0.0f;
-    switch (d.in_mode) {
-    case RDQ_IN_UPSAMPLE2: {
+    const int kh = KH ? KH : d.kh, kw = KH ? KH : d.kw;
+    const int kk = kh * kw;
+    const int ci = k / kk, r = k - ci * kk;
+    const int ky = r / kw, kx = r - ky * kw;
+    const int ih = oh + ky - d.pad, iw = ow + kx - d.pad;
+    if ((unsigned)ih >= (unsigned)d.H || (unsigned)iw >= (unsigned)d.W) return 0.0f;
+    if (MODE == RDQ_IN_UPSAMPLE2) {
         const int h2 = d.H >> 1, w2 = d.W >> 1;
         return a.x[(((size_t)b * d.cin1 + ci) * h2 + (ih >> 1)) * w2 + (iw >> 1)];
-    }
-    case RDQ_IN_UNSHUFFLE2: {
+    } else if (MODE == RDQ_IN_UNSHUFFLE2) {
         const int c = ci >> 2, p1 = (ci >> 1) & 1, p2 = ci & 1;
-        const int H2 = d.H * 2, W2 = d.W * 2;
-        return a.x[(((size_t)b * (d.cin1 >> 2) + c) * H2 + 2 * ih + p1) * W2 + 2 * iw + p2];
-    }
-    default:
+        return a.x[(((size_t)b * (d.cin1 >> 2) + c) * (2 * d.H) + 2 * ih + p1) * (2 * d.W) + 2 * iw + p2];
+    } else {
         if (ci < d.cin1) return a.x[(((size_t)b * d.cin1 + ci) * d.H + ih) * d.W + iw];
         return a.x2[(((size_t)b * d.cin2 + (ci - d.cin1)) * d.H + ih) * d.W + iw];
     }
 }
 
-// One workgroup = 4 waves = a 64 (pixels) x 64 (channels) output tile; each wave a 32 x 32 quarter
-// as 2 x 2 MFMA 16x16 tiles.  MFMA operand maps (gfx950, 16x16x4 f32): lane l supplies
-// A[m = l&15][k = l>>4] and B[k = l>>4][n = l&15]; D[m = (l>>4)*4 + r][n = l&15].
-__global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs a)
+template <int KH, int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
 {
-    __shared__ float As[CKC][CBM + 4];
-    __shared__ float Bs[CKC][CBN + 4];
-    const rdq_conv_desc &d = a.d;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid & 1, wn = wid >> 1;
-    const int HW = d.H * d.W;
-    const int M = d.B * HW, N = d.cout, KK = d.kh * d.kw, K = (d.cin1 + d.cin2) * KK;
-    const int m0 = blockIdx.x * CBM, n0 = blockIdx.y * CBN;
-    // this thread's gather pixel
-    const int am = m0 + (tid & 63);
-    const bool mvalid = am < M;
-    const int ab = mvalid ? am / HW : 0;
-    const int apix = mvalid ? am - ab * HW : 0;
-    const int aoh = apix / d.W, aow = apix - aoh * d.W;
-    f32x4 acc[2][2];
+    __shared__ __attribute__((aligned(16))) float Ws[2][IG_BN][IG_LDW];
+    __shared__ float As[2][IG_BK][IG_LDA];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * IG_BM, n0 = blockIdx.y * IG_BN, split = blockIdx.z;
+    const int N = a.d.cout, K = a.K;
+    const int s_begin = split * a.per_split, s_end = min(a.nsteps, s_begin + a.per_split);
+    // gather role: pixel gp, k rows gk + 8j
+    const int gp = tid & (IG_BM - 1), gk = tid >> 5;
+    const int gm = m0 + gp;
+    const bool pv = gm < a.M;
+    const int gb = pv ? gm / a.HW : 0, gpix = pv ? gm - gb * a.HW : 0;
+    const int oh = gpix / a.d.W, ow = gpix - oh * a.d.W;
+    // weight role: rows wn + 32j, k quad wk
+    const int wn = tid >> 3, wk = (tid & 7) * 4;
+    const bool wvec = (K & 3) == 0;
+    float ra[4];
+    f32x4 rw[2];
+    auto load = [&](int s) {
+        const int k0 = s * IG_BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int k0 = 0; k0 < K; k0 += CKC) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int kr = (tid >> 6) + 4 * j, k = k0 + kr;
-            float v = 0.0f;
-            if (mvalid && k < K) {
-                const int ci = k / KK, rem = k - ci * KK;
-                const int ky = rem / d.kw, kx = rem - ky * d.kw;
-                v = conv_in(a, ab, ci, aoh + ky - d.pad, aow + kx - d.pad);
-            }
-            As[kr][tid & 63] = v;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int kk = tid & 15, n = (tid >> 4) + 16 * j;
-            Bs[kk][n] = (n0 + n < N && k0 + kk < K) ? a.w[(size_t)(n0 + n) * K + k0 + kk] : 0.0f;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int ks = 0; ks < CKC / 4; ++ks) {
-            const int kr = ks * 4 + (lane >> 4);
-            float af[2], bf[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = As[kr][wm * 32 + i * 16 + (lane & 15)];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = Bs[kr][wn * 32 + j * 16 + (lane & 15)];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 4; ++j) ra[j] = ig_gather<KH, MODE>(a, pv, gb, oh, ow, k0 + gk + 8 * j);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-            if (n >= N) continue;
-            const float bv = a.bias ? a.bias[n] : 0.0f;
+            const int n = n0 + wn + 32 * j, k = k0 + wk;
+            const float *wr = a.w + (size_t)n * K + k;
+            if (n < N && wvec && k + 3 < K) {
+                rw[j] = *reinterpret_cast<const f32x4 *>(wr);
+            } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-                if (m >= M) continue;
-                const int b = m / HW, pix = m - b * HW;
-                const size_t o = ((size_t)b * N + n) * HW + pix;
-                float v = acc[i][j][r] + bv;
-                if (a.res) v = v + a.res[o];
-                a.y[o] = v;
+                for (int q = 0; q < 4; ++q) rw[j][q] = (n < N && k + q < K) ? wr[q] : 0.0f;
             }
         }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[buf][gk + 8 * j][gp] = ra[j];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *reinterpret_cast<f32x4 *>(&Ws[buf][wn + 32 * j][wk]) = rw[j];
+    };
+    f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+    if (s_begin < s_end) {
+        load(s_begin);
+        stash(0);
+    }
+    __syncthreads();
+    for (int s = s_begin; s < s_end; ++s) {
+        const int buf = (s - s_begin) & 1;
+        if (s + 1 < s_end) load(s + 1);
+#pragma unroll
+        for (int ks = 0; ks < IG_BK / 4; ++ks) {
+            const int kk = ks * 4 + (lane >> 4);
+            const float av = Ws[buf][wv * 16 + (lane & 15)][kk];
+            const float b0 = As[buf][kk][lane & 15], b1 = As[buf][kk][16 + (lane & 15)];
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[1], 0, 0, 0);
+        }
+        if (s + 1 < s_end) stash(buf ^ 1);
+        __syncthreads();
+    }
+    const size_t slab = (size_t)a.M * N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = m0 + j * 16 + (lane & 15);
+        if (m >= a.M) continue;
+        const int b = m / a.HW, pix = m - b * a.HW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = n0 + wv * 16 + (lane >> 4) * 4 + r;
+            if (n >= N) continue;
+            const size_t o = ((size_t)b * N + n) * a.HW + pix;
+            if (a.S == 1) {
+                float v = acc[j][r] + (a.bias ? a.bias[n] : 0.0f);
+                if (a.res) v = v + a.res[o];
+                a.y[o] = v;
+            } else {
+                a.part[split * slab + o] = acc[j][r];
+            }
+        }
+    }
+}
+
+// split-K combine: fixed slab order, then bias and residual
+__global__ __launch_bounds__(256) void k_conv_reduce(int S, int64_t total, int N, int HW, const float *__restrict__ part,
+                                                     const float *__restrict__ bias, const float *__restrict__ res,
+                                                     float *__restrict__ y)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    float v = part[i];
+    for (int s = 1; s < S; ++s) v += part[(size_t)s * total + i];
+    if (bias) v = v + bias[(i / HW) % N];
+    if (res) v = v + res[i];
+    y[i] = v;
+}
+
+// split count: about one workgroup per CU over the tile grid, >= 4 K stages per split, and the
+// partial slabs within the caller's workspace
+int ig_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
+{
+    const int M = d->B * d->H * d->W, K = (d->cin1 + d->cin2) * d->kh * d->kw;
+    const int tiles = ((M + IG_BM - 1) / IG_BM) * ((d->cout + IG_BN - 1) / IG_BN);
+    const int nsteps = (K + IG_BK - 1) / IG_BK;
+    int S = std::max(1, std::min((256 + tiles - 1) / tiles, nsteps / 4));
+    const size_t slab = (size_t)M * d->cout * sizeof(float);
+    if (S > 1 && ws_bytes < 2 * slab) S = 1;
+    if (S > 1) S = std::min<int64_t>(S, (int64_t)(ws_bytes / slab));
+    const int per = (nsteps + S - 1) / S;
+    *per_split = per;
+    return (nsteps + per - 1) / per;
 }
 
 // -------------------------------------------------------------------------------- group norm
@@ -198,20 +249,33 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, float ep
 }
 
 // ----------------------------------------------------------------------------------- rmsnorm
-__global__ __launch_bounds__(256) void k_rmsnorm(int C, int HW, const float *__restrict__ x,
-                                                 const float *__restrict__ g, const float *__restrict__ res,
-                                                 float *__restrict__ y)
+// 64 pixels (lanes, coalesced) x 16 channel groups (waves) per workgroup: the channel sum of squares
+// is split over the waves and combined in LDS in a fixed order, so small-HW stages (9x9 x 512
+// channels) still spread over many lanes.
+constexpr int RMS_G = 16;
+__global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm(int C, int HW, const float *__restrict__ x,
+                                                        const float *__restrict__ g, const float *__restrict__ res,
+                                                        float *__restrict__ y)
 {
-    const int pix = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
-    if (pix >= HW) return;
+    __shared__ float part[RMS_G][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int pix = blockIdx.x * 64 + lane, b = blockIdx.y;
+    const bool ok = pix < HW;
     const float *px = x + (size_t)b * C * HW + pix;
     float ssum = 0.0f;
-    for (int c = 0; c < C; ++c) { const float v = px[(size_t)c * HW]; ssum += v * v; }
-    const float den = fmaxf(sqrtf(ssum), 1e-12f);      // F.normalize: x / max(||x||, eps)
+    if (ok)
+        for (int c = grp; c < C; c += RMS_G) { const float v = px[(size_t)c * HW]; ssum += v * v; }
+    part[grp][lane] = ssum;
+    __syncthreads();
+    float tot = 0.0f;
+#pragma unroll
+    for (int i = 0; i < RMS_G; ++i) tot += part[i][lane];
+    if (!ok) return;
+    const float den = fmaxf(sqrtf(tot), 1e-12f);      // F.normalize: x / max(||x||, eps)
     const float sc = sqrtf((float)C);
     float *py = y + (size_t)b * C * HW + pix;
     const float *pr = res ? res + (size_t)b * C * HW + pix : nullptr;
-    for (int c = 0; c < C; ++c) {
+    for (int c = grp; c < C; c += RMS_G) {
         float v = px[(size_t)c * HW] / den;
         v = v * g[c];
         v = v * sc;
@@ -254,59 +318,96 @@ __global__ void k_sinusoidal(int dim, float neg_emb, const int64_t *__restrict__
 }
 
 // -------------------------------------------------------------------------- linear attention
-// per (b, h, d): softmax statistics of k[d, :] over memory + pixels, then ctx[d][e] = sum_n p v
-__global__ __launch_bounds__(256) void k_la_context(int heads, int dh, int n, int nmem, const float *__restrict__ qkv,
-                                                    const float *__restrict__ mem, float *__restrict__ ctx)
+// k softmax over the (memory + pixel) tokens per (b, h, d): ONE pass of online max / sum per row
+// (one wave per row, lanes strided over tokens, fixed-order wave reduction).
+__device__ __forceinline__ void online_merge(float &m, float &s, float m2, float s2)
 {
-    const int d = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int C = heads * dh;
-    const float *krow = qkv + ((size_t)b * 3 * C + C + h * dh + d) * n;
-    const float *vbase = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
-    const float *mk = mem + ((size_t)(0 * heads + h) * dh + d) * nmem;   // mem_kv[0][h][d][:]
-    const float *mv = mem + (size_t)(1 * heads + h) * dh * nmem;          // mem_kv[1][h][e][:]
-    __shared__ float red[256];
-    __shared__ float acc[256][33];
-    const int tid = threadIdx.x;
-    float mx = -INFINITY;
-    for (int j = tid; j < nmem + n; j += 256) mx = fmaxf(mx, j < nmem ? mk[j] : krow[j - nmem]);
-    red[tid] = mx;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) { if (tid < w) red[tid] = fmaxf(red[tid], red[tid + w]); __syncthreads(); }
-    mx = red[0];
-    __syncthreads();
-    float sm = 0.0f;
-    for (int j = tid; j < nmem + n; j += 256) sm += expf((j < nmem ? mk[j] : krow[j - nmem]) - mx);
-    red[tid] = sm;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
-    const float inv = 1.0f / red[0];
-    float s[32];
-#pragma unroll
-    for (int e = 0; e < 32; ++e) s[e] = 0.0f;
-    for (int j = tid; j < nmem + n; j += 256) {
-        const float p = expf((j < nmem ? mk[j] : krow[j - nmem]) - mx) * inv;
-#pragma unroll
-        for (int e = 0; e < 32; ++e)
-            if (e < dh) s[e] += p * (j < nmem ? mv[(size_t)e * nmem + j] : vbase[(size_t)e * n + (j - nmem)]);
-    }
-#pragma unroll
-    for (int e = 0; e < 32; ++e) acc[tid][e] = s[e];
-    __syncthreads();
-    if (tid < dh) {
-        float t = 0.0f;
-        for (int i = 0; i < 256; ++i) t += acc[i][tid];
-        ctx[(((size_t)b * heads + h) * dh + d) * dh + tid] = t;
-    }
+    const float mn = fmaxf(m, m2);
+    if (mn == -INFINITY) return;
+    s = s * expf(m - mn) + s2 * expf(m2 - mn);
+    m = mn;
 }
 
-// per (b, h, pixel): q softmax over d, scale, out[e] = sum_d ctx[d][e] q[d]
-__global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float scale, const float *__restrict__ qkv,
-                                                const float *__restrict__ ctx, float *__restrict__ out)
+__global__ __launch_bounds__(256) void k_la_stats(int B, int heads, int dh, int n, int nmem,
+                                                  const float *__restrict__ qkv, const float *__restrict__ mem,
+                                                  float *__restrict__ stats)
 {
-    const int h = blockIdx.y, b = blockIdx.z;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);          // (b, h, d) flattened
     const int C = heads * dh;
-    __shared__ float cs[32][33];
-    for (int i = threadIdx.x; i < dh * dh; i += blockDim.x) cs[i / dh][i % dh] = ctx[(((size_t)b * heads + h) * dh) * dh + i];
+    if (row >= B * heads * dh) return;
+    const int b = row / (heads * dh), hd = row - b * heads * dh;
+    const float *krow = qkv + ((size_t)b * 3 * C + C + hd) * n;
+    const float *mk = mem + (size_t)hd * nmem;                   // mem_kv[0][h][d][:]
+    float m = -INFINITY, sm = 0.0f;
+    for (int j = lane; j < nmem + n; j += 64) {
+        const float v = j < nmem ? mk[j] : krow[j - nmem];
+        if (v > m) { sm = sm * expf(m - v) + 1.0f; m = v; }
+        else sm += expf(v - m);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_down(m, off, 64), s2 = __shfl_down(sm, off, 64);
+        online_merge(m, sm, m2, s2);
+    }
+    if (lane == 0) { stats[2 * row] = m; stats[2 * row + 1] = sm; }
+}
+
+// partial context over a 256-token chunk: ctx_part[chunk][b][h][d][e] = sum_j exp(k[d][j] - m_d) v[e][j]
+constexpr int LA_CH = 256;
+__global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nmem, const float *__restrict__ qkv,
+                                                const float *__restrict__ mem, const float *__restrict__ stats,
+                                                float *__restrict__ part)
+{
+    __shared__ float P[32][LA_CH + 1], V[32][LA_CH + 1];
+    const int ch = blockIdx.x, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+    const int C = heads * dh, nk = nmem + n;
+    const int j0 = ch * LA_CH;
+    const float *kb = qkv + ((size_t)b * 3 * C + C + h * dh) * n;
+    const float *vb = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
+    const float *mk = mem + (size_t)(0 * heads + h) * dh * nmem;
+    const float *mv = mem + (size_t)(1 * heads + h) * dh * nmem;
+    const float *st = stats + ((size_t)(b * heads + h) * dh) * 2;
+    for (int i = tid; i < dh * LA_CH; i += 256) {
+        const int d = i / LA_CH, jj = i - d * LA_CH, j = j0 + jj;
+        float pk = 0.0f, vv = 0.0f;
+        if (j < nk) {
+            const float kv = j < nmem ? mk[(size_t)d * nmem + j] : kb[(size_t)d * n + (j - nmem)];
+            pk = expf(kv - st[2 * d]);
+            vv = j < nmem ? mv[(size_t)d * nmem + j] : vb[(size_t)d * n + (j - nmem)];
+        }
+        P[d][jj] = pk;
+        V[d][jj] = vv;                                           // row d of V = value channel e = d
+    }
+    __syncthreads();
+    // 256 threads x 4 outputs: (d, e) = (tid >> 3, (tid & 7) * 4 + q)
+    const int d = tid >> 3, e0 = (tid & 7) * 4;
+    if (d >= dh) return;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int jj = 0; jj < LA_CH; ++jj) {
+        const float p = P[d][jj];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += p * V[e0 + q][jj];
+    }
+    float *o = part + ((((size_t)ch * gridDim.z + b) * heads + h) * dh + d) * dh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) if (e0 + q < dh) o[e0 + q] = acc[q];
+}
+
+// per (b, h, pixel): ctx = (sum of chunk partials in order) / sum_d; q softmax over d, scale,
+// out[e] = sum_d ctx[d][e] q[d]
+__global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, int nch, float scale,
+                                                const float *__restrict__ qkv, const float *__restrict__ stats,
+                                                const float *__restrict__ part, float *__restrict__ out)
+{
+    const int h = blockIdx.y, b = blockIdx.z, B = gridDim.z;
+    const int C = heads * dh;
+    __shared__ __attribute__((aligned(16))) float cs[32][32];
+    for (int i = threadIdx.x; i < dh * dh; i += blockDim.x) {
+        const int d = i / dh;
+        float t = 0.0f;
+        for (int c = 0; c < nch; ++c) t += part[(((size_t)c * B + b) * heads + h) * dh * dh + i];
+        cs[d][i - d * dh] = t / stats[((size_t)(b * heads + h) * dh + d) * 2 + 1];
+    }
     __syncthreads();
     const int pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= n) return;
@@ -320,27 +421,41 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
     for (int d = 0; d < 32; ++d) if (d < dh) { qv[d] = expf(qv[d] - mx); sm += qv[d]; }
 #pragma unroll
     for (int d = 0; d < 32; ++d) if (d < dh) qv[d] = (qv[d] / sm) * scale;
-    float *o = out + ((size_t)b * C + h * dh) * n + pix;
-    for (int e = 0; e < dh; ++e) {
-        float t = 0.0f;
+    float o[32];
 #pragma unroll
-        for (int d = 0; d < 32; ++d) if (d < dh) t += cs[d][e] * qv[d];
-        o[(size_t)e * n] = t;
+    for (int e = 0; e < 32; ++e) o[e] = 0.0f;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) {
+        if (d < dh) {
+#pragma unroll
+            for (int e4 = 0; e4 < 8; ++e4) {
+                const f32x4 c4 = *reinterpret_cast<const f32x4 *>(&cs[d][e4 * 4]);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) o[e4 * 4 + q4] += c4[q4] * qv[d];
+            }
+        }
     }
+    float *ob = out + ((size_t)b * C + h * dh) * n + pix;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) if (e < dh) ob[(size_t)e * n] = o[e];
 }
 
 // ---------------------------------------------------------------------------- full attention
-// one workgroup per (b, h); one thread per query pixel (n <= blockDim); head width DH (32 in the U-Net)
+// Workgroup = (b, h, 32 queries) x FA_KS key splits: thread (query i, split ks) runs an online
+// softmax over the keys j = ks (mod FA_KS) from LDS; the FA_KS partial (max, sum, o[32]) of a query
+// are merged in a fixed order, each split thread finishing 32 / FA_KS output channels.
+constexpr int FA_KS = 8, FA_QB = 256 / FA_KS;
 template <int DH>
 __global__ __launch_bounds__(256) void k_full_attn(int heads, int n, int nmem, const float *__restrict__ qkv,
                                                    const float *__restrict__ mem, float *__restrict__ out)
 {
-    constexpr int dh = DH;
+    constexpr int dh = DH, LD = DH + 1;
     const int h = blockIdx.x, b = blockIdx.y;
     const int C = heads * dh, nk = nmem + n;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *Ks = sm;                      // [nk][dh+1]
-    float *Vs = sm + nk * (dh + 1);      // [nk][dh+1]
+    float *Ks = sm;                      // [nk][LD]
+    float *Vs = Ks + nk * LD;            // [nk][LD]
+    float *Po = Vs + nk * LD;            // [256][LD + 2]: o[0..dh), m, l per (query, split)
     const float *kb = qkv + ((size_t)b * 3 * C + C + h * dh) * n;
     const float *vb = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
     for (int i = threadIdx.x; i < nk * dh; i += blockDim.x) {
@@ -353,40 +468,59 @@ __global__ __launch_bounds__(256) void k_full_attn(int heads, int n, int nmem, c
             kv = kb[(size_t)d * n + (j - nmem)];
             vv = vb[(size_t)d * n + (j - nmem)];
         }
-        Ks[j * (dh + 1) + d] = kv;
-        Vs[j * (dh + 1) + d] = vv;
+        Ks[j * LD + d] = kv;
+        Vs[j * LD + d] = vv;
     }
     __syncthreads();
-    const int i = threadIdx.x;
-    if (i >= n) return;
-    const float *qb = qkv + ((size_t)b * 3 * C + h * dh) * n + i;
-    float q[DH];
+    const int ql = threadIdx.x % FA_QB, ks = threadIdx.x / FA_QB;
+    const int qi = blockIdx.z * FA_QB + ql;
+    const bool qok = qi < n;
+    float q[DH], o[DH];
+    const float *qb = qkv + ((size_t)b * 3 * C + h * dh) * n + (qok ? qi : 0);
 #pragma unroll
-    for (int d = 0; d < dh; ++d) q[d] = qb[(size_t)d * n];
+    for (int d = 0; d < dh; ++d) { q[d] = qok ? qb[(size_t)d * n] : 0.0f; o[d] = 0.0f; }
     const float scale = 1.0f / sqrtf((float)dh);
-    float mx = -INFINITY;
-    for (int j = 0; j < nk; ++j) {
-        float s = 0.0f;
+    float m = -INFINITY, l = 0.0f;
+    for (int j = ks; j < nk; j += FA_KS) {
+        float sc = 0.0f;
 #pragma unroll
-        for (int d = 0; d < dh; ++d) s += q[d] * Ks[j * (dh + 1) + d];
-        mx = fmaxf(mx, s * scale);
+        for (int d = 0; d < dh; ++d) sc += q[d] * Ks[j * LD + d];
+        sc = sc * scale;
+        const float mn = fmaxf(m, sc);
+        const float corr = expf(m - mn), p = expf(sc - mn);
+        l = l * corr + p;
+#pragma unroll
+        for (int d = 0; d < dh; ++d) o[d] = o[d] * corr + p * Vs[j * LD + d];
+        m = mn;
     }
-    float o[DH];
+    float *po = Po + (size_t)threadIdx.x * (LD + 2);
 #pragma unroll
-    for (int d = 0; d < dh; ++d) o[d] = 0.0f;
-    float den = 0.0f;
-    for (int j = 0; j < nk; ++j) {
-        float s = 0.0f;
+    for (int d = 0; d < dh; ++d) po[d] = o[d];
+    po[LD] = m;
+    po[LD + 1] = l;
+    __syncthreads();
+    if (!qok) return;
+    // merge the FA_KS partials of query ql in split order; this thread writes channels ks*dh/FA_KS...
+    float M = -INFINITY;
 #pragma unroll
-        for (int d = 0; d < dh; ++d) s += q[d] * Ks[j * (dh + 1) + d];
-        const float p = expf(s * scale - mx);
-        den += p;
+    for (int k2 = 0; k2 < FA_KS; ++k2) M = fmaxf(M, Po[(size_t)(k2 * FA_QB + ql) * (LD + 2) + LD]);
+    float Lsum = 0.0f, w[FA_KS];
 #pragma unroll
-        for (int d = 0; d < dh; ++d) o[d] += p * Vs[j * (dh + 1) + d];
+    for (int k2 = 0; k2 < FA_KS; ++k2) {
+        const float *pk = Po + (size_t)(k2 * FA_QB + ql) * (LD + 2);
+        w[k2] = pk[LD] == -INFINITY ? 0.0f : expf(pk[LD] - M);
+        Lsum += pk[LD + 1] * w[k2];
     }
-    float *ob = out + ((size_t)b * C + h * dh) * n + i;
+    constexpr int DPS = DH / FA_KS;
+    float *ob = out + ((size_t)b * C + h * dh) * n + qi;
 #pragma unroll
-    for (int d = 0; d < dh; ++d) ob[(size_t)d * n] = o[d] / den;
+    for (int dd = 0; dd < DPS; ++dd) {
+        const int d = ks * DPS + dd;
+        float t = 0.0f;
+#pragma unroll
+        for (int k2 = 0; k2 < FA_KS; ++k2) t += Po[(size_t)(k2 * FA_QB + ql) * (LD + 2) + d] * w[k2];
+        ob[(size_t)d * n] = t / Lsum;
+    }
 }
 
 // -------------------------------------------------------------------------- RED elementwise
@@ -422,21 +556,56 @@ __global__ __launch_bounds__(256) void k_red_epilogue(int64_t n, const float *__
     g[o] = pn - eps[o];
 }
 
+template <int KH>
+void launch_conv_ig(dim3 grid, hipStream_t st, const IgArgs &a)
+{
+    switch (a.d.in_mode) {
+    case RDQ_IN_UPSAMPLE2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_ig<KH, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, a); break;
+    case RDQ_IN_UNSHUFFLE2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_ig<KH, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_ig<KH, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
+size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d)
+{
+    if (!d || d->B < 1 || d->H < 1 || d->W < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->cin1 < 1) return 0;
+    int per = 0;
+    const int S = ig_splits(d, (size_t)-1 / 2, &per);
+    return S > 1 ? (size_t)S * d->B * d->H * d->W * d->cout * sizeof(float) : 0;
+}
+
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
-               const float *residual, float *y, hipStream_t st)
+               const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
 {
     if (!d || !x || !w || !y || d->B < 1 || d->cin1 < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->H < 1 ||
-        d->W < 1 || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        d->W < 1 || d->pad < 0 || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
         return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return RDQ_E_INVALID;
-    ConvArgs a{*d, x, x2, w, bias, residual, y};
-    const int M = d->B * d->H * d->W;
-    hipLaunchKernelGGL(k_conv_mfma, dim3((M + CBM - 1) / CBM, (d->cout + CBN - 1) / CBN), dim3(256), 0, st, a);
+    IgArgs a{};
+    a.d = *d; a.x = x; a.x2 = x2; a.w = w; a.bias = bias; a.res = residual; a.y = y;
+    a.part = static_cast<float *>(ws);
+    a.K = (d->cin1 + d->cin2) * d->kh * d->kw;
+    a.HW = d->H * d->W;
+    a.M = d->B * a.HW;
+    a.nsteps = (a.K + IG_BK - 1) / IG_BK;
+    a.S = ws ? ig_splits(d, ws_bytes, &a.per_split) : 1;
+    if (a.S == 1) a.per_split = a.nsteps;
+    const dim3 grid((a.M + IG_BM - 1) / IG_BM, (d->cout + IG_BN - 1) / IG_BN, a.S);
+    const bool sq = d->kh == d->kw;
+    if (sq && d->kh == 3) launch_conv_ig<3>(grid, st, a);
+    else if (sq && d->kh == 1) launch_conv_ig<1>(grid, st, a);
+    else if (sq && d->kh == 7) launch_conv_ig<7>(grid, st, a);
+    else launch_conv_ig<0>(grid, st, a);
+    if (a.S > 1) {
+        const int64_t total = (int64_t)a.M * d->cout;
+        hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a.S, total, d->cout,
+                           a.HW, a.part, bias, residual, y);
+    }
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -467,7 +636,7 @@ int rdq_rmsnorm(int32_t B, int32_t C, int32_t HW, const float *x, const float *g
                 hipStream_t st)
 {
     if (B < 1 || C < 1 || HW < 1 || !x || !g || !y) return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_rmsnorm, dim3((HW + 255) / 256, B), dim3(256), 0, st, C, HW, x, g, res, y);
+    hipLaunchKernelGGL(k_rmsnorm, dim3((HW + 63) / 64, B), dim3(64 * RMS_G), 0, st, C, HW, x, g, res, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -491,9 +660,12 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
     return 0;
 }
 
-size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh)
+static int la_chunks(int n, int nmem) { return (n + nmem + LA_CH - 1) / LA_CH; }
+
+size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem)
 {
-    return (size_t)B * heads * dh * dh * sizeof(float);
+    if (B < 1 || heads < 1 || dh < 1 || n < 1 || nmem < 0) return 0;
+    return ((size_t)B * heads * dh * 2 + (size_t)la_chunks(n, nmem) * B * heads * dh * dh) * sizeof(float);
 }
 
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
@@ -501,9 +673,14 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
 {
     if (B < 1 || heads < 1 || dh < 1 || dh > 32 || n < 1 || nmem < 0 || !qkv || !mem_kv || !out || !ws)
         return RDQ_E_INVALID;
-    float *ctx = (float *)ws;
-    hipLaunchKernelGGL(k_la_context, dim3(dh, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, ctx);
-    hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx, out);
+    float *stats = (float *)ws;
+    float *part = stats + (size_t)B * heads * dh * 2;
+    const int nch = la_chunks(n, nmem);
+    hipLaunchKernelGGL(k_la_stats, dim3((B * heads * dh + 3) / 4), dim3(256), 0, st, B, heads, dh, n, nmem, qkv,
+                       mem_kv, stats);
+    hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, stats, part);
+    hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, nch, scale, qkv,
+                       stats, part, out);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -511,11 +688,11 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
 int rdq_full_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, const float *qkv,
                        const float *mem_kv, float *out, hipStream_t st)
 {
-    if (B < 1 || heads < 1 || dh != 32 || n < 1 || n > 256 || nmem < 0 || !qkv || !mem_kv || !out)
-        return RDQ_E_INVALID;
-    const size_t lds = (size_t)2 * (nmem + n) * (dh + 1) * sizeof(float);
-    if (lds > 64 * 1024) return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_full_attn<32>, dim3(heads, B), dim3(256), lds, st, heads, n, nmem, qkv, mem_kv, out);
+    if (B < 1 || heads < 1 || dh != 32 || n < 1 || nmem < 0 || !qkv || !mem_kv || !out) return RDQ_E_INVALID;
+    const size_t lds = ((size_t)2 * (nmem + n) * (dh + 1) + (size_t)256 * (dh + 3)) * sizeof(float);
+    if (lds > 160 * 1024) return RDQ_E_INVALID;
+    hipLaunchKernelGGL(k_full_attn<32>, dim3(heads, B, (n + FA_QB - 1) / FA_QB), dim3(256), lds, st, heads, n, nmem,
+                       qkv, mem_kv, out);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

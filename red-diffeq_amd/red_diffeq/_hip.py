@@ -11,6 +11,8 @@ import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libred_diffeq_hip.so")
+if os.environ.get("RDQ_EXP_LIB"):        # timing experiments only (tools/exp_variants.sh)
+    LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "exp", os.environ["RDQ_EXP_LIB"])
 
 c_int32, c_int64, c_float, c_double, c_size_t, c_void_p = (
     ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
@@ -68,8 +70,9 @@ SIGNATURES = {
     "rdq_smooth_reg_backward": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                           c_void_p, c_void_p]),
     # include/red_diffeq_unet.h
+    "rdq_conv2d_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p]),
+                             c_void_p, c_size_t, c_void_p]),
     "rdq_group_norm_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
     "rdq_group_norm_silu": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -77,7 +80,7 @@ SIGNATURES = {
     "rdq_linear": (c_int32, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                              c_void_p]),
     "rdq_sinusoidal_emb": (c_int32, [c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
-    "rdq_linear_attention_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_linear_attention_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "rdq_linear_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p]),
     "rdq_full_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,

@@ -43,8 +43,11 @@ def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
     d = _hip.ConvDesc(B=B, cin1=cin1, cin2=cin2, H=H, W=W, cout=cout, kh=kh, kw=kw, pad=pad, in_mode=mode)
     y = torch.empty(B, cout, H, W, device=x.device, dtype=torch.float32)
     res = _f(residual)
-    _hip.check(_hip.lib().rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(w.contiguous()),
-                                     _hip.ptr(conv.bias), _hip.ptr(res), _hip.ptr(y), _hip.stream_of(x)),
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+    _hip.check(L.rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(w.contiguous()),
+                            _hip.ptr(conv.bias), _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, _hip.stream_of(x)),
                "rdq_conv2d")
     return y
 
@@ -105,7 +108,8 @@ def linear_attention(x, m):
     xn = rmsnorm(x, m.norm.g)
     qkv = conv2d(xn, m.to_qkv)
     L = _hip.lib()
-    ws = torch.empty(int(L.rdq_linear_attention_ws_bytes(B, heads, dh)), dtype=torch.uint8, device=x.device)
+    ws = torch.empty(int(L.rdq_linear_attention_ws_bytes(B, heads, dh, H * W, m.mem_kv.shape[-1])),
+                     dtype=torch.uint8, device=x.device)
     out = torch.empty(B, heads * dh, H, W, device=x.device, dtype=torch.float32)
     _hip.check(L.rdq_linear_attention(B, heads, dh, H * W, m.mem_kv.shape[-1], float(m.scale), _hip.ptr(qkv),
                                       _hip.ptr(m.mem_kv.contiguous()), _hip.ptr(out), _hip.ptr(ws),

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build timing-experiment variants of the FWI library (knockouts that give WRONG results; never
+# used by tests or the product): lib/exp/<name>.so.  Run on the GPU with RDQ_EXP_LIB=<name>.so.
+cd "$(dirname "$0")/../red-diffeq_amd"
+mkdir -p lib/exp build/exp
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -ffp-contract=off -fno-slp-vectorize"
+build() {  # name, defines
+  /opt/rocm/bin/hipcc $FL $2 -c -o build/exp/$1.o csrc/fwi.hip &&
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/exp/$1.so build/exp/$1.o build/unet.o build/loop.o
+}
+build nobarrier "-DRDQ_EXP_NOBARRIER" &
+build sweeponce "-DRDQ_EXP_SWEEP_ONCE=1" &
+build noload "-DRDQ_EXP_NOPLOAD=1 -DRDQ_EXP_NOSTORE=1" &
+wait
+ls -la lib/exp
