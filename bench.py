@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-loop", action="store_true", help="skip the InversionEngine per-iteration wallclock")
     p.add_argument("--cpu-sample-shots", type=int, default=4)
+    p.add_argument("--no-red", action="store_true", help="skip the configs[2] RED-DiffEq loop timing")
     return p.parse_args()
 
 
@@ -90,6 +91,42 @@ def loop_wallclock(fwi, mu0, vt, y, a, dev, world):
     t_w = run(a.warmup)
     t_all = run(a.warmup + a.steps)
     return round((t_all - t_w) / a.steps * 1e3, 4)
+
+
+def red_loop_wallclock(dev, a, ns=32):
+    """configs[2]: CurveVel-A, 32 shots, the full RED-DiffEq loop (HIP forward + adjoint + U-Net
+    regulariser + Adam + metrics) through the drop-in InversionEngine, lambda 0.75, lr 0.03,
+    random-init U-Net (dim 64, mults 1,2,4,8: the reference architecture; no checkpoint offline).
+    Returns ms per iteration over iterations [warmup, warmup + steps)."""
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.models.diffusion import GaussianDiffusion, Unet
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import prepare_initial_model, s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.ssim import SSIM
+    from red_diffeq.utils.synthetic import make_model
+    torch.manual_seed(8888)
+    ctx = dict(n_grid=70, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns)
+    fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
+    vt = torch.from_numpy(make_model("curvevel", 70, 70, seed=8888, batch=1))
+    with torch.no_grad():
+        y = fwi(v_normalize(vt).to(dev))
+    mu = torch.nn.functional.pad(prepare_initial_model(vt, "smoothed", sigma=10.0), (1, 1, 1, 1))
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1)
+    diff = GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                             objective="pred_noise").to(dev)
+    eng = InversionEngine(diff, SSIM(), regularization="diffusion", sigma_x0=1e-4, show_progress=False)
+
+    def run(ts):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization="diffusion")
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(1)
+    t_w = run(a.warmup)
+    t_all = run(a.warmup + a.steps)
+    return round((t_all - t_w) / a.steps * 1e3, 3)
 
 
 def main():
@@ -151,6 +188,10 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     t_step = el.item() / a.steps
+    dbg = os.environ.get("RDQ_DEBUG_STATUS")
+    if dbg:
+        print("after timed loop:", fwi._plan(70, 70, dev).debug_words(), file=sys.stderr, flush=True)
+    fwi.check()          # raises if any persistent launch of the timed region gave up a hand-off
 
     # ---- phase timing with HIP events on the stream the graphs/kernels are launched on ----
     plan = fwi._plan(70, 70, dev)
@@ -172,6 +213,9 @@ def main():
         fw_ms.append(ev[0].elapsed_time(ev[1]))
         adj_ms.append(ev[2].elapsed_time(ev[3]))
         del hist
+    if dbg:
+        print("after phases:", plan.debug_words(), file=sys.stderr, flush=True)
+    fwi.check()
     fw_ms, adj_ms = float(np.median(fw_ms)), float(np.median(adj_ms))
     info = plan.launch_info(B)
     T = info["adj_T"]
@@ -216,6 +260,13 @@ def main():
         # per-iteration wallclock of the drop-in loop itself (InversionEngine.optimize with TV,
         # metrics and histories included), the metric's second half
         out["per_iter_fwi_wallclock_ms"] = loop_wallclock(fwi, mu0, vt, y, a, dev, world)
+    if world == 1 and not a.no_red:
+        out["configs2_red_loop"] = {"workload": "configs[2]: OpenFWI CurveVel-A 70x70, 32 shots, full RED-DiffEq "
+                                                "loop (fwd+adj + U-Net regulariser + Adam + metrics), random-init U-Net",
+                                    "ms_per_iter": red_loop_wallclock(dev, a),
+                                    "shot_timesteps_per_s_incl_unet": None}
+        r = out["configs2_red_loop"]
+        r["shot_timesteps_per_s_incl_unet"] = round(32 * nt / (r["ms_per_iter"] * 1e-3), 1)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, vtrue[:1], a.cpu_sample_shots)
     if rank == 0:

@@ -82,9 +82,13 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
  *                          registers instead of loading the three K3 fields (identical results);
  *   RDQ_VARIANT_ADJ_EXACT  the persistent adjoint keeps the oracle's exact fp32 operation order (gA
  *                          bit-identical to oracle/fwi_oracle.c) instead of contracting into FMAs and
- *                          accumulating the sponge term per cell in fp32 (faster; within 1e-6). */
+ *                          accumulating the sponge term per cell in fp32 (faster; within 1e-6);
+ *   RDQ_VARIANT_NO_XCD_LOCAL the persistent kernels publish every neighbour hand-off write-through
+ *                          (sc1) instead of keeping whole slices on one XCD (read from HW_REG_XCC_ID)
+ *                          with L2-resident hand-offs (identical results; slower). */
 #define RDQ_VARIANT_FWD_GEN 1
 #define RDQ_VARIANT_ADJ_EXACT 2
+#define RDQ_VARIANT_NO_XCD_LOCAL 4
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the
@@ -94,6 +98,10 @@ int rdq_fwi_set_persistent(rdq_fwi_plan *plan, int32_t mode);
 /* Synchronises `stream` and reports (then clears) a persistent-kernel hand-off timeout:
  * 0, or RDQ_E_HANDOFF when some launch since the last call gave up waiting for a neighbour. */
 int rdq_fwi_status(rdq_fwi_plan *plan, hipStream_t stream);
+/* Diagnostics (synchronises the device): the plan's 32 status words: [0] hand-off status
+ * (1 = neighbour timeout, 2 = launch not resident), [16..23] workgroups per XCD of the last
+ * persistent launch. */
+int rdq_fwi_debug_words(rdq_fwi_plan *plan, uint32_t out[32]);
 /* Which kernels a forward / adjoint call for batch B runs: out = {forward persistent region
  * height in waves (0 = chunked), the same for the adjoint, forward steps per epoch/launch,
  * adjoint steps per epoch/launch}. */

@@ -626,6 +626,15 @@ __device__ __forceinline__ void gran_put(__amdgpu_buffer_rsrc_t r, int voff, int
     x.y = tag;
     __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, CP_SC1);
 }
+// XCD-local hand-off: a plain store stays in the producer XCD's L2, where a same-XCD consumer's
+// sc1 (L1-bypassing, L2-served) load sees it without the write-through round trip to memory
+__device__ __forceinline__ void gran_put_l2(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v)
+{
+    u32x2 x;
+    x.x = __float_as_uint(v);
+    x.y = tag;
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, 0);
+}
 __device__ __forceinline__ u32x2 gran_get(__amdgpu_buffer_rsrc_t r, int voff, int soff)
 {
     return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, CP_SC1);
@@ -638,6 +647,74 @@ __device__ __forceinline__ int wrap_row(int uz, int Hp)
     return uz >= Hp ? uz - Hp : uz;
 }
 
+// Slice / tile assignment of a persistent launch by the XCD each workgroup actually runs on.
+// Every workgroup reads its XCD id (s_getreg HW_REG_XCC_ID), takes a slot on that XCD's arrival
+// counter and waits until all gridDim.x workgroups have arrived (the launch is fully resident by
+// construction: the host sizes the grid to the occupancy query).  From the final per-XCD counts
+// every workgroup derives the same assignment: whole (model, shot) slices go to single XCDs in XCD
+// order ("local" slices: every hand-off between their tiles stays inside one L2, so granules are
+// published with plain stores that stay in that L2); slices that do not fit whole on one XCD are
+// dealt over the leftover workgroups ("global": write-through sc1 granules, as before).
+// Correctness never depends on the placement guess: the XCD id is read, not assumed, and every
+// granule carries its epoch tag, so a stale read is re-polled, never consumed.
+struct PtTile { int tx, ty, tile, sl; bool valid, local; };
+constexpr unsigned long long PT_ARRIVE_TICKS = 10000000ull;   // 100 ms
+
+__device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
+{
+    __shared__ int sh[3];
+    unsigned *cnt = status + 16;                         // [8] per-XCD arrivals (zeroed per launch)
+    if (threadIdx.x == 0) {
+        unsigned x = 0;
+        if (xcd_mode) {
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            x &= 7u;
+        }
+        const unsigned slot = __hip_atomic_fetch_add(cnt + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned n[8], tot = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        for (;;) {
+            tot = 0;
+            for (int i = 0; i < 8; ++i) {
+                n[i] = __hip_atomic_load(cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tot += n[i];
+            }
+            if (tot >= gridDim.x) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > PT_ARRIVE_TICKS) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        int sl = -1, tile = 0, local = 0;
+        if (ok) {
+            const int Tt = g.ntiles, S = g.B * g.ns_grp;
+            int placed = 0, take[8];
+            for (int i = 0; i < 8; ++i) {
+                take[i] = xcd_mode ? min((int)n[i] / Tt, S - placed) : 0;
+                placed += take[i];
+            }
+            int base = 0;
+            for (int i = 0; i < (int)x; ++i) base += take[i];
+            if ((int)slot < take[x] * Tt) {
+                sl = base + (int)slot / Tt; tile = (int)slot % Tt; local = 1;
+            } else {
+                int r = (int)slot - take[x] * Tt;
+                for (int i = 0; i < (int)x; ++i) r += (int)n[i] - take[i] * Tt;
+                if (r < (S - placed) * Tt) { sl = placed + r / Tt; tile = r % Tt; }
+            }
+        } else {
+            __hip_atomic_store(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // not resident
+        }
+        sh[0] = sl; sh[1] = tile; sh[2] = local;
+    }
+    __syncthreads();
+    PtTile t;
+    t.sl = sh[0]; t.tile = sh[1]; t.local = sh[2] != 0;
+    t.valid = t.sl >= 0;
+    t.ty = t.tile / g.tiles_x;
+    t.tx = t.tile - t.ty * g.tiles_x;
+    return t;
+}
+
 // Region geometry of the persistent kernels (flat locals so every block-/wave-uniform value stays
 // provably uniform: SGPRs and scalar branches, never waterfall loops).  Row classes are
 // wave-uniform bit masks; lane classes: xin (own interior column), bx (interior column within H of
@@ -647,8 +724,9 @@ __device__ __forceinline__ int wrap_row(int uz, int Hp)
     constexpr int R = TB_R, RH = (NW_) * TB_R, H = 2 * T, IW = 64 - 2 * H, IH = RH - 2 * H;        \
     const int lane = threadIdx.x & 63;                                                              \
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                \
-    const TileId ti = decode_tile(blockIdx.x, g.tiles_x, g.ntiles, g.B * g.ns_grp);                 \
+    const PtTile ti = pt_assign(g, a.status, a.xcd_mode);                                           \
     if (!ti.valid) return;                                                                          \
+    const bool gl2 = ti.local;                     /* uniform: XCD-local slice, L2 hand-offs */      \
     const int b = __builtin_amdgcn_readfirstlane(ti.sl / g.ns_grp);                                 \
     const int s = __builtin_amdgcn_readfirstlane(g.s_off + (ti.sl - b * g.ns_grp));                 \
     const int bs = b * g.ns + s;                                                                    \
@@ -699,6 +777,10 @@ __device__ __forceinline__ int wrap_row(int uz, int Hp)
                     live = false;                                                                   \
                 else if (__builtin_amdgcn_s_memrealtime() - t0_ > PT_TIMEOUT_TICKS) {               \
                     __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   \
+                    if (lane == 0) {                    /* diagnostics: rdq_fwi_debug_words */      \
+                        a.status[1] = (TAG); a.status[2] = blockIdx.x; a.status[3] = bs;            \
+                        a.status[4] = tile; a.status[5] = gl2; a.status[6] = w;                      \
+                    }                                                                               \
                     live = false;                                                                   \
                 }                                                                                   \
             }                                                                                       \
@@ -716,8 +798,13 @@ __device__ __forceinline__ int wrap_row(int uz, int Hp)
         if (!((rin >> r) & 1u)) continue;                                                           \
         if (((rby >> r) & 1u) ? xin : xb) {                                                         \
             const int sof_ = PT_ROFS(r) * 8;                                                        \
-            gran_put(GR, vo8, sof_, (TAG), V0[r]);                                                  \
-            gran_put(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                                      \
+            if (gl2) {                                                                              \
+                gran_put_l2(GR, vo8, sof_, (TAG), V0[r]);                                           \
+                gran_put_l2(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                               \
+            } else {                                                                                \
+                gran_put(GR, vo8, sof_, (TAG), V0[r]);                                              \
+                gran_put(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                                  \
+            }                                                                                       \
         }                                                                                           \
     }
 
@@ -739,6 +826,7 @@ struct FwdPtArgs {
     unsigned *status;
     unsigned long long *prof;            // nullable: [0] hand-off, [1] steps, [2] publish (10 ns ticks), [3] waves
     int nt;
+    int xcd_mode;                        // 1: XCD-local slices (pt_assign), 0: all hand-offs write-through
 };
 
 // one forward step P_{n+1} = temp1 P_n - temp2 P_{n-1} + alpha N(P_n) (+ source), pde.py:79-81
@@ -892,6 +980,7 @@ struct AdjPtArgs {
     unsigned *status;
     unsigned long long *prof;            // nullable, as FwdPtArgs
     int nt, nblk;
+    int xcd_mode;
 };
 
 // P_{k-1} (history slot K) rows uz0-2 .. uz0+9 into PD
@@ -1343,6 +1432,7 @@ struct rdq_fwi_plan {
     std::vector<unsigned long long> prof_host;
     bool graphs = true;
     int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves)
+    int xcd_mode = 1;           // persistent kernels: XCD-local slices with L2 hand-offs (pt_assign)
     int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
     int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
@@ -1569,13 +1659,14 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.g.ntiles = a.g.tiles_x * ((p->Hp + ih - 1) / ih);
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
-    a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof;
+    a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof; a.xcd_mode = p->xcd_mode;
     // consecutive shot groups, one resident launch each (granules live at per-slice offsets, so
     // one zeroing serves every group)
     for (int s0 = 0; s0 < p->g.ns; s0 += per) {
         a.g.s_off = s0;
         a.g.ns_grp = std::min(per, p->g.ns - s0);
         const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
         else launch_fwd_pt<8>(T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
@@ -1602,10 +1693,12 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + PROF_WORDS : nullptr;
+    a.xcd_mode = p->xcd_mode;
     for (int s0 = 0; s0 < p->g.ns; s0 += per) {
         a.g.s_off = s0;
         a.g.ns_grp = std::min(per, p->g.ns - s0);
         const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
         else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }
         RDQ_CHECK(hipGetLastError());
@@ -1695,6 +1788,16 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     return join_chains(p, st, S);
 }
 
+// destroy every cached graph; a graph may still be queued or running (asynchronous launches), so
+// the device is drained first
+void drop_graphs(rdq_fwi_plan *p)
+{
+    if (p->cache.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+    p->cache.clear();
+}
+
 template <class F>
 int run_cached(rdq_fwi_plan *p, int kind, int B, std::initializer_list<const void *> key, hipStream_t st, F &&launch)
 {
@@ -1722,9 +1825,14 @@ int run_cached(rdq_fwi_plan *p, int kind, int B, std::initializer_list<const voi
     (void)hipGraphDestroy(graph);
     RDQ_CHECK(ie);
     e.last_use = ++p->tick;
-    if (p->cache.size() >= 8) {
+    if (p->cache.size() >= 16) {
         auto old = std::min_element(p->cache.begin(), p->cache.end(),
                                     [](const GraphEntry &a, const GraphEntry &b) { return a.last_use < b.last_use; });
+        // the evicted graph may still be queued or running on `st` (everything here is
+        // asynchronous): destroying an executing graph frees its kernel-argument storage under the
+        // running persistent kernel, so drain the stream first (evictions are rare: a steady loop
+        // replays cached graphs)
+        RDQ_CHECK(hipStreamSynchronize(st));
         (void)hipGraphExecDestroy(old->exec);
         p->cache.erase(old);
     }
@@ -1785,7 +1893,7 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
 int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
 {
     if (!p) return 0;
-    for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+    drop_graphs(p);
     if (p->cap) (void)hipStreamDestroy(p->cap);
     for (auto st : p->aux) (void)hipStreamDestroy(st);
     for (auto e : p->evs) (void)hipEventDestroy(e);
@@ -1812,7 +1920,7 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
         chains > 16)
         return RDQ_E_INVALID;
     if (p->fwd_T != fwd_steps || p->adj_T != adj_steps || p->chains != chains) {   // graphs encode these
-        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+        drop_graphs(p);
         p->cache.clear();
     }
     p->fwd_T = fwd_steps;
@@ -1823,14 +1931,16 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
 
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
-    if (!p || (flags & ~3)) return RDQ_E_INVALID;
+    if (!p || (flags & ~7)) return RDQ_E_INVALID;
     const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0, fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0;
-    if (p->fwd_gen != gen || p->adj_fma != fma) {
-        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+    const int xcd = (flags & RDQ_VARIANT_NO_XCD_LOCAL) ? 0 : 1;
+    if (p->fwd_gen != gen || p->adj_fma != fma || p->xcd_mode != xcd) {
+        drop_graphs(p);
         p->cache.clear();
     }
     p->fwd_gen = gen;
     p->adj_fma = fma;
+    p->xcd_mode = xcd;
     return 0;
 }
 
@@ -1838,7 +1948,7 @@ int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 {
     if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12)) return RDQ_E_INVALID;
     if (p->persist != mode) {
-        for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);
+        drop_graphs(p);
         p->cache.clear();
     }
     p->persist = mode;
@@ -1858,7 +1968,7 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[4])
 int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
 {
     if (!p) return RDQ_E_INVALID;
-    for (auto &e : p->cache) (void)hipGraphExecDestroy(e.exec);   // graphs bake the pointer in
+    drop_graphs(p);   // graphs bake the pointer in
     p->cache.clear();
     if (enable && !p->d_prof) {
         RDQ_CHECK(hipMalloc(&p->d_prof, 2 * PROF_WORDS * sizeof(unsigned long long)));
@@ -1903,6 +2013,14 @@ int rdq_fwi_status(rdq_fwi_plan *p, hipStream_t st)
         RDQ_CHECK(hipStreamSynchronize(st));
         return RDQ_E_HANDOFF;
     }
+    return 0;
+}
+
+int rdq_fwi_debug_words(rdq_fwi_plan *p, uint32_t out[32])
+{
+    if (!p || !out) return RDQ_E_INVALID;
+    RDQ_CHECK(hipDeviceSynchronize());
+    RDQ_CHECK(hipMemcpy(out, p->d_status, 32 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -1962,8 +2080,9 @@ int rdq_fwi_forward(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, floa
     int per = 0;
     if (const int nw = persistent_nw(p, B, false, &per)) {
         if (!ring) return RDQ_E_INVALID;   // the persistent kernel's hand-off granules live in `ring`
-        return run_cached(p, (hist ? 3 : 4) + 16 * nw, B, {coeffs, seis, hist, ring}, st,
-                          [&](hipStream_t s) { return launch_forward_pt(p, B, nw, per, coeffs, seis, hist, ring, s); });
+        // direct launch (one kernel + memsets per shot group: nothing for a graph to amortise; the
+        // arrival counters of pt_assign are zeroed by a stream-ordered memset right before it)
+        return launch_forward_pt(p, B, nw, per, coeffs, seis, hist, ring, st);
     }
     return run_cached(p, hist ? 0 : 1, B, {coeffs, seis, hist, ring}, st,
                       [&](hipStream_t s) { return launch_forward(p, B, coeffs, seis, hist, ring, s); });
@@ -1976,9 +2095,7 @@ int rdq_fwi_adjoint(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, cons
     if (!p || !coeffs || !hist || !dseis || !ring || !gA || !gk || !gbeta || B < 1) return RDQ_E_INVALID;
     int per = 0;
     if (const int nw = persistent_nw(p, B, true, &per))
-        return run_cached(p, 5 + 16 * nw, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
-            return launch_adjoint_pt(p, B, nw, per, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
-        });
+        return launch_adjoint_pt(p, B, nw, per, coeffs, hist, dseis, ring, gA, gk, gbeta, st);
     return run_cached(p, 2, B, {coeffs, hist, dseis, ring, gA, gk, gbeta}, st, [&](hipStream_t s) {
         return launch_adjoint(p, B, coeffs, hist, dseis, ring, gA, gk, gbeta, s);
     });

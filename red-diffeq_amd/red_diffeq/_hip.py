@@ -50,6 +50,7 @@ SIGNATURES = {
     "rdq_fwi_set_variant": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_persistent": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_status": (c_int32, [c_void_p, c_void_p]),
+    "rdq_fwi_debug_words": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "rdq_fwi_set_profile": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_profile_waves": (c_int32, [c_void_p, c_int32, ctypes.POINTER(ctypes.c_uint64), c_size_t]),
     "rdq_fwi_launch_info": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_int32)]),

@@ -10,6 +10,7 @@ hand-written discrete adjoint (K2 + K4) as the autograd backward — where the r
 ~5 MB-per-shot-step autograd tape, this keeps one fp32 wavefield per step (store-all history).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -75,10 +76,11 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
-    def set_variant(self, fwd_gen_coeffs=False, adj_exact=False):
+    def set_variant(self, fwd_gen_coeffs=False, adj_exact=False, xcd_local=True):
         """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
-        the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction."""
-        flags = (1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0)
+        the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction; xcd_local:
+        persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs."""
+        flags = (1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_persistent(self, enable):
@@ -89,6 +91,12 @@ class FwiPlan:
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         _hip.check(self.lib.rdq_fwi_status(self.handle, ctypes.c_void_p(stream)), "rdq_fwi_status")
+
+    def debug_words(self):
+        """[status, per-XCD workgroup counts of the last persistent launch] (synchronises)."""
+        out = (ctypes.c_uint32 * 32)()
+        _hip.check(self.lib.rdq_fwi_debug_words(self.handle, out), "rdq_fwi_debug_words")
+        return int(out[0]), [int(v) for v in out[1:7]], [int(v) for v in out[16:24]]
 
     def launch_info(self, B):
         """{'fwd_persistent', 'adj_persistent', 'fwd_T', 'adj_T'} of a call with batch B."""
@@ -264,6 +272,10 @@ class FWIForward(nn.Module):
                 raise ValueError("empty shot range")
             self._plans[key] = FwiPlan(nz, nx, c, self.sample_temporal, isx, isz, igx, igz,
                                        ricker(c["f"], c["dt"], c["nt"]), device)
+            if os.environ.get("RDQ_NO_XCD_LOCAL"):       # A/B switches (tools/, experiments)
+                self._plans[key].set_variant(xcd_local=False)
+            if os.environ.get("RDQ_NO_GRAPHS"):
+                self._plans[key].set_graphs(False)
         return self._plans[key]
 
     def _fused_denorm(self):

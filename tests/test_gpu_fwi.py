@@ -236,6 +236,32 @@ def test_persistent_shot_groups_openfwi_ns20(cuda):
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-6
 
 
+@pytest.mark.parametrize("ns,B", [(8, 1), (3, 2), (20, 1)])
+def test_persistent_xcd_local_equals_write_through(cuda, ns, B):
+    """XCD-local slices (pt_assign: L2-resident granule hand-offs between the tiles of a slice on
+    one XCD) vs every hand-off write-through: identical seismograms and adjoint accumulators."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=70, nt=240, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns)
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vnorm(make_model("curvevel", 70, 70, seed=11, batch=B))).to(cuda)
+    plan = fwi._plan(70, 70, v.device)
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(3)
+    dseis = torch.from_numpy(rng.standard_normal((B, ns, sz.nrec, plan.ng)).astype(np.float32)).to(cuda)
+    out = {}
+    for xl in (True, False):
+        plan.set_variant(adj_exact=True, xcd_local=xl)
+        assert plan.launch_info(B)["fwd_persistent"]
+        coeffs, vstat = plan.coeffs(v, 0)
+        seis, hist = plan.forward(coeffs, B, keep_history=True)
+        gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+        plan.status()
+        out[xl] = (seis.cpu().numpy(), gA.cpu().numpy(), gb.cpu().numpy())
+        del hist
+    for a, b in zip(out[True], out[False]):
+        assert bits_equal(a, b)
+
+
 def test_damp_profile_vs_reference(cuda):
     """Sponge (get_Abc, columns overwrite rows) as kappa/dt vs the reference fixture."""
     z = load_golden("damp")

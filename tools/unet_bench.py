@@ -40,6 +40,45 @@ def conv_flops(net, x, t):
     return tot[0]
 
 
+def conv_shapes(net, x, t):
+    """(x shape, x2 channels, conv, mode, residual?) of every convolution of one forward."""
+    from red_diffeq.models import unet_ops as ops
+    calls = []
+    orig = ops.conv2d
+
+    def rec(x, conv, x2=None, mode=ops.PLAIN, residual=None):
+        calls.append((tuple(x.shape), 0 if x2 is None else x2.shape[1], conv, mode, residual is not None))
+        return orig(x, conv, x2=x2, mode=mode, residual=residual)
+
+    ops.conv2d = rec
+    try:
+        with torch.no_grad():
+            net(x, t)
+    finally:
+        ops.conv2d = orig
+    return calls
+
+
+def per_conv(net, x, t, reps):
+    from red_diffeq.models import unet_ops as ops
+    rows = []
+    for xs, c2, conv, mode, has_res in conv_shapes(net, x, t):
+        xa = torch.randn(xs, device="cuda")
+        x2 = torch.randn(xs[0], c2, xs[2], xs[3], device="cuda") if c2 else None
+        y = ops.conv2d(xa, conv, x2=x2, mode=mode)
+        res = torch.randn_like(y) if has_res else None
+        ms = time_fn(lambda: ops.conv2d(xa, conv, x2=x2, mode=mode, residual=res), reps)
+        cout, cin, kh, kw = conv.weight.shape
+        fl = 2 * y.shape[0] * y.shape[2] * y.shape[3] * cout * cin * kh * kw
+        rows.append({"x": list(xs), "cin2": c2, "cout": cout, "k": kh, "mode": mode, "HW": y.shape[2],
+                     "us": round(ms * 1e3, 2), "tflops": round(fl / ms / 1e9, 2)})
+    rows.sort(key=lambda r: -r["us"])
+    tot = sum(r["us"] for r in rows)
+    print(json.dumps({"convs": len(rows), "sum_us": round(tot, 1)}))
+    for r in rows:
+        print(json.dumps(r))
+
+
 def time_fn(fn, reps):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(3):
@@ -60,6 +99,7 @@ def main():
     ap.add_argument("--B", type=int, nargs="+", default=[1, 4])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--H", type=int, default=72)
+    ap.add_argument("--per-conv", action="store_true")
     a = ap.parse_args()
     import unet_torch_ref as R
     torch.manual_seed(0)
@@ -67,6 +107,9 @@ def main():
     for B in a.B:
         x = torch.randn(B, 1, a.H, a.H, device="cuda")
         t = torch.randint(0, 1000, (B,), device="cuda")
+        if a.per_conv:
+            per_conv(net, x, t, a.reps)
+            continue
         fl = conv_flops(net, x, t)
         with torch.no_grad():
             hip_ms = time_fn(lambda: net(x, t), a.reps)
