@@ -108,9 +108,10 @@ int rdq_fwi_debug_words(rdq_fwi_plan *plan, uint32_t out[32]);
 int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[4]);
 /* Diagnostics: 1 = the persistent kernels accumulate per-wave phase times (s_memrealtime, 10 ns
  * ticks); read_profile synchronises the device, returns and clears them:
- * out[0..3] forward {hand-off wait, time steps, publish, waves}, out[4..7] the same for the adjoint. */
+ * out[0..5] forward {hand-off wait, time steps, publish, waves, first sweep pass, sweep passes},
+ * out[6..11] the same for the adjoint. */
 int rdq_fwi_set_profile(rdq_fwi_plan *plan, int32_t enable);
-int rdq_fwi_read_profile(rdq_fwi_plan *plan, uint64_t out[8]);
+int rdq_fwi_read_profile(rdq_fwi_plan *plan, uint64_t out[12]);
 /* Per-wave records of the last read_profile: out[(block * 16 + wave) * 3 + {0,1,2}] = {hand-off,
  * steps, publish} ticks of the forward (adj = 0) or adjoint (adj = 1) kernel. */
 int rdq_fwi_profile_waves(rdq_fwi_plan *plan, int32_t adj, uint64_t *out, size_t count);

@@ -587,7 +587,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 // Region height is a template parameter (NW waves x 8 rows): 12 waves -> 64 x 96 regions, one
 // workgroup per CU at OpenFWI size (28 tiles x 8 shots = 224 <= 256 CUs).
 //
-// Granule buffer (inside the caller's `ring`): [2 epoch parity][2 level][B][ns][Hp][ld] u64,
+// Granule buffer (inside the caller's `ring`): [2 epoch parity][B][ns][Hp][ld] x 16-B granules,
 // zeroed before each launch; tag = epoch index (>= 1) so a zeroed granule never matches.
 // timing-experiment knockouts (0 in the product build; tools/exp_variants.sh builds the others)
 #ifndef RDQ_EXP_SWEEP_ONCE
@@ -619,25 +619,31 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, int vo
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
 }
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void gran_put(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v)
+// One cell's hand-off granule = BOTH wavefield levels, 16 bytes {v0, tag, v1, tag}: each 8-byte
+// half carries its own epoch tag, so a read torn between the halves is still caught by the tag
+// check (the guarantee used is only that an aligned 8-byte store is seen whole), and a sweep or a
+// publish is one dwordx4 instruction per row instead of two dwordx2.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 gran2(unsigned tag, float v0, float v1)
 {
-    u32x2 x;
-    x.x = __float_as_uint(v);
-    x.y = tag;
-    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, CP_SC1);
+    u32x4 x;
+    x.x = __float_as_uint(v0); x.y = tag; x.z = __float_as_uint(v1); x.w = tag;
+    return x;
+}
+__device__ __forceinline__ void gran_put(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v0, float v1)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(gran2(tag, v0, v1), r, voff, soff, CP_SC1);
 }
 // XCD-local hand-off: a plain store stays in the producer XCD's L2, where a same-XCD consumer's
 // sc1 (L1-bypassing, L2-served) load sees it without the write-through round trip to memory
-__device__ __forceinline__ void gran_put_l2(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v)
+// (tools/probe/l2_probe.hip)
+__device__ __forceinline__ void gran_put_l2(__amdgpu_buffer_rsrc_t r, int voff, int soff, unsigned tag, float v0, float v1)
 {
-    u32x2 x;
-    x.x = __float_as_uint(v);
-    x.y = tag;
-    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(gran2(tag, v0, v1), r, voff, soff, 0);
 }
-__device__ __forceinline__ u32x2 gran_get(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+__device__ __forceinline__ u32x4 gran_get(__amdgpu_buffer_rsrc_t r, int voff, int soff)
 {
-    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, CP_SC1);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CP_SC1);
 }
 
 // padded-grid row of region row uz (periodic wrap, pde.py:79); |uz| < 2 Hp
@@ -747,30 +753,31 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
         if (ly < vh + H) rcy |= 1u << r;                                                            \
     }                                                                                               \
     const size_t so = (size_t)bs * g.slice;                                                         \
-    const int vo4 = gx * 4, vo8 = gx * 8;                                                           \
+    const int vo4 = gx * 4, vo16 = gx * 16;                                                         \
     const bool hx = !xin && cx, xb = xin && bx;
 #define PT_ROFS(r) (wrap_row(uz0 + (r), g.Hp) * g.ld)
 
-// Reload the halo cells of two levels V0/V1 from the granule slot GR (level 1 at +lev_bytes),
+// Reload the halo cells of two levels V0/V1 from the granule slot GR (16-byte two-level granules),
 // zero the dead cells.  `live` turns false once this wave gave up (timeout / another's timeout).
 #define PT_SWEEP(GR, TAG, V0, V1)                                                                   \
     {                                                                                               \
         unsigned long long t0_ = 0;                                                                 \
+        const unsigned long long ts_ = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;               \
         for (unsigned pass_ = 0; live; ++pass_) {                                                   \
             bool ok_ = true;                                                                        \
             _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
                 const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                      \
                 if (!rowin_ && !rowcy_) continue;                                                   \
                 if (rowin_ ? hx : cx) {                                                             \
-                    const int sof_ = PT_ROFS(r) * 8;                                                \
-                    const u32x2 x0_ = gran_get(GR, vo8, sof_);                                      \
-                    const u32x2 x1_ = gran_get(GR, vo8, sof_ + lev_bytes);                          \
-                    ok_ = ok_ && x0_.y == (TAG) && x1_.y == (TAG);                                  \
-                    V0[r] = __uint_as_float(x0_.x);                                                 \
-                    V1[r] = __uint_as_float(x1_.x);                                                 \
+                    const u32x4 x_ = gran_get(GR, vo16, PT_ROFS(r) * 16);                           \
+                    ok_ = ok_ && x_.y == (TAG) && x_.w == (TAG);                                    \
+                    V0[r] = __uint_as_float(x_.x);                                                  \
+                    V1[r] = __uint_as_float(x_.z);                                                  \
                 }                                                                                   \
             }                                                                                       \
-            if (RDQ_EXP_SWEEP_ONCE || __all(ok_)) break;                                            \
+            const bool done_ = RDQ_EXP_SWEEP_ONCE || __all(ok_);                                     \
+            if (a.prof && pass_ == 0) tfp += __builtin_amdgcn_s_memrealtime() - ts_;                 \
+            if (done_) { npass += pass_ + 1; break; }                                               \
             if (pass_ == 0) t0_ = __builtin_amdgcn_s_memrealtime();                                 \
             if ((pass_ & 15) == 15) {                                                               \
                 if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)   \
@@ -797,14 +804,8 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
     _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                 \
         if (!((rin >> r) & 1u)) continue;                                                           \
         if (((rby >> r) & 1u) ? xin : xb) {                                                         \
-            const int sof_ = PT_ROFS(r) * 8;                                                        \
-            if (gl2) {                                                                              \
-                gran_put_l2(GR, vo8, sof_, (TAG), V0[r]);                                           \
-                gran_put_l2(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                               \
-            } else {                                                                                \
-                gran_put(GR, vo8, sof_, (TAG), V0[r]);                                              \
-                gran_put(GR, vo8, sof_ + lev_bytes, (TAG), V1[r]);                                  \
-            }                                                                                       \
+            if (gl2) gran_put_l2(GR, vo16, PT_ROFS(r) * 16, (TAG), V0[r], V1[r]);                   \
+            else gran_put(GR, vo16, PT_ROFS(r) * 16, (TAG), V0[r], V1[r]);                          \
         }                                                                                           \
     }
 
@@ -902,7 +903,6 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     const bool rec = rrow >= 0 && xin && rcv0 >= 0;
     const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
     const size_t L = g.level;
-    const int lev_bytes = (int)(L * 8);
     const int slice_bytes = (int)(g.slice * 4);
     int hv[R];                                            // history store offset of (row, lane), OOB if not own
 #pragma unroll
@@ -910,6 +910,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
     // Wavelet samples of an epoch are loaded BEFORE its hand-off sweep, which ends the loop body:
     // the sweep waits vmcnt(0) on every path into the next epoch (and the prologue waits
     // explicitly), so no step ever waits on a load - a load inside the epoch would be waited for
@@ -947,7 +948,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         PT_PROF(tst)
         if (e + 1 < nep) {
             const unsigned tag = (unsigned)(e + 1);
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, P0, P1)
 #pragma unroll
             for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
@@ -959,6 +960,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     PT_PROF(tsw)
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+        atomicAdd(a.prof + 4, tfp); atomicAdd(a.prof + 5, npass);
         if (blockIdx.x < PROF_WAVES / 16) {
             unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
             raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
@@ -1111,7 +1113,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     double ksum = 0.0;
     float gbacc = 0.0f;
     const size_t L = g.level;
-    const int lev_bytes = (int)(L * 8);
     float PA[PR], PB[PR];
     int pv[PR];                                           // P row (uz0 - 2 + i) offset of this lane
 #pragma unroll
@@ -1135,6 +1136,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
     for (int e = 0; e < nep; ++e) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -1153,7 +1155,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         PT_PROF(tst)
         if (e + 1 < nep) {
             const unsigned tag = (unsigned)(e + 1);
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + so);
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, L0, L1)
             const int kn = a.nt - (e + 1) * T;            // first step k of the next epoch
             ADJ_PLOAD(PA, kn)
@@ -1171,6 +1173,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 #undef DLOAD
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
+        atomicAdd(a.prof + 4, tfp); atomicAdd(a.prof + 5, npass);
         if (blockIdx.x < PROF_WAVES / 16) {
             unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
             raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
@@ -1980,7 +1983,7 @@ int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
     return 0;
 }
 
-int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[8])
+int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[12])
 {
     if (!p || !out) return RDQ_E_INVALID;
     if (!p->d_prof) { for (int i = 0; i < 8; ++i) out[i] = 0; return 0; }
@@ -1989,7 +1992,7 @@ int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[8])
     RDQ_CHECK(hipMemcpy(p->prof_host.data(), p->d_prof, 2 * PROF_WORDS * sizeof(unsigned long long),
                         hipMemcpyDeviceToHost));
     RDQ_CHECK(hipMemset(p->d_prof, 0, 2 * PROF_WORDS * sizeof(unsigned long long)));
-    for (int i = 0; i < 4; ++i) { out[i] = p->prof_host[i]; out[4 + i] = p->prof_host[PROF_WORDS + i]; }
+    for (int i = 0; i < 6; ++i) { out[i] = p->prof_host[i]; out[6 + i] = p->prof_host[PROF_WORDS + i]; }
     return 0;
 }
 

@@ -110,13 +110,14 @@ class FwiPlan:
 
     def read_profile(self):
         """Per-wave average phase times (us) of the persistent kernels since the last read."""
-        out = (ctypes.c_uint64 * 8)()
+        out = (ctypes.c_uint64 * 12)()
         _hip.check(self.lib.rdq_fwi_read_profile(self.handle, out), "rdq_fwi_read_profile")
         res = {}
-        for name, o in (("fwd", 0), ("adj", 4)):
+        for name, o in (("fwd", 0), ("adj", 6)):
             n = max(int(out[o + 3]), 1)
             res[name] = {"wait_us": out[o] / n / 100.0, "steps_us": out[o + 1] / n / 100.0,
-                         "publish_us": out[o + 2] / n / 100.0, "waves": int(out[o + 3])}
+                         "publish_us": out[o + 2] / n / 100.0, "waves": int(out[o + 3]),
+                         "first_pass_us": out[o + 4] / n / 100.0, "passes": out[o + 5] / n}
         return res
 
     def profile_waves(self, adj):
