@@ -8,7 +8,7 @@ build() {  # name, defines
   /opt/rocm/bin/hipcc $FL $2 -c -o build/exp/$1.o csrc/fwi.hip &&
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/exp/$1.so build/exp/$1.o build/unet.o build/loop.o
 }
-build nobarrier "-DRDQ_EXP_NOBARRIER" &
+build drainfirst "-DRDQ_EXP_DRAIN_FIRST=1" &
 build sweeponce "-DRDQ_EXP_SWEEP_ONCE=1" &
 build noload "-DRDQ_EXP_NOPLOAD=1 -DRDQ_EXP_NOSTORE=1" &
 wait
