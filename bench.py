@@ -100,7 +100,7 @@ def loop_wallclock(fwi, mu0, vt, y, a, dev, world):
     return round((t_all - t_w) / a.steps * 1e3, 4)
 
 
-def red_loop_wallclock(dev, a, ns=32):
+def red_loop_wallclock(dev, a, ns=32, family="curvevel"):
     """configs[2]: CurveVel-A, 32 shots, the full RED-DiffEq loop (HIP forward + adjoint + U-Net
     regulariser + Adam + metrics) through the drop-in InversionEngine, lambda 0.75, lr 0.03,
     random-init U-Net (dim 64, mults 1,2,4,8: the reference architecture; no checkpoint offline).
@@ -114,7 +114,7 @@ def red_loop_wallclock(dev, a, ns=32):
     torch.manual_seed(8888)
     ctx = dict(n_grid=70, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns)
     fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
-    vt = torch.from_numpy(make_model("curvevel", 70, 70, seed=8888, batch=1))
+    vt = torch.from_numpy(make_model(family, 70, 70, seed=8888, batch=1))
     with torch.no_grad():
         y = fwi(v_normalize(vt).to(dev))
     mu = torch.nn.functional.pad(prepare_initial_model(vt, "smoothed", sigma=10.0), (1, 1, 1, 1))
@@ -274,6 +274,14 @@ def main():
                                     "shot_timesteps_per_s_incl_unet": None}
         r = out["configs2_red_loop"]
         r["shot_timesteps_per_s_incl_unet"] = round(32 * nt / (r["ms_per_iter"] * 1e-3), 1)
+        # the one published number for this path: RED-DiffEq on OpenFWI CF, ns=5,
+        # 2.25 s/iter on an RTX 3090 (example/example_openfwi.ipynb:657-658), same loop here
+        p_ms = red_loop_wallclock(dev, a, ns=5, family="curvefault")
+        out["published_config_red_loop"] = {
+            "workload": "RED-DiffEq loop, OpenFWI CurveFault 70x70, ns=5, nt=1000, B=1 (the reference notebook's "
+                        "configuration), random-init U-Net", "ms_per_iter": p_ms,
+            "reference_ms_per_iter": 2250.0, "reference_hw": "RTX 3090 (BASELINE.md §1)",
+            "speedup_vs_reference": round(2250.0 / p_ms, 1)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, vtrue[:1], a.cpu_sample_shots, a.cpu_sample_reps)
     if rank == 0:

@@ -4,10 +4,12 @@ Same constructor, same ``ctx`` handling (including the in-place ``sx``/``gx`` mu
 pde.py:16-24), same ``forward(v) -> seis`` contract: (B,1,H,W) fp32, possibly a non-contiguous
 view, to (B, ns, ceil(nt/sample_temporal), ng') fp32, differentiable w.r.t. ``v``.
 
-The compute is the MI355X HIP path (include/red_diffeq_fwi.h): coefficient fields (K3), one
-fused stencil/source/receiver launch per time step replayed from a cached hipGraph (K1), and a
-hand-written discrete adjoint (K2 + K4) as the autograd backward — where the reference records a
-~5 MB-per-shot-step autograd tape, this keeps one fp32 wavefield per step (store-all history).
+The compute is the MI355X HIP path (include/red_diffeq_fwi.h): coefficient fields (K3), the whole
+time loop (stencil + periodic wrap + source injection + receiver sampling + history store) in one
+persistent launch when the survey fits resident on the chip, else temporal-blocked launches of T
+steps replayed from a cached hipGraph (K1), and a hand-written discrete adjoint (K2 + K4) as the
+autograd backward — where the reference records a ~5 MB-per-shot-step autograd tape, this keeps
+one fp32 wavefield per step (store-all history).
 """
 import ctypes
 import os

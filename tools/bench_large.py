@@ -1,0 +1,66 @@
+"""configs[4] (Marmousi-scale) FWI propagator timing on one MI355X: a 500 x 3000 synthetic model
+(740 x 3240 padded, Npad = 2,397,600), `--ns` shots per GPU (16 = 128 shots sharded 8-way), ng = nx
+receivers, nt = 1000, store-all history (16 shots: 155 GB of HBM).  One launch of this size does not
+fit resident on the chip, so the chunked temporal-blocked kernels (k_fwd_tb / k_adj_tb) run it.
+
+Prints one JSON line per blocking depth: forward / adjoint ms, shot-timesteps/s, algorithmic GB/s
+(12·Npad B per forward shot-step, 16·Npad B per adjoint shot-step).
+python tools/bench_large.py [--ns 16] [--nz 500] [--nx 3000] [--nt 1000] [--reps 2]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+from red_diffeq.solvers.pde import FWIForward  # noqa: E402
+from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize, v_normalize  # noqa: E402
+from red_diffeq.utils.synthetic import make_model  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--ns", type=int, default=16)
+ap.add_argument("--nz", type=int, default=500)
+ap.add_argument("--nx", type=int, default=3000)
+ap.add_argument("--nt", type=int, default=1000)
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--T", type=str, default="2,3,4", help="blocking depths to time")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+ctx = dict(n_grid=a.nx, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=a.nx, ns=a.ns)
+fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
+v = v_normalize(torch.from_numpy(make_model("curvefault", a.nz, a.nx, batch=1))).to(dev)
+plan = fwi._plan(a.nz, a.nx, dev)
+sz = plan.sizes(1)
+npad = sz.Hp * sz.Wp
+dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
+print(json.dumps({"grid": [a.nz, a.nx], "padded": [sz.Hp, sz.Wp], "ld": sz.ld, "ns": a.ns, "nt": a.nt,
+                  "history_GB": round(sz.history / 1e9, 2), "launch": plan.launch_info(1)}), flush=True)
+for T in [int(t) for t in a.T.split(",")]:
+    plan.set_tuning(T, T, 1)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fw, ad = [], []
+    t0 = time.time()
+    for i in range(a.reps + 1):
+        coeffs, vstat = plan.coeffs(v, 0)
+        ev[0].record()
+        seis, hist = plan.forward(coeffs, 1, keep_history=True)
+        ev[1].record()
+        plan.adjoint(coeffs, hist, dseis, 1)
+        ev[2].record()
+        torch.cuda.synchronize()
+        del hist
+        if i:
+            fw.append(ev[0].elapsed_time(ev[1]))
+            ad.append(ev[1].elapsed_time(ev[2]))
+    plan.status()
+    f, d = min(fw), min(ad)
+    shot_steps = a.ns * a.nt
+    print(json.dumps({"T": T, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+                      "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
+                      "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
+                      "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
+                      "fwd_adj_frac_of_8TBps": round(28 * npad * shot_steps / (f + d) / 1e6 / 8000, 4),
+                      "wall_s": round(time.time() - t0, 1)}), flush=True)
