@@ -600,6 +600,9 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 #define RDQ_EXP_NOSTORE 0
 #endif
 constexpr int CP_SC1 = 16;
+#ifndef PT_ADJ_SG
+#define PT_ADJ_SG 4   // adjoint hand-off sweep: rows per load group (register budget)
+#endif
 constexpr size_t PROF_RAW = 8;                        // per-wave records after the 4 summary words
 constexpr size_t PROF_WAVES = 4096 * 16;              // blocks x waves recorded
 constexpr size_t PROF_WORDS = PROF_RAW + PROF_WAVES * 3;   // per kernel (fwd, then adj)                           // buffer cache policy: sc1 (write-through / L1 bypass)
@@ -753,26 +756,42 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
         if (ly < vh + H) rcy |= 1u << r;                                                            \
     }                                                                                               \
     const size_t so = (size_t)bs * g.slice;                                                         \
-    const int vo4 = gx * 4, vo16 = gx * 16;                                                         \
+    const int vo16 = gx * 16;                                                                       \
     const bool hx = !xin && cx, xb = xin && bx;
 #define PT_ROFS(r) (wrap_row(uz0 + (r), g.Hp) * g.ld)
 
 // Reload the halo cells of two levels V0/V1 from the granule slot GR (16-byte two-level granules),
 // zero the dead cells.  `live` turns false once this wave gave up (timeout / another's timeout).
-#define PT_SWEEP(GR, TAG, V0, V1)                                                                   \
+// The wave's own traffic for the next epoch (history stores / prefetch loads, wavelet, receiver
+// residuals) is issued only AFTER the sweep (FWD_ISSUE / ADJ_ISSUE), not before it: a hand-off's
+// latency is set by the consumer CU's own memory queue (MI355X_MICROARCH.md, handoff-1to1), and on
+// gfx9 the in-order vmcnt also counts stores, so the granule loads would otherwise wait behind it.
+#define PT_SWEEP(GR, TAG, V0, V1, SG)                                                               \
     {                                                                                               \
         unsigned long long t0_ = 0;                                                                 \
         const unsigned long long ts_ = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;               \
         for (unsigned pass_ = 0; live; ++pass_) {                                                   \
+            /* the loads of a group of SG rows are all issued before any is checked: lanes        \
+               without a halo cell in a row load from an out-of-range offset (no memory access,   \
+               returns 0) instead of branching, which would make the compiler wait vmcnt(0) after \
+               each load (one serial L2 round trip per row).  SG < R bounds the registers held.  */ \
             bool ok_ = true;                                                                        \
-            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
-                const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                      \
-                if (!rowin_ && !rowcy_) continue;                                                   \
-                if (rowin_ ? hx : cx) {                                                             \
-                    const u32x4 x_ = gran_get(GR, vo16, PT_ROFS(r) * 16);                           \
-                    ok_ = ok_ && x_.y == (TAG) && x_.w == (TAG);                                    \
-                    V0[r] = __uint_as_float(x_.x);                                                  \
-                    V1[r] = __uint_as_float(x_.z);                                                  \
+            _Pragma("unroll") for (int g_ = 0; g_ < R; g_ += (SG)) {                                \
+                u32x4 x_[(SG)];                                                                     \
+                _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
+                    const int r = g_ + i_;                                                          \
+                    const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                  \
+                    if (!rowin_ && !rowcy_) continue;             /* wave-uniform */               \
+                    x_[i_] = gran_get(GR, (rowin_ ? hx : cx) ? vo16 : OOB, PT_ROFS(r) * 16);        \
+                }                                                                                   \
+                _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
+                    const int r = g_ + i_;                                                          \
+                    const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                  \
+                    if (!rowin_ && !rowcy_) continue;                                               \
+                    const bool nd_ = rowin_ ? hx : cx;                                              \
+                    ok_ = ok_ && (!nd_ || (x_[i_].y == (TAG) && x_[i_].w == (TAG)));                \
+                    V0[r] = nd_ ? __uint_as_float(x_[i_].x) : V0[r];                                \
+                    V1[r] = nd_ ? __uint_as_float(x_[i_].z) : V1[r];                                \
                 }                                                                                   \
             }                                                                                       \
             const bool done_ = RDQ_EXP_SWEEP_ONCE || __all(ok_);                                     \
@@ -854,7 +873,8 @@ struct FwdPtArgs {
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
                 if ((sm_ >> r) & 1u) PRV[r] = PRV[r] + add;                                         \
         }                                                                                           \
-        if (!RDQ_EXP_NOSTORE && a.hist && (t + 2 < T || e + 1 == nep)) {   /* own cells only */    \
+        if (!RDQ_EXP_NOSTORE && a.hist) {   /* own cells only; issued at once (the faster of the     \
+                                               store placements measured: tools/exp_variants.sh) */ \
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
             _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PRV[r], hv[r], 0);            \
         }                                                                                           \
@@ -911,28 +931,15 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
-    // Wavelet samples of an epoch are loaded BEFORE its hand-off sweep, which ends the loop body:
-    // the sweep waits vmcnt(0) on every path into the next epoch (and the prologue waits
-    // explicitly), so no step ever waits on a load - a load inside the epoch would be waited for
-    // behind the in-order vmcnt of the history stores.
+    // The next epoch's wavelet samples are loaded right after the hand-off sweep (FWD_ISSUE), not
+    // before it, so the granule loads do not queue behind them.
     float wv[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+#define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
-        // The previous epoch's last two levels are stored only now, after the hand-off: on gfx9
-        // vmcnt also counts stores, so stores still in flight would hold up every hand-off load.
-        if (e > 0 && a.hist) {
-            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n0 + 1) * L + so, slice_bytes);
-#pragma unroll
-            for (int r = 0; r < R; ++r) bstore(HR, P1[r], hv[r], 0);            // P_{n0}
-            if (T >= 2) {
-                const __amdgpu_buffer_rsrc_t HQ = rsrc_of(a.hist + (size_t)n0 * L + so, slice_bytes);
-#pragma unroll
-                for (int r = 0; r < R; ++r) bstore(HQ, P0[r], hv[r], 0);        // P_{n0-1}
-            }
-        }
         PT_PROF(tsw)
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -950,13 +957,12 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             const unsigned tag = (unsigned)(e + 1);
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, P0, P1)
-#pragma unroll
-            for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
             PT_PROF(tpb)
-            PT_SWEEP(GR, tag, P0, P1)
-            __builtin_amdgcn_s_waitcnt(0x0F70);           // also on the gave-up path (no loads left)
+            PT_SWEEP(GR, tag, P0, P1, R)
+            FWD_ISSUE
         }
     }
+#undef FWD_ISSUE
     PT_PROF(tsw)
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
@@ -1121,10 +1127,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         pv[i] = grad ? (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4 : OOB;   // OOB: no memory access
     }
     // Per-epoch inputs (the first step's history slice P, the receiver residuals dseis[k-1] and the
-    // wavelet w[k-1] of the epoch's T steps) are loaded BEFORE the epoch's hand-off sweep, which
-    // ends the loop body: the sweep waits vmcnt(0) on every path into the next epoch (the prologue
-    // waits explicitly), so inside an epoch the only loads in flight are the one-step-ahead
-    // history prefetches and a step waits only for its own P.
+    // wavelet w[k-1] of the epoch's T steps) are issued right behind the hand-off loads of the
+    // previous epoch's sweep (ADJ_ISSUE), so the sweep does not wait for this HBM traffic; inside an
+    // epoch a step waits only for its own P (prefetched one step ahead).
     float wv[T], dv[T];
     ADJ_PLOAD(PA, a.nt)
 #pragma unroll
@@ -1133,6 +1138,12 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         dv[t] = DLOAD(a.nt - t);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+#define ADJ_ISSUE                                                                                   \
+    ADJ_PLOAD(PA, kn)                                                                               \
+    _Pragma("unroll") for (int t = 0; t < T; ++t) {                                                 \
+        wv[t] = a.wav[max(kn - t - 1, 0)];                                                          \
+        dv[t] = DLOAD(kn - t);                                                                      \
+    }
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1158,19 +1169,14 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, L0, L1)
             const int kn = a.nt - (e + 1) * T;            // first step k of the next epoch
-            ADJ_PLOAD(PA, kn)
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                wv[t] = a.wav[max(kn - t - 1, 0)];
-                dv[t] = DLOAD(kn - t);
-            }
             PT_PROF(tpb)
-            PT_SWEEP(GR, tag, L0, L1)
-            __builtin_amdgcn_s_waitcnt(0x0F70);           // also on the gave-up path (no loads left)
+            PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
+            ADJ_ISSUE
             PT_PROF(tsw)
         }
     }
 #undef DLOAD
+#undef ADJ_ISSUE
     if (a.prof && lane == 0) {
         atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
         atomicAdd(a.prof + 4, tfp); atomicAdd(a.prof + 5, npass);

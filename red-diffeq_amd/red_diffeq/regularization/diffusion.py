@@ -72,33 +72,105 @@ class RED_DiffEq:
         return reg.view(B, -1).mean(dim=1), g.view(B, -1).mean(dim=1), t
 
     def get_reg_loss_patched(self, mu, generator: Optional[torch.Generator] = None, t=None, noise=None):
-        """Width > image_size (Marmousi 70x190): overlapping 70-wide windows, 0.5 blending
-        (diffusion.py:85-155).  All windows go through ONE batched U-Net call."""
+        """Models larger than image_size.  Height <= image_size - 2 (Marmousi 70x190): the reference's
+        width-wise windows of size H with 0.5 blending in the overlaps (diffusion.py:85-155), same
+        arithmetic order.  Taller models (configs[4], 500x3000; the reference has no path for them):
+        2-D tiles of (image_size - 2)^2 placed by calculate_patches along both axes, blending weight
+        = product of the two axes' 0.5-overlap weights.  All tiles go through ONE batched U-Net call;
+        tiles are gathered and the gradient re-assembled by index (deterministic, no atomics)."""
         mu_c = diffusion_crop(mu)
         B, _, H, W = mu_c.shape
-        pos, ov = calculate_patches(W, H)
         if t is None:
             t = torch.randint(0, self._max_t(), (B,), generator=generator, device=mu.device, dtype=torch.long)
         if noise is None:
             noise = torch.randn(mu_c.shape, generator=generator, device=mu.device, dtype=mu.dtype)
-        P = len(pos)
-        x0 = torch.cat([diffusion_pad(mu_c[:, :, :, a:b].detach()) for a, b in pos], dim=0)
-        nz = torch.cat([diffusion_pad(noise[:, :, :, a:b]) for a, b in pos], dim=0)
-        gp = diffusion_crop(self._eps_residual(x0, t.repeat(P), nz))
-        grad = torch.zeros_like(mu_c)
-        wmap = torch.zeros_like(mu_c)
-        for i, (a, b) in enumerate(pos):
-            w = torch.ones(b - a, device=mu.device)
-            if i > 0:
-                w[:ov[i - 1]] = 0.5
-            if i < P - 1:
-                w[-ov[i]:] = 0.5
-            w = w.view(1, 1, 1, -1)
-            grad[:, :, :, a:b] += gp[i * B:(i + 1) * B] * w
-            wmap[:, :, :, a:b] += w
-        grad = grad / wmap.clamp(min=1e-8)
+        tp = tile_plan(H, W, self.input_size - 2, B, mu.device)
+        x0 = diffusion_pad(tp.gather(mu_c.detach()))
+        nz = diffusion_pad(tp.gather(noise))
+        gp = diffusion_crop(self._eps_residual(x0, t.repeat(tp.P), nz))
+        grad = tp.assemble(gp)
         reg = self._apply_time_weight(grad * mu_c, t)
         return reg.view(B, -1).mean(dim=1), grad.view(B, -1).mean(dim=1), t
+
+
+def _axis_windows(n: int, m: int):
+    """Windows of size m along an axis of length n and their blending weights: 1, and 0.5 where a
+    window overlaps a neighbour (diffusion.py:135-141, including `w[-0:] = 0.5` when an overlap is
+    empty: the reference then halves the whole window; the normalisation undoes it)."""
+    pos, ov = calculate_patches(n, m)
+    ws = []
+    for i, (a, b) in enumerate(pos):
+        w = torch.ones(b - a, dtype=torch.float32)
+        if i > 0:
+            w[:ov[i - 1]] = 0.5
+        if i < len(pos) - 1:
+            w[-ov[i]:] = 0.5
+        ws.append(w)
+    return pos, ws
+
+
+class TilePlan:
+    """Index maps of one (H, W, B) tiling: gather of the P tiles (patch-major batch p*B + b, the
+    order of the reference's per-patch loop) and, per pixel, up to 4 covering tiles in tile order,
+    so the blended sum accumulates in the reference's order without scatter-adds."""
+
+    def __init__(self, H, W, m, B, device):
+        if H <= m:                          # reference behaviour: width-wise windows of size H
+            rows, rws = [(0, H)], [torch.ones(H)]
+            cols, cws = _axis_windows(W, H)
+        else:                               # 2-D tiles (new behaviour)
+            rows, rws = _axis_windows(H, m)
+            cols, cws = _axis_windows(W, m)
+        mh, mw = rows[0][1] - rows[0][0], cols[0][1] - cols[0][0]
+        self.P, self.B, self.mh, self.mw = len(rows) * len(cols), B, mh, mw
+        self.rows, self.cols = rows, cols
+        R = torch.tensor([[a + k for k in range(mh)] for a, _ in rows for _ in cols])
+        C = torch.tensor([[a + k for k in range(mw)] for _ in rows for a, _ in cols])
+        self.R, self.C = R.to(device), C.to(device)
+        idx = torch.zeros(4, H, W, dtype=torch.int64)    # unused slots: index 0, weight 0
+        wgt = torch.zeros(4, H, W, dtype=torch.float32)
+        cnt = torch.zeros(H, W, dtype=torch.int64)
+        p = 0
+        for (r0, r1), wr in zip(rows, rws):
+            for (c0, c1), wc in zip(cols, cws):
+                ys, xs = torch.meshgrid(torch.arange(r0, r1), torch.arange(c0, c1), indexing="ij")
+                q = cnt[r0:r1, c0:c1]
+                idx[q, ys, xs] = p * B * mh * mw + (ys - r0) * mw + (xs - c0)
+                wgt[q, ys, xs] = wr[:, None] * wc[None, :]
+                cnt[r0:r1, c0:c1] += 1
+                p += 1
+        if int(cnt.max()) > 4 or int(cnt.min()) < 1:
+            raise ValueError(f"tiling of {H}x{W} by {m}: coverage {int(cnt.min())}..{int(cnt.max())}")
+        boff = (torch.arange(B, dtype=torch.int64) * mh * mw).view(1, B, 1, 1)
+        self.idx = (idx.view(4, 1, H, W) + boff).to(device)          # (4, B, H, W)
+        self.wgt = wgt.to(device)
+        wsum = torch.zeros(H, W)
+        for q in range(4):                                           # reference order: 0 + w0 + w1 ...
+            wsum = wsum + wgt[q]
+        self.wsum = wsum.clamp(min=1e-8).to(device)
+
+    def gather(self, x):
+        """(B,1,H,W) -> (P*B, 1, mh, mw), patch-major."""
+        t = x[:, 0][:, self.R[:, :, None], self.C[:, None, :]]       # (B, P, mh, mw)
+        return t.transpose(0, 1).reshape(self.P * self.B, 1, self.mh, self.mw)
+
+    def assemble(self, gp):
+        """Blend per-tile fields (P*B, 1, mh, mw) back to (B, 1, H, W)."""
+        flat = gp.reshape(-1)
+        acc = torch.zeros(self.idx.shape[1:], dtype=gp.dtype, device=gp.device)
+        for q in range(4):
+            acc = acc + flat[self.idx[q]] * self.wgt[q]
+        return (acc / self.wsum).unsqueeze(1)
+
+
+_TILE_PLANS = {}
+
+
+def tile_plan(H, W, m, B, device):
+    key = (H, W, m, B, str(device))
+    if key not in _TILE_PLANS:
+        _TILE_PLANS[key] = TilePlan(H, W, m, B, device)
+    return _TILE_PLANS[key]
 
 
 class RED_DiffEq_POST_PROCESS:
