@@ -174,6 +174,21 @@ __global__ __launch_bounds__(256) void k_coeff_fields(CoefArgs p)
     p.coeffs[5 * p.cstride + i] = o.v;
 }
 
+// buffer addressing: scalar base + 32-bit lane offset; an offset past the range is dropped (no
+// memory access; loads return 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int bytes = 0x7fffffff)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+constexpr int OOB = (int)0x80000000u;               // buffer offset beyond every range: store dropped
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, int voff, int soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
 // --------------------------------------------------------------------------------------- K1/K2
 // Temporal blocking on a register-resident region (the MI355X design of the time loop).
 //
@@ -355,6 +370,10 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
     const bool scol = gx == isx;
     const float bsrc = (smask != 0) ? a.coeffs[4 * g.cstride + (size_t)b * g.slice + (size_t)g.isz * g.ld + isx] : 0.0f;
     const int rs = (rrow >= 0) ? g.rcv_start[gx] : 0, re = (rrow >= 0) ? g.rcv_start[gx + 1] : 0;
+    // this lane's (usually only) receiver, read once: a per-step index load would put an L2 round
+    // trip in front of every step's seismogram store
+    const int rcv0 = rs < re ? g.rcv_list[rs] : -1;
+    const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
     (void)srow;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -393,7 +412,9 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
 #pragma unroll
             for (int r = 0; r < TB_R; ++r) if (r == rrow) val = prv[r];
             float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;
-            for (int j = rs; j < re; ++j) SK[g.rcv_list[j]] = val;
+            if (rcv0 >= 0) SK[rcv0] = val;
+            if (rmulti)
+                for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = val;
         }
     }
     if (a.out_cur && xin) {   // ring path: keep the last two levels
@@ -471,14 +492,27 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     }
     const bool scol = gx == isx;
     const int rs = rmask ? g.rcv_start[gx] : 0, re = rmask ? g.rcv_start[gx + 1] : 0;
+    const int rcv0 = rs < re ? g.rcv_list[rs] : -1;      // this lane's (usually only) receiver
+    const bool rmulti = __any(re - rs > 1);
+    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.ng;
+    // gbeta of this shot accumulates in a register over the launch's steps (same order as a
+    // per-step read-modify-write of a.gbeta[bs]), stored once at the end
+    const bool gbl = (smask & rin) && scol && xin;       // the source cell is this lane's own cell
+    float gbacc = gbl ? a.gbeta[bs] : 0.0f;
     double ksum = 0.0;
     // history P_{k-1} on the rows whose stencil the interior needs: HBM stream, prefetched one
     // step ahead so its latency hides under the previous step
+    // Buffer loads with an out-of-range offset outside pmask (no memory access, returns 0): no
+    // select on the loaded value, so the compiler need not wait for each load in turn.
     float Pn[TB_R];
-    {
-        const float *PS = a.hist + (size_t)a.k0 * g.level + so + gx;
+    int pofs[TB_R];
 #pragma unroll
-        for (int r = 0; r < TB_R; ++r) Pn[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+    for (int r = 0; r < TB_R; ++r) pofs[r] = (pmask & (1u << r)) ? (rofs[r] + gx) * 4 : OOB;
+    const int slice_bytes = (int)(g.slice * 4);
+    {
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, slice_bytes);
+#pragma unroll
+        for (int r = 0; r < TB_R; ++r) Pn[r] = bload(HR, pofs[r], 0);
     }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -490,10 +524,13 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) P[r] = Pn[r];
         if (t + 1 < a.nsteps) {
-            const float *PS = a.hist + (size_t)(k - 1) * g.level + so + gx;
+            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(k - 1) * g.level + so, slice_bytes);
 #pragma unroll
-            for (int r = 0; r < TB_R; ++r) Pn[r] = (pmask & (1u << r)) ? PS[rofs[r]] : 0.0f;
+            for (int r = 0; r < TB_R; ++r) Pn[r] = bload(HR, pofs[r], 0);
         }
+        // this step's receiver residual, loaded before the stencil so its latency hides under it
+        const bool rstep = rmask && ((k - 1) % g.st) == 0;   // wave-uniform
+        const float dsv = (rstep && rcv0 >= 0) ? DSb[(size_t)((k - 1) / g.st) * g.ng + rcv0] : -0.0f;
         float q[TB_R];
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) q[r] = A[r] * cur[r];
@@ -516,12 +553,17 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
             float l = t1 * cur[r]; const float l2 = t2 * prv[r]; l = l - l2; l = l + nb;
             prv[r] = l;
         }
-        if (rmask && ((k - 1) % g.st) == 0) {   // adjoint of the receiver sampling
-            const float *DS = a.dseis + ((size_t)bs * g.nrec + (k - 1) / g.st) * g.ng;
+        if (rstep) {                            // adjoint of the receiver sampling
 #pragma unroll
             for (int r = 0; r < TB_R; ++r)
-                if (rmask & (1u << r))
-                    for (int j = rs; j < re; ++j) prv[r] = prv[r] + DS[g.rcv_list[j]];
+                if (rmask & (1u << r)) prv[r] = prv[r] + dsv;     // -0 on lanes without a receiver
+            if (rmulti) {
+                const float *DS = DSb + (size_t)((k - 1) / g.st) * g.ng;
+#pragma unroll
+                for (int r = 0; r < TB_R; ++r)
+                    if (rmask & (1u << r))
+                        for (int j = rs + 1; j < re; ++j) prv[r] = prv[r] + DS[g.rcv_list[j]];
+            }
         }
         // gradient accumulators on the interior (P halo rows came with the same exchange)
 #pragma unroll
@@ -541,7 +583,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
                 ga = ga + c;
                 float kk = kal[w * TB_R + r][lane] * pc; const float dl = cur[r] - l; kk = kk * dl;  // fp32 term,
                 ksum += (double)kk;                                                             // fp64 sum
-                if ((smask & (1u << r)) && scol) { const float gb = l * a.w[t]; a.gbeta[bs] = a.gbeta[bs] + gb; }
+                if ((smask & (1u << r)) && scol) { const float gb = l * a.w[t]; gbacc = gbacc + gb; }
             }
         }
     }
@@ -556,6 +598,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
                 a.gA[o] = gal[w * TB_R + r][lane];
             }
     }
+    if (gbl) a.gbeta[bs] = gbacc;
     // deterministic workgroup reduction of the sponge-coefficient partial sum
     const int tid = threadIdx.x;
     red[tid] = ksum;
@@ -608,19 +651,6 @@ constexpr size_t PROF_WAVES = 4096 * 16;              // blocks x waves recorded
 constexpr size_t PROF_WORDS = PROF_RAW + PROF_WAVES * 3;   // per kernel (fwd, then adj)                           // buffer cache policy: sc1 (write-through / L1 bypass)
 constexpr unsigned long long PT_TIMEOUT_TICKS = 20000000ull;   // 200 ms of s_memrealtime (100 MHz)
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int bytes = 0x7fffffff)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
-}
-constexpr int OOB = (int)0x80000000u;               // buffer offset beyond every range: store dropped
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff)
-{
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, int voff, int soff)
-{
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
-}
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // One cell's hand-off granule = BOTH wavefield levels, 16 bytes {v0, tag, v1, tag}: each 8-byte
 // half carries its own epoch tag, so a read torn between the halves is still caught by the tag
