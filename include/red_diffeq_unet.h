@@ -39,6 +39,17 @@ size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
                const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
+/* Mixed-precision conv2d (same input modes and epilogue): bf16 operands, fp32 accumulation on
+ * v_mfma_f32_32x32x16_bf16.  The weights are packed once by rdq_conv2d_bf16_pack into
+ * wp[cout][kh*kw][cinp] bf16 (round-to-nearest-even, cinp = cin1+cin2 rounded up to 32, zero-padded;
+ * rdq_conv2d_bf16_wpack_bytes bytes); activations are rounded to bf16 as they are staged.
+ * New behaviour for configs[4] (no reference counterpart; the reference U-Net runs in fp32). */
+size_t rdq_conv2d_bf16_wpack_bytes(const rdq_conv_desc *d);
+int rdq_conv2d_bf16_pack(const rdq_conv_desc *d, const float *w, void *wp, hipStream_t stream);
+size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
+int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                    const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
+
 /* GroupNorm(G) -> [x*(scale+1)+shift] -> SiLU  (Block.forward, diffusion.py:142-149).
  * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes. */
 size_t rdq_group_norm_ws_bytes(int32_t B, int32_t C, int32_t HW, int32_t G);

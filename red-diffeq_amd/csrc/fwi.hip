@@ -1279,10 +1279,39 @@ __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
     const float *V = p.coeffs + 5 * p.cstride + ro;
     const int amz = (int)(p.amin[b] / p.nx), amx = (int)(p.amin[b] - (int64_t)amz * p.nx);
     const int apz = amz == 0 ? 0 : amz + p.nbc, apx = amx == 0 ? 0 : amx + p.nbc;
+    // sponge term sum(gk_part) of the argmin row: a fixed-order two-level fp64 sum (256 contiguous
+    // segments, then the segment sums in order) instead of one thread's serial loop of dependent
+    // loads (ns * nblk round trips)
+    __shared__ double gk_s[256];
+    if (z == apz) {
+        const int cnt = p.ns * p.nblk, per = (cnt + 255) / 256;
+        const double *GK = p.gk_part + (size_t)b * cnt;
+        double acc = 0.0;
+        const int j0 = threadIdx.x * per, j1 = min(cnt, j0 + per);
+        for (int j = j0; j < j1; j += 4) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = GK[min(j + u, cnt - 1)];   // independent loads
+#pragma unroll
+            for (int u = 0; u < 4; ++u) if (j + u < j1) acc += v[u];
+        }
+        gk_s[threadIdx.x] = acc;
+    }
+    __syncthreads();
     for (int x = threadIdx.x; x < p.Wp; x += blockDim.x) {
         float a1 = V[x] * p.dt; a1 = a1 / p.dx;
         float ga = 0.0f;
-        for (int s = 0; s < p.ns; ++s) ga = ga + GA[(size_t)s * p.slice + x];   // shots in order
+        {   // shots in order (the oracle's order); the loads are issued 4 at a time
+            int s = 0;
+            for (; s + 4 <= p.ns; s += 4) {
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = GA[(size_t)(s + u) * p.slice + x];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ga = ga + v[u];
+            }
+            for (; s < p.ns; ++s) ga = ga + GA[(size_t)s * p.slice + x];
+        }
         float t = ga * (2.0f * a1); t = t / p.dx; t = t * p.dt;
         double gv = (double)t;
         if (z == p.isz) {
@@ -1295,7 +1324,7 @@ __global__ __launch_bounds__(256) void k_fin_rows(FinArgs p)
         }
         if (z == apz && x == apx) {
             double gk = 0.0;
-            for (int j = 0; j < p.ns * p.nblk; ++j) gk += p.gk_part[(size_t)b * p.ns * p.nblk + j];
+            for (int j = 0; j < 256; ++j) gk += gk_s[j];
             gv += gk / (double)p.vmin[b];
         }
         gv_s[x] = gv;
@@ -1357,13 +1386,19 @@ __global__ __launch_bounds__(L1_BLOCK) void k_l1_partial(int64_t n, const float 
     const int64_t base = (int64_t)b * n;
     const int64_t c0 = (int64_t)c * L1_BLOCK * L1_ITEMS;
     double se = 0.0, sm = 0.0;
+    float dv[L1_ITEMS], mv[L1_ITEMS];
+#pragma unroll
+    for (int k = 0; k < L1_ITEMS; ++k) {      // all loads first (clamped index, no branch per element)
+        const int64_t j = min(c0 + (int64_t)k * L1_BLOCK + threadIdx.x, n - 1);
+        mv[k] = mask ? mask[base + j] : 1.0f;
+        dv[k] = fabsf(y[base + j] - pred[base + j]);
+    }
+#pragma unroll
     for (int k = 0; k < L1_ITEMS; ++k) {
         const int64_t j = c0 + (int64_t)k * L1_BLOCK + threadIdx.x;
         if (j < n) {
-            const float m = mask ? mask[base + j] : 1.0f;
-            const float d = fabsf(y[base + j] - pred[base + j]);
-            se += (double)(d * m);
-            sm += (double)m;
+            se += (double)(dv[k] * mv[k]);
+            sm += (double)mv[k];
         }
     }
     se = block_sum(se, sh);

@@ -139,6 +139,28 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
         __syncthreads();
     }
     const size_t slab = (size_t)a.M * N;
+    // residual / bias of the 8 outputs loaded together first (clamped addresses: no per-element
+    // branch), then stored: loads behind stores would be waited for one store at a time
+    float rv[2][4], bv[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = min(m0 + j * 16 + (lane & 15), a.M - 1);
+        const int b = m / a.HW, pix = m - b * a.HW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = min(n0 + wv * 16 + (lane >> 4) * 4 + r, N - 1);
+            rv[j][r] = (a.S == 1 && a.res) ? a.res[((size_t)b * N + n) * a.HW + pix] : 0.0f;
+            bv[j][r] = (a.S == 1 && a.bias) ? a.bias[n] : 0.0f;
+        }
+    }
+    float ov[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            ov[j][r] = a.S == 1 ? (acc[j][r] + bv[j][r]) + rv[j][r] : acc[j][r];
+            asm volatile("" : "+v"(ov[j][r]));        // formed before any conditional store
+        }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int m = m0 + j * 16 + (lane & 15);
@@ -149,13 +171,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
             const int n = n0 + wv * 16 + (lane >> 4) * 4 + r;
             if (n >= N) continue;
             const size_t o = ((size_t)b * N + n) * a.HW + pix;
-            if (a.S == 1) {
-                float v = acc[j][r] + (a.bias ? a.bias[n] : 0.0f);
-                if (a.res) v = v + a.res[o];
-                a.y[o] = v;
-            } else {
-                a.part[split * slab + o] = acc[j][r];
-            }
+            if (a.S == 1) a.y[o] = ov[j][r];
+            else a.part[split * slab + o] = ov[j][r];
         }
     }
 }
@@ -404,8 +421,16 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, int nc
     __shared__ __attribute__((aligned(16))) float cs[32][32];
     for (int i = threadIdx.x; i < dh * dh; i += blockDim.x) {
         const int d = i / dh;
-        float t = 0.0f;
-        for (int c = 0; c < nch; ++c) t += part[(((size_t)c * B + b) * heads + h) * dh * dh + i];
+        float t = 0.0f;                       // chunks in order; loads issued 4 at a time
+        int c = 0;
+        for (; c + 4 <= nch; c += 4) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = part[(((size_t)(c + u) * B + b) * heads + h) * dh * dh + i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t += v[u];
+        }
+        for (; c < nch; ++c) t += part[(((size_t)c * B + b) * heads + h) * dh * dh + i];
         cs[d][i - d * dh] = t / stats[((size_t)(b * heads + h) * dh + d) * 2 + 1];
     }
     __syncthreads();
@@ -415,7 +440,9 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, int nc
     float qv[32];
     float mx = -INFINITY;
 #pragma unroll
-    for (int d = 0; d < 32; ++d) if (d < dh) { qv[d] = q[(size_t)d * n]; mx = fmaxf(mx, qv[d]); }
+    for (int d = 0; d < 32; ++d) qv[d] = q[(size_t)min(d, dh - 1) * n];   // no branch per load
+#pragma unroll
+    for (int d = 0; d < 32; ++d) if (d < dh) mx = fmaxf(mx, qv[d]);
     float sm = 0.0f;
 #pragma unroll
     for (int d = 0; d < 32; ++d) if (d < dh) { qv[d] = expf(qv[d] - mx); sm += qv[d]; }
@@ -566,6 +593,228 @@ void launch_conv_ig(dim3 grid, hipStream_t st, const IgArgs &a)
     }
 }
 
+
+// ------------------------------------------------------------------------------- conv2d, bf16
+// Mixed-precision implicit GEMM for large batches (configs[4]: hundreds of 72x72 tiles per
+// iteration): bf16 operands (activations rounded to bf16 as they are staged, weights pre-packed once
+// by k_pack_w_bf16), fp32 accumulation on v_mfma_f32_32x32x16_bf16 (16x the fp32 matrix rate).
+// The reduction runs tap-major, k = tap * cinp + ci (cinp = cin rounded up to 32; the packed weights
+// are zero-padded), so one 32-deep K stage is ONE filter tap over 32 consecutive channels: a thread
+// gathers 16 channels of its pixel at a fixed stride with one bounds check per stage.
+// Tile: 128 pixels (4 waves x 32: the B operand, pixel on the lane, so every accumulator register
+// stores 32 consecutive pixels of one output channel) x 32*NB output channels (the A operand).
+// mfma_f32_32x32x16_bf16 lane maps: A[row l&31][k 8(l>>5)+j], B[k 8(l>>5)+j][col l&31],
+// D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31] (cdna_hip_programming.md §3).
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr int BF_BM = 128, BF_BK = 32, BF_LD = BF_BK + 8;   // LDS rows of 80 B
+
+struct BfArgs {
+    rdq_conv_desc d;
+    const float *x, *x2, *bias, *res;
+    const __bf16 *w;                 // [cout][taps][cinp]
+    float *y, *part;
+    int cinp, K, M, HW, nsteps, per_split, S;
+};
+
+__global__ __launch_bounds__(256) void k_pack_w_bf16(int cout, int cin, int taps, int cinp,
+                                                     const float *__restrict__ w, __bf16 *__restrict__ wp)
+{
+    const int64_t n = (int64_t)cout * taps * cinp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = i / ((int64_t)taps * cinp);
+        const int r = (int)(i - o * taps * cinp), tap = r / cinp, ci = r - tap * cinp;
+        wp[i] = ci < cin ? (__bf16)w[(o * cin + ci) * taps + tap] : (__bf16)0.0f;
+    }
+}
+
+template <int MODE, int NB>
+__global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
+{
+    constexpr int BN = 32 * NB;
+    __shared__ __attribute__((aligned(16))) __bf16 Ws[2][BN][BF_LD];
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][BF_BM][BF_LD];
+    const rdq_conv_desc &d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * BF_BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+    const int s_begin = split * a.per_split, s_end = min(a.nsteps, s_begin + a.per_split);
+    const int cin = d.cin1 + d.cin2, cch = a.cinp / BF_BK;
+    // gather role: pixel gp, channels 16 gc .. 16 gc + 15 of the stage (gc is wave-uniform)
+    const int gp = tid & (BF_BM - 1), gc = tid >> 7;
+    const int gm = m0 + gp;
+    const bool pv = gm < a.M;
+    const int gb = pv ? gm / a.HW : 0, gpix = pv ? gm - gb * a.HW : 0;
+    const int oh = gpix / d.W, ow = gpix - oh * d.W;
+    // weight role: rows wn + 64 j, k octet wq
+    const int wn = tid >> 2, wq = (tid & 3) * 8;
+    float ra[16];
+    bf16x8 rw[NB / 2];
+    auto load = [&](int s) {
+        const int tap = s / cch, c0 = (s - tap * cch) * BF_BK + 16 * gc;
+        const int ky = tap / d.kw, kx = tap - ky * d.kw;
+        const int ih = oh + ky - d.pad, iw = ow + kx - d.pad;
+        const bool ok = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+        if constexpr (MODE == RDQ_IN_UPSAMPLE2) {
+            const int w2 = d.W >> 1;
+            const size_t hw2 = (size_t)(d.H >> 1) * w2;
+            const float *p = a.x + ((size_t)gb * d.cin1 + c0) * hw2 + (ok ? (ih >> 1) * w2 + (iw >> 1) : 0);
+            if (c0 + 16 <= d.cin1) {                 // wave-uniform: loads without per-element tests
+#pragma unroll
+                for (int j = 0; j < 16; ++j) { const float v = p[j * hw2]; ra[j] = ok ? v : 0.0f; }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) ra[j] = (ok && c0 + j < d.cin1) ? p[j * hw2] : 0.0f;
+            }
+        } else if constexpr (MODE == RDQ_IN_UNSHUFFLE2) {
+            const int W2 = 2 * d.W;
+            const size_t hw4 = (size_t)4 * d.H * d.W;           // one plane of the full-res input
+            const float *p = a.x + (size_t)gb * (d.cin1 >> 2) * hw4 + (ok ? (2 * ih) * W2 + 2 * iw : 0);
+            if (c0 + 16 <= d.cin1) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {       // channel c0 + j = 4c + 2 p1 + p2
+                    const int ci = c0 + j;
+                    const float v = p[(size_t)(ci >> 2) * hw4 + ((ci >> 1) & 1) * W2 + (ci & 1)];
+                    ra[j] = ok ? v : 0.0f;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int ci = c0 + j;
+                    ra[j] = (ok && ci < d.cin1) ? p[(size_t)(ci >> 2) * hw4 + ((ci >> 1) & 1) * W2 + (ci & 1)] : 0.0f;
+                }
+            }
+        } else {
+            const size_t hw = (size_t)d.H * d.W;
+            const int off = ok ? ih * d.W + iw : 0;
+            if (c0 + 16 <= d.cin1) {
+                const float *p = a.x + ((size_t)gb * d.cin1 + c0) * hw + off;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) { const float v = p[j * hw]; ra[j] = ok ? v : 0.0f; }
+            } else if (c0 >= d.cin1 && c0 + 16 <= cin) {  // wave-uniform: all from the skip tensor
+                const float *p = a.x2 + ((size_t)gb * d.cin2 + (c0 - d.cin1)) * hw + off;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) { const float v = p[j * hw]; ra[j] = ok ? v : 0.0f; }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int ci = c0 + j;
+                    float v = 0.0f;
+                    if (ok && ci < d.cin1) v = a.x[((size_t)gb * d.cin1 + ci) * hw + off];
+                    else if (ok && ci < cin) v = a.x2[((size_t)gb * d.cin2 + (ci - d.cin1)) * hw + off];
+                    ra[j] = v;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB / 2; ++j) {
+            const int n = n0 + wn + 64 * j;
+            bf16x8 v = {};
+            if (n < d.cout) v = *reinterpret_cast<const bf16x8 *>(a.w + (size_t)n * a.K + (size_t)s * BF_BK + wq);
+            rw[j] = v;
+        }
+    };
+    auto stash = [&](int buf) {
+        bf16x8 v0, v1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v0[j] = (__bf16)ra[j]; v1[j] = (__bf16)ra[8 + j]; }
+        *reinterpret_cast<bf16x8 *>(&As[buf][gp][16 * gc]) = v0;
+        *reinterpret_cast<bf16x8 *>(&As[buf][gp][16 * gc + 8]) = v1;
+#pragma unroll
+        for (int j = 0; j < NB / 2; ++j) *reinterpret_cast<bf16x8 *>(&Ws[buf][wn + 64 * j][wq]) = rw[j];
+    };
+    f32x16 acc[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) acc[c] = f32x16{};
+    if (s_begin < s_end) {
+        load(s_begin);
+        stash(0);
+    }
+    __syncthreads();
+    for (int s = s_begin; s < s_end; ++s) {
+        const int buf = (s - s_begin) & 1;
+        if (s + 1 < s_end) load(s + 1);
+#pragma unroll
+        for (int ks = 0; ks < BF_BK / 16; ++ks) {
+            const int kk = 16 * ks + 8 * (lane >> 5);
+            const bf16x8 bv = *reinterpret_cast<const bf16x8 *>(&As[buf][wv * 32 + (lane & 31)][kk]);
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                const bf16x8 av = *reinterpret_cast<const bf16x8 *>(&Ws[buf][c * 32 + (lane & 31)][kk]);
+                acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[c], 0, 0, 0);
+            }
+        }
+        if (s + 1 < s_end) stash(buf ^ 1);
+        __syncthreads();
+    }
+    const int m = m0 + wv * 32 + (lane & 31);
+    if (m >= a.M) return;
+    const int b = m / a.HW, pix = m - b * a.HW;
+    const size_t slab = (size_t)a.M * d.cout;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        // residual / bias of the block's 16 outputs loaded together (clamped addresses, no branch
+        // per element: a conditional load would be waited for one at a time)
+        float rv[16], bv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = min(n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), d.cout - 1);
+            rv[r] = (a.S == 1 && a.res) ? a.res[((size_t)b * d.cout + n) * a.HW + pix] : 0.0f;
+            bv[r] = (a.S == 1 && a.bias) ? a.bias[n] : 0.0f;
+        }
+        // every output value is formed before the first (conditional) store: a loaded value
+        // consumed inside a store's branch block makes the compiler wait vmcnt(0) there, and on
+        // gfx9 that also drains the stores already issued (one store round trip per element)
+        float ov[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            ov[r] = a.S == 1 ? (acc[c][r] + bv[r]) + rv[r] : acc[c][r];
+            asm volatile("" : "+v"(ov[r]));
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (n >= d.cout) continue;
+            const size_t o = ((size_t)b * d.cout + n) * a.HW + pix;
+            if (a.S == 1) a.y[o] = ov[r];
+            else a.part[split * slab + o] = ov[r];
+        }
+    }
+}
+
+int bf_cinp(const rdq_conv_desc *d) { return (d->cin1 + d->cin2 + BF_BK - 1) / BF_BK * BF_BK; }
+
+// split count as ig_splits: about two workgroups per CU over the tile grid, >= 4 K stages each
+int bf_splits(const rdq_conv_desc *d, int BN, int nsteps, size_t ws_bytes, int *per_split)
+{
+    const int M = d->B * d->H * d->W;
+    const int tiles = ((M + BF_BM - 1) / BF_BM) * ((d->cout + BN - 1) / BN);
+    int S = std::max(1, std::min((512 + tiles - 1) / tiles, nsteps / 4));
+    const size_t slab = (size_t)M * d->cout * sizeof(float);
+    if (S > 1 && ws_bytes < 2 * slab) S = 1;
+    if (S > 1) S = std::min<int64_t>(S, (int64_t)(ws_bytes / slab));
+    const int per = (nsteps + S - 1) / S;
+    *per_split = per;
+    return (nsteps + per - 1) / per;
+}
+
+template <int NB>
+void launch_conv_bf16(dim3 grid, hipStream_t st, const BfArgs &a)
+{
+    switch (a.d.in_mode) {
+    case RDQ_IN_UPSAMPLE2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_bf16<RDQ_IN_UPSAMPLE2, NB>), grid, dim3(256), 0, st, a); break;
+    case RDQ_IN_UNSHUFFLE2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_bf16<RDQ_IN_UNSHUFFLE2, NB>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_bf16<RDQ_IN_PLAIN, NB>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
+bool conv_desc_ok(const rdq_conv_desc *d)
+{
+    if (!d || d->B < 1 || d->cin1 < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->H < 1 || d->W < 1 || d->pad < 0)
+        return false;
+    if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return false;
+    if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return false;
+    return true;
+}
 }  // namespace
 
 extern "C" {
@@ -601,6 +850,61 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
     else if (sq && d->kh == 1) launch_conv_ig<1>(grid, st, a);
     else if (sq && d->kh == 7) launch_conv_ig<7>(grid, st, a);
     else launch_conv_ig<0>(grid, st, a);
+    if (a.S > 1) {
+        const int64_t total = (int64_t)a.M * d->cout;
+        hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a.S, total, d->cout,
+                           a.HW, a.part, bias, residual, y);
+    }
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+size_t rdq_conv2d_bf16_wpack_bytes(const rdq_conv_desc *d)
+{
+    if (!conv_desc_ok(d)) return 0;
+    return (size_t)d->cout * d->kh * d->kw * bf_cinp(d) * sizeof(__bf16);
+}
+
+int rdq_conv2d_bf16_pack(const rdq_conv_desc *d, const float *w, void *wp, hipStream_t st)
+{
+    if (!conv_desc_ok(d) || !w || !wp) return RDQ_E_INVALID;
+    const int taps = d->kh * d->kw, cinp = bf_cinp(d);
+    const int64_t n = (int64_t)d->cout * taps * cinp;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_pack_w_bf16, dim3(blocks), dim3(256), 0, st, d->cout, d->cin1 + d->cin2, taps, cinp, w,
+                       static_cast<__bf16 *>(wp));
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d)
+{
+    if (!conv_desc_ok(d)) return 0;
+    const int BN = d->cout >= 128 ? 128 : 64;
+    int per = 0;
+    const int S = bf_splits(d, BN, d->kh * d->kw * bf_cinp(d) / BF_BK, (size_t)-1 / 2, &per);
+    return S > 1 ? (size_t)S * d->B * d->H * d->W * d->cout * sizeof(float) : 0;
+}
+
+int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                    const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    if (!conv_desc_ok(d) || !x || !wp || !y || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        return RDQ_E_INVALID;
+    BfArgs a{};
+    a.d = *d; a.x = x; a.x2 = x2; a.w = static_cast<const __bf16 *>(wp); a.bias = bias; a.res = residual; a.y = y;
+    a.part = static_cast<float *>(ws);
+    a.cinp = bf_cinp(d);
+    a.K = d->kh * d->kw * a.cinp;
+    a.HW = d->H * d->W;
+    a.M = d->B * a.HW;
+    a.nsteps = a.K / BF_BK;
+    const int NB = d->cout >= 128 ? 4 : 2;
+    a.S = ws ? bf_splits(d, 32 * NB, a.nsteps, ws_bytes, &a.per_split) : 1;
+    if (a.S == 1) a.per_split = a.nsteps;
+    const dim3 grid((a.M + BF_BM - 1) / BF_BM, (d->cout + 32 * NB - 1) / (32 * NB), a.S);
+    if (NB == 4) launch_conv_bf16<4>(grid, st, a);
+    else launch_conv_bf16<2>(grid, st, a);
     if (a.S > 1) {
         const int64_t total = (int64_t)a.M * d->cout;
         hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a.S, total, d->cout,

@@ -208,6 +208,15 @@ class Unet(nn.Module):
         self.out_dim = default(out_dim, channels * (1 if not learned_variance else 2))
         self.final_res_block = block(dim * 2, dim, time_emb_dim=time_dim)
         self.final_conv = nn.Conv2d(dim, self.out_dim, 1)
+        self.precision = "fp32"     # conv arithmetic: "fp32" (reference) or "bf16" (configs[4])
+
+    def set_precision(self, mode):
+        """U-Net convolutions in "fp32" (the reference's arithmetic, default) or "bf16" (bf16
+        operands, fp32 accumulation; new behaviour for large tiled models, configs[4])."""
+        with ops.precision(mode):
+            pass
+        self.precision = mode
+        return self
 
     @property
     def downsample_factor(self):
@@ -228,6 +237,10 @@ class Unet(nn.Module):
     def forward(self, x, time, x_self_cond=None):
         assert all(divisible_by(d, self.downsample_factor) for d in x.shape[-2:]), \
             f"your input dimensions {x.shape[-2:]} need to be divisible by {self.downsample_factor}, given the unet"
+        with ops.precision(self.precision):
+            return self._forward(x, time, x_self_cond)
+
+    def _forward(self, x, time, x_self_cond):
         if self.self_condition:
             x_self_cond = default(x_self_cond, lambda: torch.zeros_like(x))
             x = torch.cat((x_self_cond, x), dim=1)

@@ -7,6 +7,7 @@ conv operand gather; bias, residual adds (168, 286, 290, 297) into the conv / RM
 the time-conditioned scale/shift (147) and SiLU into GroupNorm.  There is no PyTorch fallback:
 CPU tensors raise.
 """
+import contextlib
 import ctypes
 import math
 
@@ -21,8 +22,43 @@ def _f(t):
     return t.contiguous() if t is not None else None
 
 
+# Convolution precision of the current U-Net forward ("fp32", the reference's; or "bf16": bf16
+# operands with fp32 accumulation, the configs[4] mixed-precision U-Net).  Set by Unet.forward.
+_PREC = {"mode": "fp32"}
+
+
+@contextlib.contextmanager
+def precision(mode):
+    if mode not in ("fp32", "bf16"):
+        raise ValueError(f"unknown U-Net precision {mode!r} (fp32 | bf16)")
+    old = _PREC["mode"]
+    _PREC["mode"] = mode
+    try:
+        yield
+    finally:
+        _PREC["mode"] = old
+
+
+def _bf16_weights(conv, d, stream):
+    """bf16 pack of conv.weight ([cout][tap][cin padded to 32]), cached on the module and rebuilt
+    when the weight changes (load_state_dict, in-place updates)."""
+    w = conv.weight
+    key = (w.data_ptr(), w._version, w.device)
+    ent = getattr(conv, "_rdq_bf16", None)
+    if ent is None or ent[0] != key:
+        L = _hip.lib()
+        wp = torch.empty(int(L.rdq_conv2d_bf16_wpack_bytes(ctypes.byref(d))), dtype=torch.uint8, device=w.device)
+        _hip.check(L.rdq_conv2d_bf16_pack(ctypes.byref(d), _hip.ptr(w.detach().contiguous()), _hip.ptr(wp), stream),
+                   "rdq_conv2d_bf16_pack")
+        ent = (key, wp)
+        conv._rdq_bf16 = ent
+    return ent[1]
+
+
 def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
-    """nn.Conv2d(stride 1, padding conv.padding) of the logical input formed by `mode`."""
+    """nn.Conv2d(stride 1, padding conv.padding) of the logical input formed by `mode`.  Under
+    precision("bf16") the dense contractions (K = cin*kh*kw >= 128, cout >= 16) run on the bf16
+    matrix cores; the tiny first/last convolutions stay fp32."""
     _hip.require_device(x)
     x = _f(x)
     x2 = _f(x2)
@@ -44,6 +80,14 @@ def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
     y = torch.empty(B, cout, H, W, device=x.device, dtype=torch.float32)
     res = _f(residual)
     L = _hip.lib()
+    if _PREC["mode"] == "bf16" and cin * kh * kw >= 128 and cout >= 16:
+        st = _hip.stream_of(x)
+        wp = _bf16_weights(conv, d, st)
+        nws = int(L.rdq_conv2d_bf16_ws_bytes(ctypes.byref(d)))
+        ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+        _hip.check(L.rdq_conv2d_bf16(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(wp), _hip.ptr(conv.bias),
+                                     _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, st), "rdq_conv2d_bf16")
+        return y
     nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
     ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
     _hip.check(L.rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(w.contiguous()),

@@ -145,3 +145,62 @@ def test_red_regulariser_vs_reference(cuda, tag):
     close(reg.detach(), torch.from_numpy(zr[tag + "_reg"]).to(cuda), rel=1e-3)
     close(gpm.detach(), torch.from_numpy(zr[tag + "_gpm"]).to(cuda), rel=1e-3)
     close(mu.grad, torch.from_numpy(zr[tag + "_grad"]).to(cuda), rel=2e-4)
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+@pytest.mark.parametrize("cin,cout,k,H,B", [(64, 64, 3, 72, 2), (128, 256, 3, 18, 3), (48, 40, 3, 9, 1),
+                                             (256, 128, 1, 9, 2), (512, 512, 3, 9, 1)])
+def test_conv_bf16_vs_torch_on_bf16_operands(cuda, cin, cout, k, H, B):
+    """Mixed-precision conv (configs[4]): bf16 operands, fp32 accumulation.  Reference: the fp32 torch
+    conv of the bf16-ROUNDED input and weights (products of bf16 values are exact in fp32, so only the
+    summation order differs).  Covers channel padding (48 -> 64), cout not a multiple of 32, both
+    cout-block widths and the split-K path (512 channels at 9x9, B = 1)."""
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(10)
+    conv = nn.Conv2d(cin, cout, k, padding=k // 2).to(cuda)
+    x = torch.randn(B, cin, H, H, device=cuda)
+    ref = torch.nn.functional.conv2d(_bf(x), _bf(conv.weight), conv.bias, padding=k // 2)
+    with ops.precision("bf16"):
+        got = ops.conv2d(x, conv)
+    close(got, ref, rel=2e-5)
+
+
+def test_conv_bf16_concat_residual_upsample_unshuffle(cuda):
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(11)
+    conv = nn.Conv2d(48, 32, 3, padding=1).to(cuda)
+    a = torch.randn(2, 32, 18, 18, device=cuda)
+    b = torch.randn(2, 16, 18, 18, device=cuda)
+    res = torch.randn(2, 32, 18, 18, device=cuda)
+    with ops.precision("bf16"):
+        got = ops.conv2d(a, conv, x2=b, residual=res)
+        up = nn.Conv2d(32, 16, 3, padding=1).to(cuda)
+        got_up = ops.conv2d(a, up, mode=ops.UPSAMPLE2)
+        dn = nn.Conv2d(128, 64, 1).to(cuda)
+        got_dn = ops.conv2d(a, dn, mode=ops.UNSHUFFLE2)
+    F = torch.nn.functional
+    close(got, F.conv2d(_bf(torch.cat((a, b), 1)), _bf(conv.weight), conv.bias, padding=1) + res)
+    close(got_up, F.conv2d(_bf(R.upsample_nearest2(a)), _bf(up.weight), up.bias, padding=1))
+    close(got_dn, F.conv2d(_bf(R.pixel_unshuffle2(a)), _bf(dn.weight), dn.bias))
+
+
+def test_unet_bf16_close_to_fp32(cuda):
+    """Whole U-Net (reference architecture, dim 64) with bf16 convolutions vs fp32: new behaviour
+    (configs[4]), no reference counterpart; the deviation is bounded, not bitwise."""
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(12)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    x = torch.randn(6, 1, 72, 72, device=cuda).clamp(-1, 1)
+    t = torch.tensor([0, 10, 200, 500, 800, 999], device=cuda)
+    with torch.no_grad():
+        ref = net(x, t)
+        net.set_precision("bf16")
+        got = net(x, t)
+        net.set_precision("fp32")
+        again = net(x, t)
+    assert torch.equal(again, ref)
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 2e-2, rel
