@@ -57,8 +57,8 @@ def _bf16_weights(conv, d, stream):
 
 def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
     """nn.Conv2d(stride 1, padding conv.padding) of the logical input formed by `mode`.  Under
-    precision("bf16") the dense contractions (K = cin*kh*kw >= 128, cout >= 16) run on the bf16
-    matrix cores; the tiny first/last convolutions stay fp32."""
+    precision("bf16") the dense contractions (K = cin*kh*kw >= 64, cout >= 16: every conv but the
+    7x7 single-channel stem and the single-channel output) run on the bf16 matrix cores."""
     _hip.require_device(x)
     x = _f(x)
     x2 = _f(x2)
@@ -80,7 +80,7 @@ def conv2d(x, conv, x2=None, mode=PLAIN, residual=None):
     y = torch.empty(B, cout, H, W, device=x.device, dtype=torch.float32)
     res = _f(residual)
     L = _hip.lib()
-    if _PREC["mode"] == "bf16" and cin * kh * kw >= 128 and cout >= 16:
+    if _PREC["mode"] == "bf16" and cin * kh * kw >= 64 and cout >= 16:
         st = _hip.stream_of(x)
         wp = _bf16_weights(conv, d, st)
         nws = int(L.rdq_conv2d_bf16_ws_bytes(ctypes.byref(d)))
