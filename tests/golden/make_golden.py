@@ -272,8 +272,36 @@ def gen_small_losses():
          overlaps_190_70=np.array(ref.reg_diffusion.calculate_patches(190, 70)[1]))
 
 
+def gen_dfwi():
+    """DiffusionFWI baseline (diffusion_bench/diffusionfwi.py:79-366) on a 14x14 model (16x16 after
+    diffusion_pad: U-Net-divisible), dim-8 U-Net of gen_unet, two variants: the defaults
+    (grad_norm, grad_clip 1.0) and with grad_smooth 1.0.  No RNG draws (noise_std 0, no missing
+    traces), so the trajectory is a pure function of the inputs."""
+    spec = importlib.util.spec_from_file_location("_ref_dfwi", "/root/reference/diffusion_bench/diffusionfwi.py")
+    dfwi = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(dfwi)
+    ctx = dict(SMALL, n_grid=14, ng=14, ns=2)
+    v_true = synthetic.make_model("curvefault", 14, 14, seed=31, batch=1)
+    y = torch.from_numpy(run_forward(ctx, v_true))
+    init = ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=3.0)
+    net = _unet_dim8()
+    diff = ref.diffusion.GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise").eval()
+    out = dict(v_true=v_true, y=y.numpy(), mu0=init.numpy(), **ctx_arrays(ctx))
+    for tag, kw in (("base", {}), ("smooth", dict(grad_smooth=1.0))):
+        fwi = make_fwi(ctx)
+        bench = dfwi.DiffusionFWI(diff, fwi, ref.ssim.SSIM(window_size=11))
+        mu, hist = bench.optimize(init.clone(), torch.from_numpy(v_true), y, fwi, ts=3, diffusion_ts=4, lr=0.03,
+                                  **kw)
+        h = hist[0]
+        out.update({tag + "_mu": mu.detach().numpy(), tag + "_obs": np.array(h["obs_losses"]).ravel(),
+                    tag + "_ssim": np.array(h["ssim"]).ravel(), tag + "_mae": np.array(h["mae"]).ravel(),
+                    tag + "_rmse": np.array(h["rmse"]).ravel()})
+    save("dfwi_small", **out)
+
+
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
-            loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses)
+            loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi)
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

@@ -198,3 +198,34 @@ def test_tile_plan_2d_covers_and_round_trips(H, W):
     assert torch.equal(tp.assemble(t), x)
     if (H, W) == (500, 3000):
         assert tp.P == 8 * 43
+
+
+def test_diffusion_bench_patch_split_merge_and_smoothing():
+    """DiffusionFWI host helpers (reference diffusion_bench/diffusionfwi.py:32-76, 289-295):
+    split -> merge round-trips with overlapping patches, the fold-based merge equals the reference's
+    loop, and the device Gaussian smoothing equals scipy.ndimage.gaussian_filter (reflect)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+    from scipy.ndimage import gaussian_filter
+    from diffusion_bench.diffusionfwi import _gaussian_smooth, merge_patches_to_data, split_data_to_patches
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 1, 20, 30, generator=g)
+    k, st = [8, 10], [4, 5]
+    p = split_data_to_patches(x, k, st)
+    assert p.shape == (((20 - 8) // 4 + 1) * ((30 - 10) // 5 + 1), 1, 8, 10)
+    torch.testing.assert_close(merge_patches_to_data(p, [20, 30], k, st), x, rtol=0, atol=1e-6)
+    q = p * torch.rand(p.shape, generator=g)                  # reference loop (diffusionfwi.py:56-76)
+    merged = torch.zeros(1, 1, 20, 30)
+    count = torch.zeros(1, 1, 20, 30)
+    idx = 0
+    for i in range((20 - 8) // 4 + 1):
+        for j in range((30 - 10) // 5 + 1):
+            merged[:, :, i * 4:i * 4 + 8, j * 5:j * 5 + 10] += q[idx]
+            count[:, :, i * 4:i * 4 + 8, j * 5:j * 5 + 10] += 1
+            idx += 1
+    torch.testing.assert_close(merge_patches_to_data(q, [20, 30], k, st), merged / count.clamp(min=1),
+                               rtol=1e-6, atol=1e-6)
+    gr = torch.randn(2, 1, 16, 21, generator=g)
+    for s in (0.7, 1.0, 2.5):
+        ref = gaussian_filter(gr.numpy().astype(np.float64), sigma=[0, 0, s, s])
+        np.testing.assert_allclose(_gaussian_smooth(gr, s).numpy(), ref, rtol=1e-5, atol=1e-6)
