@@ -657,6 +657,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // check (the guarantee used is only that an aligned 8-byte store is seen whole), and a sweep or a
 // publish is one dwordx4 instruction per row instead of two dwordx2.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32x4 gran2(unsigned tag, float v0, float v1)
 {
     u32x4 x;
@@ -820,8 +821,8 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
                     if (!rowin_ && !rowcy_) continue;                                               \
                     const bool nd_ = rowin_ ? hx : cx;                                              \
                     ok_ = ok_ && (!nd_ || (x_[i_].y == (TAG) && x_[i_].w == (TAG)));                \
-                    V0[r] = nd_ ? __uint_as_float(x_[i_].x) : V0[r];                                \
-                    V1[r] = nd_ ? __uint_as_float(x_[i_].z) : V1[r];                                \
+                    PT_AT(V0, r) = nd_ ? __uint_as_float(x_[i_].x) : PT_AT(V0, r);                  \
+                    PT_AT(V1, r) = nd_ ? __uint_as_float(x_[i_].z) : PT_AT(V1, r);                  \
                 }                                                                                   \
             }                                                                                       \
             const bool done_ = RDQ_EXP_SWEEP_ONCE || __all(ok_);                                     \
@@ -844,7 +845,7 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
         }                                                                                           \
         _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
             const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                          \
-            if (rowin_ ? (!xin && !cx) : (!rowcy_ || !cx)) { V0[r] = 0.0f; V1[r] = 0.0f; }          \
+            if (rowin_ ? (!xin && !cx) : (!rowcy_ || !cx)) { PT_AT(V0, r) = 0.0f; PT_AT(V1, r) = 0.0f; } \
         }                                                                                           \
     }
 
@@ -853,8 +854,8 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
     _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                 \
         if (!((rin >> r) & 1u)) continue;                                                           \
         if (((rby >> r) & 1u) ? xin : xb) {                                                         \
-            if (gl2) gran_put_l2(GR, vo16, PT_ROFS(r) * 16, (TAG), V0[r], V1[r]);                   \
-            else gran_put(GR, vo16, PT_ROFS(r) * 16, (TAG), V0[r], V1[r]);                          \
+            if (gl2) gran_put_l2(GR, vo16, PT_ROFS(r) * 16, (TAG), PT_AT(V0, r), PT_AT(V1, r));     \
+            else gran_put(GR, vo16, PT_ROFS(r) * 16, (TAG), PT_AT(V0, r), PT_AT(V1, r));            \
         }                                                                                           \
     }
 
@@ -879,21 +880,32 @@ struct FwdPtArgs {
     int xcd_mode;                        // 1: XCD-local slices (pt_assign), 0: all hand-offs write-through
 };
 
-// one forward step P_{n+1} = temp1 P_n - temp2 P_{n-1} + alpha N(P_n) (+ source), pde.py:79-81
+// One forward step P_{n+1} = temp1 P_n - temp2 P_{n-1} + alpha N(P_n) (+ source), pde.py:79-81, on
+// packed fp32: a wave's 8 rows are held as 4 row PAIRS {r, r+4} (float2 = one VGPR pair), so every
+// add / mul of the stencil is one v_pk_*_f32 for two rows (IEEE-identical to the scalar ops, same
+// operation order per row).  With this pairing the vertical neighbours of pair i are pairs i-1 /
+// i+1 / i-2 / i+2 except at the slab ends, where four pairs are assembled from the halo rows.  The
+// horizontal taps stay per-row DPP lane shifts (DPP has no packed form).
 #define FWD_STEP(CUR, PRV)                                                                          \
     {                                                                                               \
-        const Halo4 h4 = exchange_nw<NW>(xch, n & 1, w, lane, CUR[0], CUR[1], CUR[R - 2], CUR[R - 1]); \
-        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
-            TB_VERT(CUR, r, h4, zm2, zm1, zp1, zp2)                                                 \
-            const float c = CUR[r];                                                                 \
-            const float xl1 = dpp_shr1(c), xr1 = dpp_shl1(c);                                       \
-            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                                   \
-            float s1 = zm1 + zp1; s1 = s1 + xl1; s1 = s1 + xr1;                                     \
-            float s2 = zm2 + zp2; s2 = s2 + xl2; s2 = s2 + xr2;                                     \
-            float lap = C2 * s1; const float l2 = C3 * s2; lap = lap + l2;                          \
-            float a1 = C1[r] * c; const float a2 = C2v[r] * PRV[r]; a1 = a1 - a2;                   \
-            const float a3 = A[r] * lap;                                                            \
-            PRV[r] = a1 + a3;                                                                       \
+        const Halo4 h4 = exchange_nw<NW>(xch, n & 1, w, lane, CUR[0].x, CUR[1].x, CUR[2].y, CUR[3].y); \
+        const f32x2 eU1 = {h4.u1, CUR[3].x}, eU2 = {h4.u2, CUR[2].x};  /* rows (-1,3), (-2,2) */    \
+        const f32x2 eD1 = {CUR[0].y, h4.d1}, eD2 = {CUR[1].y, h4.d2};  /* rows (4,8), (5,9)   */    \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            const f32x2 m1 = i >= 1 ? CUR[i - 1] : eU1;                                             \
+            const f32x2 p1 = i <= 2 ? CUR[i + 1] : eD1;                                             \
+            const f32x2 m2 = i >= 2 ? CUR[i - 2] : (i == 1 ? eU1 : eU2);                            \
+            const f32x2 p2 = i <= 1 ? CUR[i + 2] : (i == 2 ? eD1 : eD2);                            \
+            const f32x2 c = CUR[i];                                                                 \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
+            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
+            f32x2 s1 = m1 + p1; s1 = s1 + xl1; s1 = s1 + xr1;                                       \
+            f32x2 s2 = m2 + p2; s2 = s2 + xl2; s2 = s2 + xr2;                                       \
+            f32x2 lap = kC2 * s1; const f32x2 l2 = kC3 * s2; lap = lap + l2;                        \
+            f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
+            const f32x2 a3 = A[i] * lap;                                                            \
+            PRV[i] = a1 + a3;                                                                       \
         }                                                                                           \
         if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
             unsigned sm_ = smask;                                                                   \
@@ -901,27 +913,28 @@ struct FwdPtArgs {
             /* x + (-0) == x bit for bit: the other lanes add -0 instead of branching */            \
             const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if ((sm_ >> r) & 1u) PRV[r] = PRV[r] + add;                                         \
+                if ((sm_ >> r) & 1u) PT_AT(PRV, r) = PT_AT(PRV, r) + add;                                         \
         }                                                                                           \
         if (!RDQ_EXP_NOSTORE && a.hist) {   /* own cells only; issued at once (the faster of the     \
                                                store placements measured: tools/exp_variants.sh) */ \
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
-            _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PRV[r], hv[r], 0);            \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PT_AT(PRV, r), hv[r], 0);            \
         }                                                                                           \
         if (rrow >= 0 && (n % g.st) == 0) {                                                         \
             float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;                           \
             int rr_ = rrow;                                                                         \
             LAUNDER(rr_);                                                                           \
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if (r == rr_ && rec) SK[rcv0] = PRV[r];                                             \
+                if (r == rr_ && rec) SK[rcv0] = PT_AT(PRV, r);                                             \
             if (rmulti) {                                /* several receivers in one column */      \
                 float v_ = 0.0f;                                                                    \
-                _Pragma("unroll") for (int r = 0; r < R; ++r) if (r == rr_) v_ = PRV[r];            \
+                _Pragma("unroll") for (int r = 0; r < R; ++r) if (r == rr_) v_ = PT_AT(PRV, r);            \
                 for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = v_;                           \
             }                                                                                       \
         }                                                                                           \
     }
 
+#define PT_AT(V, r) V[(r) & 3][(r) >> 2]       // row r of a row-pair array
 template <int T, int NW>
 __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 {
@@ -929,15 +942,16 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    float A[R], C1[R], C2v[R], P0[R], P1[R];
+    f32x2 A[4], C1[4], C2v[4], P0[4], P1[4];              // row pairs {r, r+4}: PT_AT(X, r)
+    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
     unsigned smask = 0;
     int rrow = -1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int gz = wrap_row(uz0 + r, g.Hp);
         const int o = gz * g.ld + gx;
-        A[r] = AL[o]; C1[r] = AL[g.cstride + o]; C2v[r] = AL[2 * g.cstride + o];
-        P0[r] = 0.0f; P1[r] = 0.0f;                       // P_{-1} = P_0 = 0 (pde.py:74-75)
+        PT_AT(A, r) = AL[o]; PT_AT(C1, r) = AL[g.cstride + o]; PT_AT(C2v, r) = AL[2 * g.cstride + o];
+        PT_AT(P0, r) = 0.0f; PT_AT(P1, r) = 0.0f;         // P_{-1} = P_0 = 0 (pde.py:74-75)
         if (gz == g.isz) smask |= 1u << r;
         if (gz == g.igz && ((rin >> r) & 1u)) rrow = r;
     }
@@ -980,7 +994,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         }
         if (T & 1) {   // keep "P1 = newest" at every epoch boundary
 #pragma unroll
-            for (int r = 0; r < R; ++r) { const float tmp = P0[r]; P0[r] = P1[r]; P1[r] = tmp; }
+            for (int i = 0; i < 4; ++i) { const f32x2 tmp = P0[i]; P0[i] = P1[i]; P1[i] = tmp; }
         }
         PT_PROF(tst)
         if (e + 1 < nep) {
@@ -1004,6 +1018,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
 }
 #undef FWD_STEP
+#undef PT_AT
+#define PT_AT(V, r) V[r]                         // adjoint: plain per-row arrays
 
 struct AdjPtArgs {
     TBGeo g;
