@@ -1,4 +1,4 @@
-"""Shot-parallel data parallelism on CPU with the gloo backend, world size 2.
+"""Shot-parallel data parallelism on CPU with the gloo backend, world sizes 2 and 3.
 
 Each rank models a contiguous block of shots; the data-term gradient is summed by ONE
 all-reduce inside backward (red_diffeq.core.inversion.grad_all_reduce) and the misfit is
@@ -53,7 +53,7 @@ def _sharded_grad(rank, world, port, out):
     z = load_golden("grad_small")
     ctx = ctx_of(z)
     ns = 3
-    shots = [(0, 2), (2, 3)][rank]                 # uneven shot blocks on purpose
+    shots = {2: [(0, 2), (2, 3)], 3: [(0, 1), (1, 2), (2, 3)]}[world][rank]   # uneven at world 2
     import numpy as _np
     from oracle.oracle import geometry
     isx, isz, igx, igz = geometry(ctx)
@@ -88,7 +88,8 @@ def _worker(rank, world, port, q):
         q.put(out)
 
 
-def test_shot_parallel_gradient_equals_single_rank():
+@pytest.mark.parametrize("world", [2, 3])
+def test_shot_parallel_gradient_equals_single_rank(world):
     from oracle import oracle as O
     z = load_golden("grad_small")
     ctx = ctx_of(z)
@@ -102,7 +103,7 @@ def test_shot_parallel_gradient_equals_single_rank():
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    ps = [ctxm.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctxm.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     out = q.get(timeout=300)

@@ -11,7 +11,6 @@ build() {  # name, defines
 }
 
 
-build sg8 "-DPT_ADJ_SG=8" &
-build sg2 "-DPT_ADJ_SG=2" &
+build noload "-DRDQ_EXP_NOPLOAD=1"
 wait
 ls -la lib/exp
