@@ -87,6 +87,10 @@ class DiffusionFWI:
         self.ssim_loss = ssim_loss
         self.device = diffusion_model.device
 
+    def _condition(self, denoised, current, step):
+        """Hook after denoising (ILVR_FWI adds its low-frequency conditioning here)."""
+        return denoised
+
     @torch.no_grad()
     def _apply_diffusion_denoising_with_patches(self, current_model, diffusion_step, kernel_size=None,
                                                 stride=None, use_patches=False):
@@ -135,6 +139,7 @@ class DiffusionFWI:
                                         position=0)):
             denoised = self._apply_diffusion_denoising_with_patches(current, step, kernel_size=patch_kernel_size,
                                                                     stride=patch_stride, use_patches=use_patches)
+            denoised = self._condition(denoised, current, step)
             if step != 0:
                 mu_opt = denoised.clone().detach().contiguous().requires_grad_(True)
                 opt = FusedAdamClamp(mu_opt, lr=lr, clamp=None if model_blur else (-1.0, 1.0))

@@ -300,8 +300,57 @@ def gen_dfwi():
     save("dfwi_small", **out)
 
 
+def gen_ilvr():
+    """ILVR_FWI (diffusion_bench/ilvr_fwi.py) on the gen_dfwi case with the q_sample noise drawn from a
+    seeded generator and recorded (the draw is torch.randn_like inside _apply_ilvr), plus the
+    Resizer (diffusion_bench/resizer.py) down/up outputs at the factors the schedule uses."""
+    import types
+    pkg = types.ModuleType("diffusion_bench")
+    pkg.__path__ = ["/root/reference/diffusion_bench"]
+    sys.modules["diffusion_bench"] = pkg
+    ilvr = importlib.import_module("diffusion_bench.ilvr_fwi")
+    rz = importlib.import_module("diffusion_bench.resizer")
+    out = {}
+    g = torch.Generator().manual_seed(17)
+    x = torch.rand(2, 1, 70, 70, generator=g) * 2 - 1
+    out["rz_x"] = x.numpy()
+    for n in (16, 9, 5, 2):
+        d = rz.Resizer(x.shape, 1 / n)(x)
+        u = rz.Resizer((2, 1, int(70 / n), int(70 / n)), n)(d)
+        out[f"rz_down{n}"], out[f"rz_up{n}"] = d.numpy(), u.numpy()
+    ctx = dict(SMALL, n_grid=14, ng=14, ns=2)
+    v_true = synthetic.make_model("curvefault", 14, 14, seed=31, batch=1)
+    y = torch.from_numpy(run_forward(ctx, v_true))
+    init = ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=3.0)
+    diff = ref.diffusion.GaussianDiffusion(_unet_dim8(), image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise").eval()
+    draws = []
+    gen = torch.Generator().manual_seed(23)
+    orig = torch.randn_like
+
+    def seeded_randn_like(t, **kw):
+        r = torch.randn(t.shape, generator=gen, dtype=t.dtype)
+        draws.append(r.numpy().copy())
+        return r
+
+    torch.randn_like = seeded_randn_like
+    try:
+        fwi = make_fwi(ctx)
+        bench = ilvr.ILVR_FWI(diff, fwi, ref.ssim.SSIM(window_size=11))
+        mu, hist = bench.optimize(init.clone(), torch.from_numpy(v_true), y, fwi, ts=3, diffusion_ts=4, lr=0.03,
+                                  ilvr_weight=0.3)
+    finally:
+        torch.randn_like = orig
+    h = hist[0]
+    out.update(v_true=v_true, y=y.numpy(), mu0=init.numpy(), noise=np.stack(draws), mu=mu.detach().numpy(),
+               obs=np.array(h["obs_losses"]).ravel(), ssim=np.array(h["ssim"]).ravel(),
+               mae=np.array(h["mae"]).ravel(), rmse=np.array(h["rmse"]).ravel(), **ctx_arrays(ctx))
+    save("ilvr_small", **out)
+
+
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
-            loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi)
+            loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi,
+            ilvr=gen_ilvr)
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

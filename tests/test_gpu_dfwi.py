@@ -46,3 +46,24 @@ def test_diffusionfwi_vs_reference(cuda, tag, kw):
         assert d.max() < 2e-3, d.max()
     else:
         assert d.mean() < 2e-3, (d.mean(), d.max())
+
+
+def test_ilvr_fwi_vs_reference(cuda):
+    """ILVR_FWI (diffusion_bench/ilvr_fwi.py) with the reference's recorded q_sample noise injected."""
+    from diffusion_bench import ILVR_FWI
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden("ilvr_small")
+    ctx = ctx_of(z)
+    fwi = FWIForward(dict(ctx), cuda, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
+    bench = ILVR_FWI(_diffusion(cuda), fwi, SSIM())
+    draws = iter(torch.from_numpy(z["noise"]))
+    bench.randn_like = lambda t: next(draws).to(t.device)
+    mu, hist = bench.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
+                              torch.from_numpy(z["y"]).to(cuda), fwi, ts=3, diffusion_ts=4, lr=0.03, ilvr_weight=0.3)
+    h = hist[0]
+    for k in ("obs", "ssim", "mae", "rmse"):
+        key = "obs_losses" if k == "obs" else k
+        np.testing.assert_allclose(np.array(h[key]), z[k], rtol=2e-3, err_msg=k)
+    assert np.abs(mu.cpu().numpy() - z["mu"]).max() < 2e-3

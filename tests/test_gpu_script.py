@@ -72,3 +72,49 @@ def test_run_inversion_script_tiny_dataset(cuda, tmp_path):
                            ts=3, lr=cfg.optimization.lr, reg_lambda=0.01, regularization="tv")
     np.testing.assert_array_equal(mu[1, 0].detach().cpu().numpy(), z["result"])
     np.testing.assert_array_equal(np.array(res[1]["rmse"]), z["rmse"])
+
+
+@pytest.mark.parametrize("method", ["diffusionfwi", "ilvr"])
+def test_run_bench_script_tiny_dataset(cuda, tmp_path, method):
+    """scripts/run_bench.py (drop-in for diffusion_bench/run_bench.py): both methods over a tiny
+    OpenFWI-layout dataset, the reference's results layout and keys (run_bench.py:152-183)."""
+    import sys
+    from red_diffeq import get_config
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.synthetic import make_model
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    spec = importlib.util.spec_from_file_location("run_bench", os.path.join(ROOT, "scripts", "run_bench.py"))
+    rb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rb)
+    cfg = get_config()
+    cfg.pde.nt = 200
+    cfg.pde.ns = 2
+    cfg.model.dim = 8
+    cfg.optimization.ts = 2
+    cfg.optimization.diffusion_ts = 3
+    cfg.experiment.random_seed = 8888
+    root = tmp_path / "dataset" / "OpenFWI"
+    (root / "Seismic_Data").mkdir(parents=True)
+    (root / "Velocity_Data").mkdir(parents=True)
+    vel = make_model("curvevel", 70, 70, seed=4, batch=2)
+    fwi = FWIForward(cfg.pde.to_dict(), cuda, normalize=True, v_denorm_func=v_denormalize,
+                     s_norm_func=s_normalize_none)
+    with torch.no_grad():
+        seis = fwi(v_normalize(torch.from_numpy(vel)).to(cuda)).cpu().numpy()
+    np.save(root / "Seismic_Data" / "CV.npy", seis)
+    np.save(root / "Velocity_Data" / "CV.npy", vel)
+    cfg.data.seismic_data_dir = str(root / "Seismic_Data")
+    cfg.data.velocity_data_dir = str(root / "Velocity_Data")
+    cfg.data.batch_size = 2
+    cfg.experiment.results_dir = str(tmp_path / "out")
+    cfg.experiment.name = "bench_" + method
+    cfg.diffusion.model_path = str(tmp_path / "absent.pt")
+    out = rb.run_experiment(cfg, method=method)
+    files = sorted((out / "CV").glob("*_results.npz"))
+    assert [f.name for f in files] == ["0_results.npz", "1_results.npz"]
+    z = np.load(files[0])
+    assert set(z.files) == {"result", "initial_velocity", "ground_truth", "total_losses", "obs_losses", "ssim",
+                            "mae", "rmse"}
+    assert z["result"].shape == (70, 70) and z["rmse"].shape == (3,)
+    assert np.isfinite(z["result"]).all() and np.abs(z["result"]).max() <= 1.0

@@ -229,3 +229,19 @@ def test_diffusion_bench_patch_split_merge_and_smoothing():
     for s in (0.7, 1.0, 2.5):
         ref = gaussian_filter(gr.numpy().astype(np.float64), sigma=[0, 0, s, s])
         np.testing.assert_allclose(_gaussian_smooth(gr, s).numpy(), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_ilvr_resampler_vs_reference_fixture():
+    """ILVR's bicubic antialiased resampler restated as per-axis weight matrices
+    (diffusion_bench/ilvr_fwi.py) vs the reference's Resizer outputs (tests/golden/ilvr_small.npz,
+    made by running diffusion_bench/resizer.py), down by 1/N and back up, N in {16, 9, 5, 2}."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+    from diffusion_bench.ilvr_fwi import resize
+    z = load_golden("ilvr_small")
+    x = torch.from_numpy(z["rz_x"])
+    for n in (16, 9, 5, 2):
+        d = resize(x, 1.0 / n)
+        np.testing.assert_allclose(d.numpy(), z[f"rz_down{n}"], rtol=0, atol=1e-6)
+        u = resize(torch.from_numpy(z[f"rz_down{n}"]), float(n), in_hw=(int(70 / n), int(70 / n)))
+        np.testing.assert_allclose(u.numpy(), z[f"rz_up{n}"], rtol=0, atol=1e-6)
