@@ -643,6 +643,9 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 #define RDQ_EXP_NOSTORE 0
 #endif
 constexpr int CP_SC1 = 16;
+#ifndef RDQ_EXP_NOINEPOCH
+#define RDQ_EXP_NOINEPOCH 0   // timing experiment: skip the in-epoch history prefetch (wrong results)
+#endif
 #ifndef PT_ADJ_SG
 #define PT_ADJ_SG 4   // adjoint hand-off sweep: rows per load group (register budget)
 #endif
@@ -1047,7 +1050,7 @@ struct AdjPtArgs {
 // one adjoint step k; CUR = L_{k+1}, PRV = L_{k+2} -> L_k, P = P_{k-1} rows -2..9
 #define ADJ_STEP(CUR, PRV, P, PN)                                                                   \
     {                                                                                               \
-        if (t + 1 < T) ADJ_PLOAD(PN, k - 1)         /* every wave (OOB offsets off the interior) */ \
+        if (t + 1 < T && !RDQ_EXP_NOINEPOCH) ADJ_PLOAD(PN, k - 1)  /* OOB offsets off the interior */ \
         const float dcur = dv[t];                                                                   \
         float q[R];                                                                                 \
         _Pragma("unroll") for (int r = 0; r < R; ++r) q[r] = A[r] * CUR[r];                         \

@@ -1,5 +1,5 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-for v in base noload; do
+for v in base noload noinepoch; do
   if [ $v = base ]; then unset RDQ_EXP_LIB; else export RDQ_EXP_LIB=$v.so; fi
   timeout -k 10 120 python tools/sweep_tb.py --only 4 --profile --reps 3 > gpurun_out/exp_$v.log 2>&1 || exit 1
   echo "== $v"; python -c "

@@ -11,6 +11,7 @@ build() {  # name, defines
 }
 
 
-build noload "-DRDQ_EXP_NOPLOAD=1"
+build noload "-DRDQ_EXP_NOPLOAD=1" &
+build noinepoch "-DRDQ_EXP_NOINEPOCH=1" &
 wait
 ls -la lib/exp
