@@ -11,6 +11,7 @@ ddim/p_sample loops) are out of scope.
 The arithmetic of every block goes through ``red_diffeq.models.unet_ops``.
 """
 import math
+import os
 from collections import namedtuple
 from functools import partial
 
@@ -234,11 +235,46 @@ class Unet(nn.Module):
             return ops.conv2d(x, m[1], mode=ops.UPSAMPLE2)               # nearest x2 folded in
         return ops.conv2d(x, m[1], mode=ops.UNSHUFFLE2)                  # pixel-unshuffle folded in
 
+    # Small no-grad forwards (the RED regulariser's per-iteration call, B = 1..16 at 72 x 72) are
+    # launch-bound: ~150 kernels of a few microseconds.  They are captured once per (shape,
+    # precision, weights version) into a hipGraph and replayed (RDQ_NO_UNET_GRAPH=1 disables).
+    GRAPH_MAX_PIXELS = 16 * 72 * 72
+
     def forward(self, x, time, x_self_cond=None):
         assert all(divisible_by(d, self.downsample_factor) for d in x.shape[-2:]), \
             f"your input dimensions {x.shape[-2:]} need to be divisible by {self.downsample_factor}, given the unet"
+        if (x.is_cuda and not torch.is_grad_enabled() and x_self_cond is None and not self.self_condition
+                and x.shape[0] * x.shape[2] * x.shape[3] <= self.GRAPH_MAX_PIXELS
+                and not os.environ.get("RDQ_NO_UNET_GRAPH")
+                and not torch.cuda.is_current_stream_capturing()):
+            return self._graphed(x, time)
         with ops.precision(self.precision):
             return self._forward(x, time, x_self_cond)
+
+    def _weights_version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def _graphed(self, x, time):
+        key = (tuple(x.shape), x.dtype, x.device, self.precision, time.dtype)
+        cache = self.__dict__.setdefault("_graphs", {})
+        ver = self._weights_version()
+        ent = cache.get(key)
+        if ent is None or ent["ver"] != ver:
+            xs, ts = x.detach().clone(), time.detach().clone()
+            side = torch.cuda.Stream(device=x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.stream(side), ops.precision(self.precision):
+                self._forward(xs, ts, None)            # warm-up: weight packs, workspaces, code objects
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph), ops.precision(self.precision):
+                ys = self._forward(xs, ts, None)
+            ent = {"ver": ver, "graph": graph, "x": xs, "t": ts, "y": ys}
+            cache[key] = ent
+        ent["x"].copy_(x)
+        ent["t"].copy_(time)
+        ent["graph"].replay()
+        return ent["y"].clone()
 
     def _forward(self, x, time, x_self_cond):
         if self.self_condition:

@@ -32,11 +32,13 @@ def conv_flops(net, x, t):
         return y
 
     ops.conv2d = counting
+    os.environ["RDQ_NO_UNET_GRAPH"] = "1"          # one eager forward (a graph capture runs it twice)
     try:
         with torch.no_grad():
             net(x, t)
     finally:
         ops.conv2d = orig
+        del os.environ["RDQ_NO_UNET_GRAPH"]
     return tot[0]
 
 
@@ -51,11 +53,13 @@ def conv_shapes(net, x, t):
         return orig(x, conv, x2=x2, mode=mode, residual=residual)
 
     ops.conv2d = rec
+    os.environ["RDQ_NO_UNET_GRAPH"] = "1"
     try:
         with torch.no_grad():
             net(x, t)
     finally:
         ops.conv2d = orig
+        del os.environ["RDQ_NO_UNET_GRAPH"]
     return calls
 
 
@@ -112,10 +116,14 @@ def main():
             continue
         fl = conv_flops(net, x, t)
         with torch.no_grad():
-            hip_ms = time_fn(lambda: net(x, t), a.reps)
+            hip_ms = time_fn(lambda: net(x, t), a.reps)             # default path (graph replay if small)
+            os.environ["RDQ_NO_UNET_GRAPH"] = "1"
+            eager_ms = time_fn(lambda: net(x, t), a.reps)
+            del os.environ["RDQ_NO_UNET_GRAPH"]
             ref_ms = time_fn(lambda: R.unet_forward(net, x, t), a.reps)
             d = (net(x, t) - R.unet_forward(net, x, t)).abs().max().item()
         out = {"B": B, "H": a.H, "conv_gflop": round(fl / 1e9, 3), "hip_ms": round(hip_ms, 3),
+               "hip_eager_launch_ms": round(eager_ms, 3),
                "torch_eager_ms": round(ref_ms, 3), "hip_conv_tflops": round(fl / hip_ms / 1e9, 2),
                "mfma_frac_of_fp32_peak": round(fl / hip_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4),
                "max_abs_diff_vs_torch": d}
