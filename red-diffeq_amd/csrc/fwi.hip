@@ -455,8 +455,6 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     __shared__ float xch[2][TB_NW][4][64];
     __shared__ float pxc[2][TB_NW][4][64];
     __shared__ double red[64 * TB_NW];
-    __shared__ float gal[TB_RH][64];   // gA_s accumulators of the region (interior used)
-    __shared__ float kal[TB_RH][64];   // sponge coefficient K of the region
     const TBGeo &g = a.g;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -472,6 +470,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     const float *KAp = AL + 3 * g.cstride;
     const int isx = g.isx[s];
     float A[TB_R], L0[TB_R], L1[TB_R];   // temp1/temp2 are re-derived from A and K (bit-identical)
+    float gal[TB_R], kal[TB_R];          // gA_s accumulators and the sponge coefficient K, in registers
     int rofs[TB_R];
     unsigned rin = 0, pmask = 0, smask = 0, rmask = 0;   // wave-uniform row masks
 #pragma unroll
@@ -480,7 +479,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         rofs[r] = gz * g.ld;
         const int o = rofs[r] + gx;
         A[r] = AL[o];
-        kal[w * TB_R + r][lane] = KAp[o];
+        kal[r] = KAp[o];
         L1[r] = a.in_l1[so + o];     // L_{k+1}
         L0[r] = a.in_l2[so + o];     // L_{k+2}
         const int rr = w * TB_R + r;
@@ -488,7 +487,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         if (rr >= H - 2 && rr < TB_RH - H + 2) pmask |= 1u << r;
         if (gz == g.isz) smask |= 1u << r;
         if (gz == g.igz) rmask |= 1u << r;
-        gal[rr][lane] = ((rin & (1u << r)) && xin) ? a.gA[so + o] : 0.0f;
+        gal[r] = ((rin & (1u << r)) && xin) ? a.gA[so + o] : 0.0f;
     }
     const bool scol = gx == isx;
     const int rs = rmask ? g.rcv_start[gx] : 0, re = rmask ? g.rcv_start[gx + 1] : 0;
@@ -547,7 +546,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
             float n1 = qm1 + qp1; n1 = n1 + xl1; n1 = n1 + xr1;
             float n2 = qm2 + qp2; n2 = n2 + xl2; n2 = n2 + xr2;
             float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;
-            const float kp = kal[w * TB_R + r][lane];
+            const float kp = kal[r];
             float t1 = C1X2 * A[r]; t1 = t1 + 2.0f; t1 = t1 - kp;     // pde.py:69
             const float t2 = 1.0f - kp;                               // pde.py:70
             float l = t1 * cur[r]; const float l2 = t2 * prv[r]; l = l - l2; l = l + nb;
@@ -579,9 +578,9 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
                 float d = C1X2 * pc; d = d + lap;
                 const float l = prv[r];
                 const float c = l * d;
-                float &ga = gal[w * TB_R + r][lane];
+                float &ga = gal[r];
                 ga = ga + c;
-                float kk = kal[w * TB_R + r][lane] * pc; const float dl = cur[r] - l; kk = kk * dl;  // fp32 term,
+                float kk = kal[r] * pc; const float dl = cur[r] - l; kk = kk * dl;  // fp32 term,
                 ksum += (double)kk;                                                             // fp64 sum
                 if ((smask & (1u << r)) && scol) { const float gb = l * a.w[t]; gbacc = gbacc + gb; }
             }
@@ -595,7 +594,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
                 const size_t o = so + rofs[r] + gx;
                 a.out_l1[o] = odd ? L0[r] : L1[r];
                 a.out_l2[o] = odd ? L1[r] : L0[r];
-                a.gA[o] = gal[w * TB_R + r][lane];
+                a.gA[o] = gal[r];
             }
     }
     if (gbl) a.gbeta[bs] = gbacc;
