@@ -77,9 +77,10 @@ int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
  * 1..4) and the number of concurrent shot-group launch chains (1..16).  Results are identical
  * for every setting; only speed changes. */
 int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
-/* Kernel variant flags (default 0):
- *   RDQ_VARIANT_FWD_GEN    the chunked forward regenerates alpha/temp1/temp2 from the 20 KB model in
- *                          registers instead of loading the three K3 fields (identical results);
+/* Kernel variant flags (a new plan starts at RDQ_VARIANT_FWD_GEN):
+ *   RDQ_VARIANT_FWD_GEN    the chunked forward regenerates alpha/temp1/temp2 from the model in
+ *                          registers instead of loading the three K3 fields (identical results;
+ *                          14% faster on the configs[4] grid);
  *   RDQ_VARIANT_ADJ_EXACT  the persistent adjoint keeps the oracle's exact fp32 operation order (gA
  *                          bit-identical to oracle/fwi_oracle.c) instead of contracting into FMAs and
  *                          accumulating the sponge term per cell in fp32 (faster; within 1e-6);

@@ -478,8 +478,8 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         const int uz = uz0 + r, gz = wrapn(uz, g.Hp);
         rofs[r] = gz * g.ld;
         const int o = rofs[r] + gx;
-        A[r] = AL[o];
-        kal[r] = KAp[o];
+        A[r] = AL[o];                // (regenerating alpha / K from the model, as the forward does,
+        kal[r] = KAp[o];             //  measured 5% slower here: the loads are cheaper than the math)
         L1[r] = a.in_l1[so + o];     // L_{k+1}
         L0[r] = a.in_l2[so + o];     // L_{k+2}
         const int rr = w * TB_R + r;
@@ -1529,7 +1529,7 @@ struct rdq_fwi_plan {
     int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
-    bool fwd_gen = false;       // forward regenerates coefficients from the model (vs loading K3)
+    bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;

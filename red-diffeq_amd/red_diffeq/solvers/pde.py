@@ -78,7 +78,7 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
-    def set_variant(self, fwd_gen_coeffs=False, adj_exact=False, xcd_local=True):
+    def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True):
         """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
         the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction; xcd_local:
         persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs."""

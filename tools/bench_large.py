@@ -27,12 +27,15 @@ ap.add_argument("--nx", type=int, default=3000)
 ap.add_argument("--nt", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--T", type=str, default="2,3,4", help="blocking depths to time")
+ap.add_argument("--no-gen", action="store_true",
+                help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = dict(n_grid=a.nx, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=a.nx, ns=a.ns)
 fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
 v = v_normalize(torch.from_numpy(make_model("curvefault", a.nz, a.nx, batch=1))).to(dev)
 plan = fwi._plan(a.nz, a.nx, dev)
+plan.set_variant(fwd_gen_coeffs=not a.no_gen)
 sz = plan.sizes(1)
 npad = sz.Hp * sz.Wp
 dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
@@ -58,7 +61,7 @@ for T in [int(t) for t in a.T.split(",")]:
     plan.status()
     f, d = min(fw), min(ad)
     shot_steps = a.ns * a.nt
-    print(json.dumps({"T": T, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
                       "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
                       "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
                       "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
