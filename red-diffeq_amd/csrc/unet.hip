@@ -16,6 +16,8 @@
 #include <cmath>
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 
 #include "red_diffeq_unet.h"
 
@@ -781,6 +783,212 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
     }
 }
 
+// ------------------------------------------------------------- conv2d 3x3, bf16, halo-staged
+// The per-tap kernel above re-gathers the input for each of the nine taps and waits one global
+// round trip per 32-deep K stage: at the batched U-Net's sizes (configs[4]: 344 tiles) that latency,
+// not the MFMA, sets its rate.  Here a workgroup owns 256 consecutive output pixels (flattened
+// b, h, w) x 64 output channels and walks the reduction chunk-major: the input of a 32-channel chunk
+// is gathered ONCE into LDS as the tile's halo in flattened pixel space -- rows m0 - W - 1 ..
+// m0 + 256 + W, so tap (ky, kx) of output m reads halo row (m - m0) + ky W + kx -- and the nine taps
+// run from it; a lane zeroes its B fragment where the tap leaves the image (the flattened neighbour
+// is the wrong pixel there).  Weights stream per tap through a two-slot LDS ring from a nine-tap
+// register ring (the next chunk's tap t is fetched at tap t); the next chunk's halo is gathered
+// (one 8-channel item per tap, rounded to bf16 and stored two taps later) into the other of two LDS
+// halo buffers while this chunk's MFMAs run.  4 waves x (64 pixels x 64 channels): 64
+// accumulator registers, two waves per SIMD.  Halo rows are 80 B (BF_LD): the lanes of every
+// ds_read_b128 group read 16 consecutive rows, conflict-free at that stride.
+constexpr int C3_BM = 256, C3_BN = 64, C3_NI = 7, C3_WMAX = 72;
+constexpr int C3_ROWS = C3_BM + 2 * C3_WMAX + 2;  // 402 <= 64 * C3_NI
+
+struct C3Args {
+    rdq_conv_desc d;
+    const float *x, *x2, *bias, *res;
+    const __bf16 *w;                 // [cout][9][cinp]
+    float *y;
+    int cinp, K, M, HW, R, cch, plane;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
+{
+    __shared__ __attribute__((aligned(16))) __bf16 Hs[2][C3_ROWS][BF_LD];     // 2 x 31.4 KiB
+    __shared__ __attribute__((aligned(16))) __bf16 Ws[2][C3_BN][BF_LD];
+    const rdq_conv_desc &d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * C3_BM, n0 = blockIdx.y * C3_BN;
+    const int cin = d.cin1 + d.cin2;
+    // halo items: wave wv gathers the chunk's 8-channel group wv (so the source tensor and the
+    // channel base are wave-uniform) for halo rows q = lane + 64 k; the source pixel is packed
+    // b << 20 | pix (~0u: outside the batch or past the halo -> zeros)
+    unsigned it_src[C3_NI];
+#pragma unroll
+    for (int k = 0; k < C3_NI; ++k) {
+        const int q = lane + 64 * k, p = m0 - d.W - 1 + q;
+        const bool in = q < a.R && p >= 0 && p < a.M;
+        const int b = in ? p / a.HW : 0, pp = in ? p - b * a.HW : 0;
+        int pix = pp;
+        if constexpr (MODE == RDQ_IN_UPSAMPLE2) {
+            const int ih = pp / d.W, iw = pp - ih * d.W;
+            pix = (ih >> 1) * (d.W >> 1) + (iw >> 1);
+        }
+        it_src[k] = in ? ((unsigned)b << 20 | (unsigned)pix) : ~0u;
+    }
+    // one item's 8 channels of chunk cc: unconditional loads at 32-bit offsets from a wave-uniform
+    // base (offset 0 where the item is empty), so the compiler never waits per load; the zeroing
+    // happens when the item is rounded
+    auto hload = [&](int k, int cc, float (&v)[8]) -> bool {
+        const unsigned s = it_src[k];
+        const int c = cc * BF_BK + 8 * wv;
+        const bool lo = c < d.cin1;
+        const float *__restrict__ base = lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
+        const unsigned cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane;
+        const bool ok = s != ~0u && c < cin;
+        const unsigned o = ok ? (s >> 20) * cstride + (s & 0xfffff) : 0u;
+        if (c >= cin) base = a.x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = base[o + (unsigned)(j * a.plane)];
+        return ok;
+    };
+    auto hpack = [&](const float (&v)[8], bool ok) -> bf16x8 {
+        bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (__bf16)(ok ? v[j] : 0.0f);
+        return h;
+    };
+    auto hstore = [&](int buf, int k, const bf16x8 &h) {
+        const int q = lane + 64 * k;
+        if (q < a.R) *reinterpret_cast<bf16x8 *>(&Hs[buf][q][8 * wv]) = h;
+    };
+    // weight role: row wn (of 64), 8-channel piece wq of the tap's 32
+    const int wn = tid >> 2, wq = (tid & 3) * 8;
+    const __bf16 *wrow = a.w + (size_t)(n0 + wn) * a.K + wq;
+    auto wload = [&](int cc, int t) -> bf16x8 {
+        return *reinterpret_cast<const bf16x8 *>(wrow + t * a.cinp + cc * BF_BK);
+    };
+    auto wstash = [&](int buf, const bf16x8 &v) { *reinterpret_cast<bf16x8 *>(&Ws[buf][wn][wq]) = v; };
+    // MFMA role: wave wv owns pixels wv*64 + mb*32 + (lane & 31), mb = 0, 1; bit ky*3+kx of tmask[mb]
+    // says whether tap (ky, kx) stays inside the image for this lane's pixel
+    int pl[2];
+    unsigned tmask[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        pl[mb] = wv * 64 + mb * 32 + (lane & 31);
+        const int m = m0 + pl[mb];
+        const int pix = m < a.M ? m % a.HW : 0, oh = pix / d.W, ow = pix - oh * d.W;
+        unsigned bits = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ih = oh + t / 3 - 1, iw = ow + t % 3 - 1;
+            bits |= ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W) ? 1u << t : 0u;
+        }
+        tmask[mb] = m < a.M ? bits : 0u;
+    }
+    const int kh = 8 * (lane >> 5);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) acc[c][mb] = f32x16{};
+
+    {   // chunk 0's halo
+        float v[C3_NI][8];
+        bool ok[C3_NI];
+#pragma unroll
+        for (int k = 0; k < C3_NI; ++k) ok[k] = hload(k, 0, v[k]);
+#pragma unroll
+        for (int k = 0; k < C3_NI; ++k) hstore(0, k, hpack(v[k], ok[k]));
+    }
+    // weight ring: the nine taps of a chunk in registers, the next chunk's tap t fetched at tap t
+    // (eight stages before its stash)
+    bf16x8 wr[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wr[t] = wload(0, t);
+    wstash(0, wr[0]);
+    __syncthreads();
+
+    // one chunk: nine taps; PF = whether the next chunk's halo is gathered meanwhile
+    auto chunk = [&](int cc, auto pf) {
+        constexpr bool PF = decltype(pf)::value;
+        float hv[3][8];
+        bool hok[3];
+        const int hb = cc & 1;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int s = cc * 9 + t;
+            if constexpr (PF) wr[t] = wload(cc + 1, t);
+            if constexpr (PF) {
+                if (t < C3_NI) hok[t % 3] = hload(t, cc + 1, hv[t % 3]);
+                if (t >= 2 && t - 2 < C3_NI) hstore(hb ^ 1, t - 2, hpack(hv[(t - 2) % 3], hok[(t - 2) % 3]));
+            }
+            const int toff = (t / 3) * d.W + t % 3;
+            const __bf16 *wsb = &Ws[s & 1][0][0];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int kk = 16 * ks + kh;
+                bf16x8 bfr[2], afr[2];
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) {
+                    bf16x8 v = *reinterpret_cast<const bf16x8 *>(&Hs[hb][pl[mb] + toff][kk]);
+                    if (!((tmask[mb] >> t) & 1u)) v = bf16x8{};
+                    bfr[mb] = v;
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    afr[c] = *reinterpret_cast<const bf16x8 *>(wsb + (c * 32 + (lane & 31)) * BF_LD + kk);
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+                        acc[c][mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[c], bfr[mb], acc[c][mb], 0, 0, 0);
+            }
+            if (PF || t < 8) wstash((s + 1) & 1, wr[(t + 1) % 9]);
+            __syncthreads();
+        }
+    };
+    for (int cc = 0; cc + 1 < a.cch; ++cc) chunk(cc, std::true_type{});
+    chunk(a.cch - 1, std::false_type{});
+
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int m = m0 + pl[mb];
+        const int mc = min(m, a.M - 1), b = mc / a.HW, pix = mc - b * a.HW;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float ov[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const float rv = a.res ? a.res[((size_t)b * d.cout + n) * a.HW + pix] : 0.0f;
+                const float bv = a.bias ? a.bias[n] : 0.0f;
+                ov[r] = (acc[c][mb][r] + bv) + rv;
+                asm volatile("" : "+v"(ov[r]));
+            }
+            if (m < a.M) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.y[((size_t)b * d.cout + n) * a.HW + pix] = ov[r];
+                }
+            }
+        }
+    }
+}
+
+// the halo-staged kernel takes 3x3 / pad 1 convs (plain, with a concatenated skip, or on a nearest-
+// upsampled input) whose tile grid fills the chip; everything else stays on the per-tap kernel
+bool conv3_ok(const rdq_conv_desc *d)
+{
+    if (d->kh != 3 || d->kw != 3 || d->pad != 1) return false;
+    if (d->in_mode != RDQ_IN_PLAIN && d->in_mode != RDQ_IN_UPSAMPLE2) return false;
+    if (d->cin1 % 8 || d->cin2 % 8 || d->cout % C3_BN || d->W > C3_WMAX || d->B >= 4096) return false;
+    const int64_t HW = (int64_t)d->H * d->W, M = d->B * HW;
+    if (HW >= (1 << 20) || M >= (int64_t)1 << 30) return false;
+    // the halo gather addresses each input tensor with 32-bit element offsets
+    const int64_t plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? HW / 4 : HW;
+    if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane >= (int64_t)1 << 32) return false;
+    return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN) >= 512;
+}
+
 int bf_cinp(const rdq_conv_desc *d) { return (d->cin1 + d->cin2 + BF_BK - 1) / BF_BK * BF_BK; }
 
 // split count as ig_splits: about two workgroups per CU over the tile grid, >= 4 K stages each
@@ -891,6 +1099,24 @@ int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, con
 {
     if (!conv_desc_ok(d) || !x || !wp || !y || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
         return RDQ_E_INVALID;
+    if (conv3_ok(d) && !getenv("RDQ_NO_CONV3")) {
+        C3Args c{};
+        c.d = *d; c.x = x; c.x2 = x2; c.w = static_cast<const __bf16 *>(wp); c.bias = bias; c.res = residual; c.y = y;
+        c.cinp = bf_cinp(d);
+        c.K = 9 * c.cinp;
+        c.HW = d->H * d->W;
+        c.M = d->B * c.HW;
+        c.R = C3_BM + 2 * d->W + 2;
+        c.cch = c.cinp / BF_BK;
+        c.plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? c.HW / 4 : c.HW;
+        const dim3 grid((c.M + C3_BM - 1) / C3_BM, d->cout / C3_BN);
+        if (d->in_mode == RDQ_IN_UPSAMPLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+        RDQ_CHECK(hipGetLastError());
+        return 0;
+    }
     BfArgs a{};
     a.d = *d; a.x = x; a.x2 = x2; a.w = static_cast<const __bf16 *>(wp); a.bias = bias; a.res = residual; a.y = y;
     a.part = static_cast<float *>(ws);

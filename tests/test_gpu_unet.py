@@ -187,6 +187,40 @@ def test_conv_bf16_concat_residual_upsample_unshuffle(cuda):
     close(got_dn, F.conv2d(_bf(R.pixel_unshuffle2(a)), _bf(dn.weight), dn.bias))
 
 
+@pytest.mark.parametrize("cin1,cin2,cout,H,B,mode,res", [
+    (64, 0, 64, 72, 26, "plain", False),        # tiles straddle images (5184 % 256 = 64), ragged last tile
+    (64, 64, 64, 36, 102, "plain", True),       # concatenated skip + residual (decoder ResNet block)
+    (24, 16, 128, 36, 52, "plain", False),      # channel padding inside a chunk (40 -> 64), 2 cout tiles
+    (128, 0, 128, 18, 51, "up", False),         # nearest-upsampled input (18 -> 36)
+    (256, 256, 512, 9, 203, "plain", True),     # 9 x 9 level: halo of 256 + 20 rows, 8 cout tiles
+])
+def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
+    """The halo-staged 3x3 kernel (batched U-Net sizes, >= 512 tiles of 256 pixels x 64 channels):
+    against the fp32 torch conv of the bf16-rounded operands, and against the per-tap bf16 kernel
+    (RDQ_NO_CONV3) with which it shares the operand rounding."""
+    import os
+    from red_diffeq.models import unet_ops as ops
+    F = torch.nn.functional
+    torch.manual_seed(14)
+    Hin = H // 2 if mode == "up" else H
+    conv = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    a = torch.randn(B, cin1, Hin, Hin, device=cuda)
+    b = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    r = torch.randn(B, cout, H, H, device=cuda) if res else None
+    md = ops.UPSAMPLE2 if mode == "up" else ops.PLAIN
+    with ops.precision("bf16"):
+        got = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
+        os.environ["RDQ_NO_CONV3"] = "1"
+        try:
+            per_tap = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
+        finally:
+            del os.environ["RDQ_NO_CONV3"]
+    xin = R.upsample_nearest2(a) if mode == "up" else (torch.cat((a, b), 1) if cin2 else a)
+    ref = F.conv2d(_bf(xin), _bf(conv.weight), conv.bias, padding=1) + (r if res else 0)
+    close(got, ref, rel=2e-5)
+    close(got, per_tap, rel=2e-5)
+
+
 def test_unet_bf16_close_to_fp32(cuda):
     """Whole U-Net (reference architecture, dim 64) with bf16 convolutions vs fp32: new behaviour
     (configs[4]), no reference counterpart; the deviation is bounded, not bitwise."""
