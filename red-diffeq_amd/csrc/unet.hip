@@ -752,35 +752,45 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
     if (m >= a.M) return;
     const int b = m / a.HW, pix = m - b * a.HW;
     const size_t slab = (size_t)a.M * d.cout;
+    // residual and bias of ALL the lane's outputs are loaded before the first store (clamped
+    // addresses, conditions hoisted), and every output value is formed before it: gfx9 retires
+    // loads and stores in one in-order count, so a load issued after a store -- or consumed inside
+    // a store's branch -- would wait for the stores already issued (a store round trip per block)
+    if (a.S == 1 && (a.res || a.bias)) {
+        float rv[NB][16] = {}, bv[NB][16] = {};
+        if (a.bias) {
 #pragma unroll
-    for (int c = 0; c < NB; ++c) {
-        // residual / bias of the block's 16 outputs loaded together (clamped addresses, no branch
-        // per element: a conditional load would be waited for one at a time)
-        float rv[16], bv[16];
+            for (int c = 0; c < NB; ++c)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int n = min(n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), d.cout - 1);
-            rv[r] = (a.S == 1 && a.res) ? a.res[((size_t)b * d.cout + n) * a.HW + pix] : 0.0f;
-            bv[r] = (a.S == 1 && a.bias) ? a.bias[n] : 0.0f;
+                for (int r = 0; r < 16; ++r)
+                    bv[c][r] = a.bias[min(n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), d.cout - 1)];
         }
-        // every output value is formed before the first (conditional) store: a loaded value
-        // consumed inside a store's branch block makes the compiler wait vmcnt(0) there, and on
-        // gfx9 that also drains the stores already issued (one store round trip per element)
-        float ov[16];
+        if (a.res) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            ov[r] = a.S == 1 ? (acc[c][r] + bv[r]) + rv[r] : acc[c][r];
-            asm volatile("" : "+v"(ov[r]));
+            for (int c = 0; c < NB; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = min(n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), d.cout - 1);
+                    rv[c][r] = a.res[((size_t)b * d.cout + n) * a.HW + pix];
+                }
         }
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][r] = (acc[c][r] + bv[c][r]) + rv[c][r];
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(acc[c][r]));
+    float *dst = a.S == 1 ? a.y : a.part + split * slab;
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (n >= d.cout) continue;
-            const size_t o = ((size_t)b * d.cout + n) * a.HW + pix;
-            if (a.S == 1) a.y[o] = ov[r];
-            else a.part[split * slab + o] = ov[r];
+            if (n < d.cout) dst[((size_t)b * d.cout + n) * a.HW + pix] = acc[c][r];
         }
-    }
 }
 
 // ------------------------------------------------------------- conv2d 3x3, bf16, halo-staged
@@ -791,10 +801,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
 // is gathered ONCE into LDS as the tile's halo in flattened pixel space -- rows m0 - W - 1 ..
 // m0 + 256 + W, so tap (ky, kx) of output m reads halo row (m - m0) + ky W + kx -- and the nine taps
 // run from it; a lane zeroes its B fragment where the tap leaves the image (the flattened neighbour
-// is the wrong pixel there).  Weights stream per tap through a two-slot LDS ring from a nine-tap
-// register ring (the next chunk's tap t is fetched at tap t); the next chunk's halo is gathered
-// (one 8-channel item per tap, rounded to bf16 and stored two taps later) into the other of two LDS
-// halo buffers while this chunk's MFMAs run.  4 waves x (64 pixels x 64 channels): 64
+// is the wrong pixel there).  Weights stream per tap through a two-slot LDS ring, fetched two taps
+// ahead; the next chunk's halo is gathered (seven 8-channel items over taps 0-4, each rounded to bf16
+// and stored four taps after its loads) into the other of two LDS halo buffers while this chunk's
+// MFMAs run.  4 waves x (64 pixels x 64 channels): 64
 // accumulator registers, two waves per SIMD.  Halo rows are 80 B (BF_LD): the lanes of every
 // ds_read_b128 group read 16 consecutive rows, conflict-free at that stride.
 constexpr int C3_BM = 256, C3_BN = 64, C3_NI = 7, C3_WMAX = 72;
@@ -898,27 +908,33 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 #pragma unroll
         for (int k = 0; k < C3_NI; ++k) hstore(0, k, hpack(v[k], ok[k]));
     }
-    // weight ring: the nine taps of a chunk in registers, the next chunk's tap t fetched at tap t
-    // (eight stages before its stash)
-    bf16x8 wr[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wr[t] = wload(0, t);
+    // weight ring: three taps in registers, fetched two taps before their stash
+    bf16x8 wr[3];
+    wr[0] = wload(0, 0);
+    wr[1] = wload(0, 1);
     wstash(0, wr[0]);
     __syncthreads();
 
     // one chunk: nine taps; PF = whether the next chunk's halo is gathered meanwhile
     auto chunk = [&](int cc, auto pf) {
         constexpr bool PF = decltype(pf)::value;
-        float hv[3][8];
-        bool hok[3];
+        // halo item k of the next chunk: issued at tap IT[k], rounded and stored four taps later
+        // (at most six items in flight: slot k % 6)
+        constexpr int IT[C3_NI] = {0, 0, 1, 1, 2, 3, 4};
+        float hv[6][8];
+        bool hok[6];
         const int hb = cc & 1;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int s = cc * 9 + t;
-            if constexpr (PF) wr[t] = wload(cc + 1, t);
+            wr[(t + 2) % 3] = wload(min(cc + (t + 2) / 9, a.cch - 1), (t + 2) % 9);
             if constexpr (PF) {
-                if (t < C3_NI) hok[t % 3] = hload(t, cc + 1, hv[t % 3]);
-                if (t >= 2 && t - 2 < C3_NI) hstore(hb ^ 1, t - 2, hpack(hv[(t - 2) % 3], hok[(t - 2) % 3]));
+#pragma unroll
+                for (int k = 0; k < C3_NI; ++k)
+                    if (IT[k] + 4 == t) hstore(hb ^ 1, k, hpack(hv[k % 6], hok[k % 6]));
+#pragma unroll
+                for (int k = 0; k < C3_NI; ++k)
+                    if (IT[k] == t) hok[k % 6] = hload(k, cc + 1, hv[k % 6]);
             }
             const int toff = (t / 3) * d.W + t % 3;
             const __bf16 *wsb = &Ws[s & 1][0][0];
@@ -941,36 +957,59 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
                     for (int mb = 0; mb < 2; ++mb)
                         acc[c][mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[c], bfr[mb], acc[c][mb], 0, 0, 0);
             }
-            if (PF || t < 8) wstash((s + 1) & 1, wr[(t + 1) % 9]);
+            wstash((s + 1) & 1, wr[(t + 1) % 3]);
             __syncthreads();
         }
     };
     for (int cc = 0; cc + 1 < a.cch; ++cc) chunk(cc, std::true_type{});
     chunk(a.cch - 1, std::false_type{});
 
+    // epilogue: the bias and residual of all 64 outputs of the lane are loaded before the first
+    // store (gfx9 retires stores and loads in one in-order count: a load issued after a store would
+    // wait for it), then every output is formed, then stored
+    int ob[2], opix[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
-        const int m = m0 + pl[mb];
-        const int mc = min(m, a.M - 1), b = mc / a.HW, pix = mc - b * a.HW;
+        const int mc = min(m0 + pl[mb], a.M - 1);
+        ob[mb] = mc / a.HW;
+        opix[mb] = mc - ob[mb] * a.HW;
+    }
+    float bv[2][16] = {}, rv[2][2][16] = {};
+    if (a.bias) {                       // (conditions hoisted: a per-element "load or 0" would make
+#pragma unroll                          //  the compiler branch and wait around every load)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            float ov[16];
+            for (int r = 0; r < 16; ++r) bv[c][r] = a.bias[n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+    }
+    if (a.res) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const float rv = a.res ? a.res[((size_t)b * d.cout + n) * a.HW + pix] : 0.0f;
-                const float bv = a.bias ? a.bias[n] : 0.0f;
-                ov[r] = (acc[c][mb][r] + bv) + rv;
-                asm volatile("" : "+v"(ov[r]));
-            }
-            if (m < a.M) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    a.y[((size_t)b * d.cout + n) * a.HW + pix] = ov[r];
-                }
+                for (int mb = 0; mb < 2; ++mb) rv[mb][c][r] = a.res[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]];
             }
-        }
+    }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[c][mb][r] = (acc[c][mb][r] + bv[c][r]) + rv[mb][c][r];
+                asm volatile("" : "+v"(acc[c][mb][r]));
+            }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        if (m0 + pl[mb] >= a.M) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
+            }
     }
 }
 
