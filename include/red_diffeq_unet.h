@@ -51,7 +51,8 @@ int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, con
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
 /* GroupNorm(G) -> [x*(scale+1)+shift] -> SiLU  (Block.forward, diffusion.py:142-149).
- * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes. */
+ * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes (fp64
+ * chunk partials of sum / sum of squares, then the per-(sample, group) mean and 1/std). */
 size_t rdq_group_norm_ws_bytes(int32_t B, int32_t C, int32_t HW, int32_t G);
 int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, const float *x, const float *gamma,
                         const float *beta, const float *scale_shift, float *y, void *ws, hipStream_t stream);
@@ -69,7 +70,8 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
 
 /* LinearAttention core (diffusion.py:182-194; dh <= 32), qkv = to_qkv(RMSNorm(x)) as (B, 3*heads*dh, n);
  * mem_kv (2, heads, dh, nmem); out (B, heads*dh, n) before to_out.  ws: rdq_linear_attention_ws_bytes
- * (k-softmax statistics + per-256-token context partials, combined in a fixed order). */
+ * (k-softmax statistics + per-256-token context partials, combined in a fixed order, + the combined
+ * context).  dh = 32 forms each partial context on v_mfma_f32_32x32x2_f32. */
 size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem);
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
                          const float *mem_kv, float *out, void *ws, hipStream_t stream);

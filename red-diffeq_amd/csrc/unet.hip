@@ -31,6 +31,7 @@ namespace {
 #define RDQ_E_INVALID (-10001)
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 // ------------------------------------------------------------------------------------ conv2d
 // Implicit GEMM on the fp32 matrix cores: D[cout][pixel] = W[cout][k] x A[k][pixel], k = (ci, ky, kx).
@@ -235,35 +236,58 @@ __global__ __launch_bounds__(256) void k_gn_partial(const float *__restrict__ x,
     if (threadIdx.x == 0) { part[((size_t)bg * nchunk + c) * 2] = ss[0]; part[((size_t)bg * nchunk + c) * 2 + 1] = sq[0]; }
 }
 
-__global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, float eps, int nchunk,
-                                                  const float *__restrict__ x, const float *__restrict__ gamma,
-                                                  const float *__restrict__ beta, const float *__restrict__ ss,
-                                                  const double *__restrict__ part, float *__restrict__ y)
+// mean and 1/std of every (sample, group) from the fixed-order fp64 chunk partials, once
+__global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gsize, float eps,
+                                                  const double *__restrict__ part, float *__restrict__ stat)
 {
-    const int bg = blockIdx.y;                 // (sample, group)
-    const int b = bg / G, g = bg - b * G;
-    const int cpg = C / G;
-    const int64_t gsize = (int64_t)cpg * HW;
-    __shared__ float stat[2];
-    if (threadIdx.x == 0) {
-        double s = 0.0, q = 0.0;
-        for (int c = 0; c < nchunk; ++c) { s += part[((size_t)bg * nchunk + c) * 2]; q += part[((size_t)bg * nchunk + c) * 2 + 1]; }
-        const double mean = s / (double)gsize;
-        double var = q / (double)gsize - mean * mean;
-        var = var < 0.0 ? 0.0 : var;
-        stat[0] = (float)mean;
-        stat[1] = (float)(1.0 / sqrt(var + (double)eps));
-    }
-    __syncthreads();
-    const float mean = stat[0], rstd = stat[1];
-    const float *px = x + (size_t)bg * gsize;
-    float *py = y + (size_t)bg * gsize;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < gsize; e += (int64_t)gridDim.x * blockDim.x) {
-        const int c = g * cpg + (int)(e / HW);
-        float v = (px[e] - mean) * rstd;
-        v = v * gamma[c] + beta[c];
-        if (ss) { const float sc = ss[(size_t)b * 2 * C + c], sh = ss[(size_t)b * 2 * C + C + c]; v = v * (sc + 1.0f) + sh; }
-        py[e] = v / (1.0f + expf(-v));   // SiLU
+    const int bg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bg >= BG) return;
+    double s = 0.0, q = 0.0;
+    for (int c = 0; c < nchunk; ++c) { s += part[((size_t)bg * nchunk + c) * 2]; q += part[((size_t)bg * nchunk + c) * 2 + 1]; }
+    const double mean = s / (double)gsize;
+    double var = q / (double)gsize - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    stat[2 * bg] = (float)mean;
+    stat[2 * bg + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// y = SiLU(((x - mean) rstd gamma + beta) (scale + 1) + shift), one workgroup per (channel row,
+// 1024-element chunk): the channel's constants are wave-uniform, four elements per lane (float4
+// where the row allows it); the operation order is the per-element formula's
+__device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float ga, float be, bool sso, float sc1,
+                                          float sh)
+{
+    float v = (x - mean) * rstd;
+    v = v * ga + be;
+    if (sso) v = v * sc1 + sh;
+    return v / (1.0f + expf(-v));
+}
+__global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch, const float *__restrict__ x,
+                                                  const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                  const float *__restrict__ ss, const float *__restrict__ stat,
+                                                  float *__restrict__ y)
+{
+    const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
+    const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
+    const int c = g * cpg + cl;
+    const float mean = stat[2 * bg], rstd = stat[2 * bg + 1], ga = gamma[c], be = beta[c];
+    const bool sso = ss != nullptr;
+    const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
+    const float *px = x + ((size_t)b * C + c) * HW;
+    float *py = y + ((size_t)b * C + c) * HW;
+    if ((HW & 3) == 0) {
+        const int i = (ch * 256 + (int)threadIdx.x) * 4;
+        if (i < HW) {
+            float4 v = *reinterpret_cast<const float4 *>(px + i);
+            v.x = gn_silu1(v.x, mean, rstd, ga, be, sso, sc1, sh);
+            v.y = gn_silu1(v.y, mean, rstd, ga, be, sso, sc1, sh);
+            v.z = gn_silu1(v.z, mean, rstd, ga, be, sso, sc1, sh);
+            v.w = gn_silu1(v.w, mean, rstd, ga, be, sso, sc1, sh);
+            *reinterpret_cast<float4 *>(py + i) = v;
+        }
+    } else {
+        const int e1 = min(HW, (ch + 1) * 1024);
+        for (int i = ch * 1024 + (int)threadIdx.x; i < e1; i += 256) py[i] = gn_silu1(px[i], mean, rstd, ga, be, sso, sc1, sh);
     }
 }
 
@@ -398,7 +422,27 @@ __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nm
         V[d][jj] = vv;                                           // row d of V = value channel e = d
     }
     __syncthreads();
-    // 256 threads x 4 outputs: (d, e) = (tid >> 3, (tid & 7) * 4 + q)
+    float *o = part + (((size_t)ch * gridDim.z + b) * heads + h) * dh * dh;
+    if (dh == 32) {
+        // ctx[d][e] = sum_j P[d][j] V[e][j] is a 32 x 32 GEMM with K = the chunk's tokens: each wave
+        // takes 64 of them on v_mfma_f32_32x32x2_f32 (A[row l&31][k l>>5] = P, B[k l>>5][col l&31] = V),
+        // then the four partial tiles are summed through LDS in a fixed order
+        const int w = tid >> 6, l = tid & 63;
+        f32x16 acc = {};
+#pragma unroll 8
+        for (int i = 0; i < LA_CH / 8; ++i) {
+            const int jj = w * (LA_CH / 4) + 2 * i + (l >> 5);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(P[l & 31][jj], V[l & 31][jj], acc, 0, 0, 0);
+        }
+        __syncthreads();
+        float *R = &P[0][0];                                     // 4 x 1024 floats (P holds 32 x 257)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) R[w * 1024 + ((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 32 + (l & 31)] = acc[r];
+        __syncthreads();
+        for (int i = tid; i < 1024; i += 256) o[i] = ((R[i] + R[1024 + i]) + R[2048 + i]) + R[3072 + i];
+        return;
+    }
+    // dh < 32: 256 threads x 4 outputs: (d, e) = (tid >> 3, (tid & 7) * 4 + q)
     const int d = tid >> 3, e0 = (tid & 7) * 4;
     if (d >= dh) return;
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -407,33 +451,42 @@ __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nm
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] += p * V[e0 + q][jj];
     }
-    float *o = part + ((((size_t)ch * gridDim.z + b) * heads + h) * dh + d) * dh;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) if (e0 + q < dh) o[e0 + q] = acc[q];
+    for (int q = 0; q < 4; ++q) if (e0 + q < dh) o[(size_t)d * dh + e0 + q] = acc[q];
+}
+
+// ctx[b][h][d][e] = (sum of the chunk partials, in chunk order) / sum_d, once per (b, h)
+__global__ __launch_bounds__(256) void k_la_reduce(int BHDD, int dh, int nch, const float *__restrict__ stats,
+                                                   const float *__restrict__ part, float *__restrict__ ctx)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= BHDD) return;
+    float t = 0.0f;
+    int c = 0;
+    for (; c + 4 <= nch; c += 4) {                               // loads issued 4 at a time
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = part[(size_t)(c + u) * BHDD + i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t += v[u];
+    }
+    for (; c < nch; ++c) t += part[(size_t)c * BHDD + i];
+    ctx[i] = t / stats[(size_t)(i / dh) * 2 + 1];                // row (b, h, d)
 }
 
 // per (b, h, pixel): ctx = (sum of chunk partials in order) / sum_d; q softmax over d, scale,
 // out[e] = sum_d ctx[d][e] q[d]
-__global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, int nch, float scale,
-                                                const float *__restrict__ qkv, const float *__restrict__ stats,
-                                                const float *__restrict__ part, float *__restrict__ out)
+__global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float scale,
+                                                const float *__restrict__ qkv, const float *__restrict__ ctx,
+                                                float *__restrict__ out)
 {
-    const int h = blockIdx.y, b = blockIdx.z, B = gridDim.z;
+    const int h = blockIdx.y, b = blockIdx.z;
     const int C = heads * dh;
     __shared__ __attribute__((aligned(16))) float cs[32][32];
+    const float *cb = ctx + (size_t)(b * heads + h) * dh * dh;
     for (int i = threadIdx.x; i < dh * dh; i += blockDim.x) {
         const int d = i / dh;
-        float t = 0.0f;                       // chunks in order; loads issued 4 at a time
-        int c = 0;
-        for (; c + 4 <= nch; c += 4) {
-            float v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = part[(((size_t)(c + u) * B + b) * heads + h) * dh * dh + i];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) t += v[u];
-        }
-        for (; c < nch; ++c) t += part[(((size_t)c * B + b) * heads + h) * dh * dh + i];
-        cs[d][i - d * dh] = t / stats[((size_t)(b * heads + h) * dh + d) * 2 + 1];
+        cs[d][i - d * dh] = cb[i];
     }
     __syncthreads();
     const int pix = blockIdx.x * blockDim.x + threadIdx.x;
@@ -608,7 +661,6 @@ void launch_conv_ig(dim3 grid, hipStream_t st, const IgArgs &a)
 // mfma_f32_32x32x16_bf16 lane maps: A[row l&31][k 8(l>>5)+j], B[k 8(l>>5)+j][col l&31],
 // D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31] (cdna_hip_programming.md §3).
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
 constexpr int BF_BM = 128, BF_BK = 32, BF_LD = BF_BK + 8;   // LDS rows of 80 B
 
 struct BfArgs {
@@ -1184,7 +1236,7 @@ size_t rdq_group_norm_ws_bytes(int32_t B, int32_t C, int32_t HW, int32_t G)
     if (B < 1 || C < 1 || HW < 1 || G < 1) return 0;
     const int64_t gsize = (int64_t)(C / G) * HW;
     const int64_t nchunk = (gsize + GN_CHUNK - 1) / GN_CHUNK;
-    return (size_t)B * G * nchunk * 2 * sizeof(double);
+    return (size_t)B * G * nchunk * 2 * sizeof(double) + (size_t)B * G * 2 * sizeof(float);   // + stats
 }
 
 int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, const float *x, const float *gamma,
@@ -1194,9 +1246,11 @@ int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, 
     const int64_t gsize = (int64_t)(C / G) * HW;
     const int nchunk = (int)((gsize + GN_CHUNK - 1) / GN_CHUNK);
     double *part = (double *)ws;
+    float *stat = (float *)(part + (size_t)B * G * nchunk * 2);
     hipLaunchKernelGGL(k_gn_partial, dim3(nchunk, B * G), dim3(256), 0, st, x, gsize, nchunk, part);
-    const int nb = (int)std::min<int64_t>((gsize + 255) / 256, 64);
-    hipLaunchKernelGGL(k_gn_apply, dim3(nb, B * G), dim3(256), 0, st, C, HW, G, eps, nchunk, x, gamma, beta, ss, part, y);
+    hipLaunchKernelGGL(k_gn_stats, dim3((B * G + 255) / 256), dim3(256), 0, st, B * G, nchunk, gsize, eps, part, stat);
+    const int nch = (HW + 1023) / 1024;
+    hipLaunchKernelGGL(k_gn_apply, dim3((C / G) * nch, B * G), dim3(256), 0, st, C, HW, G, nch, x, gamma, beta, ss, stat, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -1234,7 +1288,7 @@ static int la_chunks(int n, int nmem) { return (n + nmem + LA_CH - 1) / LA_CH; }
 size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem)
 {
     if (B < 1 || heads < 1 || dh < 1 || n < 1 || nmem < 0) return 0;
-    return ((size_t)B * heads * dh * 2 + (size_t)la_chunks(n, nmem) * B * heads * dh * dh) * sizeof(float);
+    return ((size_t)B * heads * dh * 2 + (size_t)(la_chunks(n, nmem) + 1) * B * heads * dh * dh) * sizeof(float);
 }
 
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
@@ -1245,11 +1299,14 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
     float *stats = (float *)ws;
     float *part = stats + (size_t)B * heads * dh * 2;
     const int nch = la_chunks(n, nmem);
+    float *ctx = part + (size_t)nch * B * heads * dh * dh;
     hipLaunchKernelGGL(k_la_stats, dim3((B * heads * dh + 3) / 4), dim3(256), 0, st, B, heads, dh, n, nmem, qkv,
                        mem_kv, stats);
     hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, stats, part);
-    hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, nch, scale, qkv,
-                       stats, part, out);
+    const int bhdd = B * heads * dh * dh;
+    hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, stats, part, ctx);
+    hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx,
+                       out);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
