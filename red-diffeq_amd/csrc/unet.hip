@@ -327,6 +327,51 @@ __global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm(int C, int HW, const flo
     }
 }
 
+// the same with the thread's NPT = ceil(C / RMS_G) channels held in registers between the two passes
+// (one HBM read of x), loads issued together at clamped indices (no per-element branch), the
+// residual loaded before the first store; sums in the same channel order as above
+template <int NPT>
+__global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm_r(int C, int HW, const float *__restrict__ x,
+                                                          const float *__restrict__ g, const float *__restrict__ res,
+                                                          float *__restrict__ y)
+{
+    __shared__ float part[RMS_G][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int pix = blockIdx.x * 64 + lane, b = blockIdx.y;
+    const bool ok = pix < HW;
+    const size_t base = (size_t)b * C * HW + min(pix, HW - 1);
+    float v[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) v[i] = x[base + (size_t)min(grp + i * RMS_G, C - 1) * HW];
+    float ssum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+        if (grp + i * RMS_G < C) ssum += v[i] * v[i];
+    part[grp][lane] = ssum;
+    __syncthreads();
+    float tot = 0.0f;
+#pragma unroll
+    for (int i = 0; i < RMS_G; ++i) tot += part[i][lane];
+    float r[NPT] = {};
+    if (res) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) r[i] = res[base + (size_t)min(grp + i * RMS_G, C - 1) * HW];
+    }
+    if (!ok) return;
+    const float den = fmaxf(sqrtf(tot), 1e-12f);      // F.normalize: x / max(||x||, eps)
+    const float sc = sqrtf((float)C);
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+        const int c = grp + i * RMS_G;
+        if (c >= C) break;
+        float o = v[i] / den;
+        o = o * g[c];
+        o = o * sc;
+        if (res) o = o + r[i];
+        y[base + (size_t)c * HW] = o;
+    }
+}
+
 // ------------------------------------------------------------------------------------ linear
 __global__ __launch_bounds__(256) void k_linear(int in, int out, const float *__restrict__ x,
                                                 const float *__restrict__ w, const float *__restrict__ bias,
@@ -1259,7 +1304,12 @@ int rdq_rmsnorm(int32_t B, int32_t C, int32_t HW, const float *x, const float *g
                 hipStream_t st)
 {
     if (B < 1 || C < 1 || HW < 1 || !x || !g || !y) return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_rmsnorm, dim3((HW + 63) / 64, B), dim3(64 * RMS_G), 0, st, C, HW, x, g, res, y);
+    const dim3 grid((HW + 63) / 64, B), blk(64 * RMS_G);
+    if (C <= 4 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<4>, grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 8 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<8>, grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 16 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<16>, grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 32 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<32>, grid, blk, 0, st, C, HW, x, g, res, y);
+    else hipLaunchKernelGGL(k_rmsnorm, grid, blk, 0, st, C, HW, x, g, res, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
