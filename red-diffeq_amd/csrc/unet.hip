@@ -236,19 +236,25 @@ __global__ __launch_bounds__(256) void k_gn_partial(const float *__restrict__ x,
     if (threadIdx.x == 0) { part[((size_t)bg * nchunk + c) * 2] = ss[0]; part[((size_t)bg * nchunk + c) * 2 + 1] = sq[0]; }
 }
 
-// mean and 1/std of every (sample, group) from the fixed-order fp64 chunk partials, once
-__global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gsize, float eps,
-                                                  const double *__restrict__ part, float *__restrict__ stat)
+// mean and 1/std of (sample, group) bg from the fixed-order fp64 chunk partials
+__device__ __forceinline__ void gn_stat_of(int bg, int nchunk, int64_t gsize, float eps, const double *part,
+                                           float &mean_f, float &rstd_f)
 {
-    const int bg = blockIdx.x * blockDim.x + threadIdx.x;
-    if (bg >= BG) return;
     double s = 0.0, q = 0.0;
     for (int c = 0; c < nchunk; ++c) { s += part[((size_t)bg * nchunk + c) * 2]; q += part[((size_t)bg * nchunk + c) * 2 + 1]; }
     const double mean = s / (double)gsize;
     double var = q / (double)gsize - mean * mean;
     var = var < 0.0 ? 0.0 : var;
-    stat[2 * bg] = (float)mean;
-    stat[2 * bg + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    mean_f = (float)mean;
+    rstd_f = (float)(1.0 / sqrt(var + (double)eps));
+}
+// ... once per (sample, group), for large grids (the apply's workgroups then read two floats)
+__global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gsize, float eps,
+                                                  const double *__restrict__ part, float *__restrict__ stat)
+{
+    const int bg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bg >= BG) return;
+    gn_stat_of(bg, nchunk, gsize, eps, part, stat[2 * bg], stat[2 * bg + 1]);
 }
 
 // y = SiLU(((x - mean) rstd gamma + beta) (scale + 1) + shift), one workgroup per (channel row,
@@ -262,15 +268,29 @@ __device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float
     if (sso) v = v * sc1 + sh;
     return v / (1.0f + expf(-v));
 }
+// stat == nullptr (small grids, where one more launch costs more than the arithmetic): every
+// workgroup derives its group's statistics from the chunk partials itself
 __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
                                                   const float *__restrict__ ss, const float *__restrict__ stat,
+                                                  const double *__restrict__ part, int nchunk, float eps,
                                                   float *__restrict__ y)
 {
     const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
     const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
     const int c = g * cpg + cl;
-    const float mean = stat[2 * bg], rstd = stat[2 * bg + 1], ga = gamma[c], be = beta[c];
+    float mean, rstd;
+    if (stat) {
+        mean = stat[2 * bg];
+        rstd = stat[2 * bg + 1];
+    } else {
+        __shared__ float st2[2];
+        if (threadIdx.x == 0) gn_stat_of(bg, nchunk, (int64_t)cpg * HW, eps, part, st2[0], st2[1]);
+        __syncthreads();
+        mean = st2[0];
+        rstd = st2[1];
+    }
+    const float ga = gamma[c], be = beta[c];
     const bool sso = ss != nullptr;
     const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
     const float *px = x + ((size_t)b * C + c) * HW;
@@ -1293,9 +1313,13 @@ int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, 
     double *part = (double *)ws;
     float *stat = (float *)(part + (size_t)B * G * nchunk * 2);
     hipLaunchKernelGGL(k_gn_partial, dim3(nchunk, B * G), dim3(256), 0, st, x, gsize, nchunk, part);
-    hipLaunchKernelGGL(k_gn_stats, dim3((B * G + 255) / 256), dim3(256), 0, st, B * G, nchunk, gsize, eps, part, stat);
     const int nch = (HW + 1023) / 1024;
-    hipLaunchKernelGGL(k_gn_apply, dim3((C / G) * nch, B * G), dim3(256), 0, st, C, HW, G, nch, x, gamma, beta, ss, stat, y);
+    const int64_t blocks = (int64_t)(C / G) * nch * B * G;
+    const bool sep = blocks > 4096;                    // a separate statistics pass pays off
+    if (sep)
+        hipLaunchKernelGGL(k_gn_stats, dim3((B * G + 255) / 256), dim3(256), 0, st, B * G, nchunk, gsize, eps, part, stat);
+    hipLaunchKernelGGL(k_gn_apply, dim3((C / G) * nch, B * G), dim3(256), 0, st, C, HW, G, nch, x, gamma, beta, ss,
+                       sep ? stat : nullptr, part, nchunk, eps, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
