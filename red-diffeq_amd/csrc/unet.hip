@@ -219,11 +219,19 @@ __global__ __launch_bounds__(256) void k_gn_partial(const float *__restrict__ x,
     const int bg = blockIdx.y, c = blockIdx.x;
     const float *p = x + (size_t)bg * gsize;
     const int64_t e0 = (int64_t)c * GN_CHUNK, e1 = min((int64_t)(c + 1) * GN_CHUNK, gsize);
+    // the thread's GN_CHUNK / 256 elements are loaded together (clamped index, zero past the end),
+    // then accumulated in the same order as a strided loop would
+    float xv[GN_CHUNK / 256];
+#pragma unroll
+    for (int u = 0; u < GN_CHUNK / 256; ++u) xv[u] = p[min(e0 + threadIdx.x + 256 * u, e1 - 1)];
     double s = 0.0, q = 0.0;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        const double v = p[e];
-        s += v;
-        q += v * v;
+#pragma unroll
+    for (int u = 0; u < GN_CHUNK / 256; ++u) {
+        if (e0 + threadIdx.x + 256 * u < e1) {
+            const double v = xv[u];
+            s += v;
+            q += v * v;
+        }
     }
     __shared__ double ss[256], sq[256];
     ss[threadIdx.x] = s;
@@ -258,7 +266,7 @@ __global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gs
 }
 
 // y = SiLU(((x - mean) rstd gamma + beta) (scale + 1) + shift), one workgroup per (channel row,
-// 1024-element chunk): the channel's constants are wave-uniform, four elements per lane (float4
+// 1024-element chunk; the pass is VALU-bound on the exact expf and division of SiLU): the channel's constants are wave-uniform, four elements per lane (float4
 // where the row allows it); the operation order is the per-element formula's
 __device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float ga, float be, bool sso, float sc1,
                                           float sh)
@@ -1313,7 +1321,7 @@ int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, 
     double *part = (double *)ws;
     float *stat = (float *)(part + (size_t)B * G * nchunk * 2);
     hipLaunchKernelGGL(k_gn_partial, dim3(nchunk, B * G), dim3(256), 0, st, x, gsize, nchunk, part);
-    const int nch = (HW + 1023) / 1024;
+    const int nch = (HW + 1023) / 1024;               // 1024 elements of one channel row per workgroup
     const int64_t blocks = (int64_t)(C / G) * nch * B * G;
     const bool sep = blocks > 4096;                    // a separate statistics pass pays off
     if (sep)
