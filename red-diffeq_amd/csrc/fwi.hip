@@ -181,13 +181,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int 
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
 }
 constexpr int OOB = (int)0x80000000u;               // buffer offset beyond every range: store dropped
+// buffer cache policy "nt" (non-temporal, streaming): the history stream is written once and read
+// once, GBs apart; without the hint it churns the L2 that carries the persistent kernels' hand-offs
+// (their first sweep pass: 306 -> 220 us per forward launch, 299 -> 214 us per adjoint launch)
+constexpr int CP_NT = 2;
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff)
 {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, int voff, int soff)
-{
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
 }
 // --------------------------------------------------------------------------------------- K1/K2
 // Temporal blocking on a register-resident region (the MI355X design of the time loop).
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
             float *HS = a.hist + (size_t)(n + 2) * g.level + so + gx;
 #pragma unroll
             for (int r = 0; r < TB_R; ++r)
-                if (rin & (1u << r)) HS[rofs[r]] = prv[r];
+                if (rin & (1u << r)) __builtin_nontemporal_store(prv[r], &HS[rofs[r]]);   // streaming
         }
         if (rrow >= 0 && (rin & (1u << rrow)) && xin && (n % g.st) == 0) {   // pde.py:82-83
             float val = 0.0f;
@@ -511,8 +511,8 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     {
         const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, slice_bytes);
 #pragma unroll
-        for (int r = 0; r < TB_R; ++r) Pn[r] = bload(HR, pofs[r], 0);
-    }
+        for (int r = 0; r < TB_R; ++r) Pn[r] = bload(HR, pofs[r], 0);   // (not nt: vertically adjacent
+    }                                                                          //  tiles re-read halo rows from L2)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if (t >= a.nsteps) break;
@@ -637,6 +637,12 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 #endif
 #ifndef RDQ_EXP_NOPLOAD
 #define RDQ_EXP_NOPLOAD 0
+#endif
+#ifndef RDQ_HLOAD_CP
+#define RDQ_HLOAD_CP CP_NT    // history loads: non-temporal (read once; keeps the hand-off lines in L2)
+#endif
+#ifndef RDQ_HIST_CP
+#define RDQ_HIST_CP CP_NT     // history stores: non-temporal (re-read only by the adjoint, GBs later)
 #endif
 #ifndef RDQ_EXP_NOSTORE
 #define RDQ_EXP_NOSTORE 0
@@ -920,7 +926,8 @@ struct FwdPtArgs {
         if (!RDQ_EXP_NOSTORE && a.hist) {   /* own cells only; issued at once (the faster of the     \
                                                store placements measured: tools/exp_variants.sh) */ \
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
-            _Pragma("unroll") for (int r = 0; r < R; ++r) bstore(HR, PT_AT(PRV, r), hv[r], 0);            \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(PRV, r)), HR, hv[r], 0, RDQ_HIST_CP); \
         }                                                                                           \
         if (rrow >= 0 && (n % g.st) == 0) {                                                         \
             float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;                           \
@@ -1043,7 +1050,8 @@ struct AdjPtArgs {
 #define ADJ_PLOAD(PD, K)                                                                            \
     if (!RDQ_EXP_NOPLOAD) {                                                                         \
         const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(K) * L + so);                   \
-        _Pragma("unroll") for (int i = 0; i < PR; ++i) PD[i] = bload(HR, pv[i], 0);                \
+        _Pragma("unroll") for (int i = 0; i < PR; ++i)                                              \
+            PD[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(HR, pv[i], 0, RDQ_HLOAD_CP));  \
     }
 
 // one adjoint step k; CUR = L_{k+1}, PRV = L_{k+2} -> L_k, P = P_{k-1} rows -2..9
