@@ -1696,10 +1696,24 @@ int pt_shots_per_launch(const rdq_fwi_plan *p, int B, int T, int NW, int cap)
     return (p->g.ns + groups - 1) / groups;
 }
 
-// grid of a persistent launch covering `nsg` shots of B models
-unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg)
+// grid of a persistent launch covering `nsg` shots of B models.  A slice is XCD-local (L2 hand-offs,
+// pt_assign) only if one XCD received all its Tt workgroups; blocks are dealt round-robin over the
+// 8 XCDs, so a launch of S slices gets that for every slice only with >= 8 Tt ceil(S / 8) blocks.
+// Launches of fewer than 8 slices (e.g. the reference's 5-shot survey: 5 x 32 = 160 blocks, 20 per
+// XCD) are padded up to it when the chip holds that many; the surplus blocks find no slice and exit.
+unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
 {
-    return pt_tiles_padded(p, T, NW) * (unsigned)B * (unsigned)nsg;
+    const unsigned S = (unsigned)B * (unsigned)nsg;
+    unsigned grid = pt_tiles_padded(p, T, NW) * S;
+    if (p->xcd_mode) {
+        const int ih = NW * TB_R - 4 * T;
+        const unsigned Tt = (unsigned)(tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih));
+        const unsigned want = 8u * Tt * ((S + 7u) / 8u);
+        const int cap = NW == 12 ? capacity_nw<12>(const_cast<rdq_fwi_plan *>(p), adj, T)
+                                 : capacity_nw<8>(const_cast<rdq_fwi_plan *>(p), adj, T);
+        if (want > grid && (int)want <= cap) grid = want;
+    }
+    return grid;
 }
 
 // region height (waves) of the persistent kernel for this call, 0 = not resident -> chunked.
@@ -1765,7 +1779,7 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     for (int s0 = 0; s0 < p->g.ns; s0 += per) {
         a.g.s_off = s0;
         a.g.ns_grp = std::min(per, p->g.ns - s0);
-        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, false));
         RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
         else launch_fwd_pt<8>(T, grid, st, a);
@@ -1797,7 +1811,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     for (int s0 = 0; s0 < p->g.ns; s0 += per) {
         a.g.s_off = s0;
         a.g.ns_grp = std::min(per, p->g.ns - s0);
-        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp));
+        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, true));
         RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
         else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }

@@ -86,7 +86,10 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_persistent(self, enable):
-        _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, int(bool(enable))), "rdq_fwi_set_persistent")
+        """True / 1: persistent launches when they fit (64 x 96 regions first); 12 / 8: persistent with
+        that region height only; False / 0: chunked launches.  Results are identical in every mode."""
+        mode = int(enable) if not isinstance(enable, bool) else int(enable)
+        _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, mode), "rdq_fwi_set_persistent")
 
     def status(self, stream=None):
         """Synchronise and raise if a persistent launch's neighbour hand-off timed out."""

@@ -21,6 +21,7 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only", type=int, default=0, help="run a single blocking depth")
 ap.add_argument("--chunked", action="store_true", help="also time the chunked (launch per T steps) kernels")
 ap.add_argument("--profile", action="store_true", help="phase counters of the persistent kernels")
+ap.add_argument("--mode", type=int, default=1, help="persistent mode: 1 auto, 12 / 8 region height")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = dict(n_grid=70, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=a.ns)
@@ -31,7 +32,7 @@ sz = plan.sizes(a.B)
 dseis = torch.randn(a.B, a.ns, sz.nrec, plan.ng, device=dev)
 res = []
 # (T, persistent)
-cfgs = [(a.only, 1)] if a.only else [(2, 1), (3, 1), (4, 1)]
+cfgs = [(a.only, a.mode)] if a.only else [(2, a.mode), (3, a.mode), (4, a.mode)]
 if a.chunked:
     cfgs += [(T, 0) for T in (2, 3, 4)]
 for T, G in cfgs:
