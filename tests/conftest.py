@@ -30,6 +30,57 @@ def vnorm(v):
     return ((v - 1500) / 3000 * 2 - 1).astype(np.float32)
 
 
+class replay_draws:
+    """Replay the reference's recorded global-RNG draws (tests/golden/make_golden.py:record_draws)
+    in call order: inside the block every torch.randn / rand / randint / randperm call returns the
+    next recorded array on the requested device.  The kind and shape of each call are checked, so
+    a product path that draws in a different order, or draws more or fewer times, fails."""
+
+    FNS = ("randn", "rand", "randint", "randperm")
+
+    def __init__(self, z):
+        import torch
+        self.torch = torch
+        kinds = [str(k) for k in z["draw_kinds"]] if "draw_kinds" in z.files else []
+        self.queue = [(k, z[f"draw{i}"]) for i, k in enumerate(kinds)]
+        self.pos = 0
+
+    @staticmethod
+    def _shape(name, args, kw):
+        if name == "randperm":
+            return (int(args[0]),)
+        if name == "randint":
+            size = kw.get("size", args[-1] if args and isinstance(args[-1], (tuple, list)) else None)
+            return tuple(int(s) for s in size)
+        size = args[0] if len(args) == 1 and not isinstance(args[0], int) else args
+        return tuple(int(s) for s in (kw.get("size") or size))
+
+    def _fn(self, name):
+        def draw(*args, **kw):
+            assert self.pos < len(self.queue), f"unrecorded torch.{name} call #{self.pos}"
+            kind, val = self.queue[self.pos]
+            assert kind == name, f"draw #{self.pos}: product called torch.{name}, reference {kind}"
+            assert self._shape(name, args, kw) == val.shape, (name, self._shape(name, args, kw), val.shape)
+            self.pos += 1
+            t = self.torch.from_numpy(val.copy())
+            if kw.get("dtype") is not None:
+                t = t.to(kw["dtype"])
+            return t.to(kw["device"]) if kw.get("device") is not None else t
+        return draw
+
+    def __enter__(self):
+        self.orig = {n: getattr(self.torch, n) for n in self.FNS}
+        for n in self.FNS:
+            setattr(self.torch, n, self._fn(n))
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self.orig.items():
+            setattr(self.torch, n, f)
+        if exc[0] is None:
+            assert self.pos == len(self.queue), f"{len(self.queue) - self.pos} recorded draws not consumed"
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

@@ -166,22 +166,70 @@ class _NoDiffusion:
     device = torch.device("cpu")
 
 
-def run_loop(ctx, family, seed, reg, ts, lr, lam, sigma, missing=0, noise_std=0.0):
-    v_true = synthetic.make_model(family, ctx["n_grid"], ctx["n_grid"], seed=seed, batch=1)
+RNG_FNS = ("randn", "rand", "randint", "randperm")
+
+
+class record_draws:
+    """Record every draw the reference makes from torch's global RNG (torch.randn / rand / randint /
+    randperm with generator=None), in call order.  The GPU tests replay them
+    (tests/conftest.py:replay_draws): the device RNG stream differs from the CPU one, so injected
+    draws are the only way to pin an RNG-driven trajectory (eps_x0 at inversion.py:73, t at
+    regularization/diffusion.py:57, eps at :63, noise at utils/data_trans.py:55/59, missing
+    receivers at :146)."""
+
+    def __init__(self):
+        self.kinds, self.vals = [], []
+
+    def __enter__(self):
+        self.orig = {n: getattr(torch, n) for n in RNG_FNS}
+        for n in RNG_FNS:
+            def wrap(*a, _n=n, **kw):
+                assert kw.get("generator") is None, "only global-RNG draws are recorded"
+                r = self.orig[_n](*a, **kw)
+                self.kinds.append(_n)
+                self.vals.append(r.detach().cpu().numpy().copy())
+                return r
+            setattr(torch, n, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self.orig.items():
+            setattr(torch, n, f)
+
+    def arrays(self):
+        out = {"draw_kinds": np.array(self.kinds, dtype="U16")}
+        out.update({f"draw{i}": v for i, v in enumerate(self.vals)})
+        return out
+
+
+def run_loop(ctx, family, seed, reg, ts, lr, lam, sigma, missing=0, noise_std=0.0, noise_type="gaussian",
+             batch=1, nz=None, diffusion=None, sigma_x0=1e-4, use_time_weight=False, record=False):
+    nz = nz or ctx["n_grid"]
+    v_true = synthetic.make_model(family, nz, ctx["n_grid"], seed=seed, batch=batch)
     y = torch.from_numpy(run_forward(ctx, v_true))
-    init = ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=sigma)
+    init = torch.cat([ref.data_trans.prepare_initial_model(torch.from_numpy(v_true[i:i + 1]), "smoothed",
+                                                           sigma=sigma) for i in range(batch)])
     mu0 = torch.nn.functional.pad(init, (1, 1, 1, 1), "constant", 0)
-    eng = ref.inversion.InversionEngine(_NoDiffusion(), ref.ssim.SSIM(window_size=11), reg)
+    eng = ref.inversion.InversionEngine(diffusion if diffusion is not None else _NoDiffusion(),
+                                        ref.ssim.SSIM(window_size=11), reg, use_time_weight=use_time_weight,
+                                        sigma_x0=sigma_x0)
     torch.manual_seed(1234)
-    mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), y, make_fwi(ctx), ts=ts, lr=lr,
-                            reg_lambda=lam, missing_number=missing, noise_std=noise_std,
-                            regularization=reg)
-    h = hist[0]
-    return dict(v_true=v_true, y=y.numpy(), mu0=mu0.numpy(), mu=mu.detach().numpy(),
-                total_losses=np.array(h["total_losses"]), obs_losses=np.array(h["obs_losses"]),
-                reg_losses=np.array(h["reg_losses"]), ssim=np.array(h["ssim"]),
-                mae=np.array(h["mae"]), rmse=np.array(h["rmse"]),
-                params=np.array([ts, lr, lam, sigma, missing, noise_std]), **ctx_arrays(ctx))
+    rec = record_draws()
+    with rec:
+        mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), y, make_fwi(ctx), ts=ts, lr=lr,
+                                reg_lambda=lam, missing_number=missing, noise_std=noise_std,
+                                noise_type=noise_type, regularization=reg)
+    keys = ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")
+    if batch == 1:      # round-1 layout: 1-D histories of model 0
+        hs = {k: np.array(hist[0][k]) for k in keys}
+    else:               # (B, ts)
+        hs = {k: np.stack([np.array(h[k]) for h in hist]) for k in keys}
+    out = dict(v_true=v_true, y=y.numpy(), mu0=mu0.numpy(), mu=mu.detach().numpy(),
+               params=np.array([ts, lr, lam, sigma, missing, noise_std]), noise_type=np.array(noise_type),
+               sigma_x0=np.array(sigma_x0), use_time_weight=np.array(use_time_weight), **hs, **ctx_arrays(ctx))
+    if record:
+        out.update(rec.arrays())
+    return out
 
 
 def gen_loop():
@@ -196,6 +244,95 @@ def gen_loop():
          **run_loop(ctx, "curvevel", 77, "l2", ts=8, lr=0.03, lam=0.1, sigma=2.0))
     save("loop_none_small", reg=np.array("none"),
          **run_loop(ctx, "curvevel", 78, None, ts=8, lr=0.05, lam=0.0, sigma=2.0))
+
+
+def gen_loop_rng():
+    """InversionEngine trajectories whose RNG draws are recorded for replay: Gaussian noise +
+    missing receivers (TV) and Laplace noise + missing receivers (Tikhonov), B = 2 models (one
+    randperm per model, the same receivers for every shot: data_trans.py:110-153)."""
+    ctx = dict(SMALL, n_grid=16)
+    for name, fam, seed, reg, lam, missing, std, kind in (
+            ("loop_noise_small", "curvefault", 81, "tv", 0.05, 4, 0.05, "gaussian"),
+            ("loop_laplace_small", "curvevel", 82, "l2", 0.1, 3, 0.02, "laplace")):
+        out = run_loop(ctx, fam, seed, reg, ts=6, lr=0.03, lam=lam, sigma=2.0, missing=missing,
+                       noise_std=std, noise_type=kind, batch=2, record=True)
+        # the perturbed data and mask the engine built (its first draws after manual_seed(1234),
+        # inversion.py:63-64), for the CPU test of the two helpers alone
+        torch.manual_seed(1234)
+        yn = ref.data_trans.add_noise_to_seismic(torch.from_numpy(out["y"]), std, noise_type=kind)
+        yn, mask = ref.data_trans.missing_trace(yn, missing, return_mask=True)
+        save(name, reg=np.array(reg), y_noisy=yn.numpy(), mask=mask.numpy(), **out)
+
+
+def gen_loop_red():
+    """RED-DiffEq loop (InversionEngine.optimize(regularization='diffusion'), inversion.py:71-92 +
+    regularization/diffusion.py:50-83) with the dim-8 U-Net of gen_unet, its eps_x0 / t / eps draws
+    recorded: OpenFWI CurveVel grid (configs[2]'s family and loop: lambda 0.75, lr 0.03,
+    sigma_x0 1e-4), and the Marmousi 70x190 model (310x430 padded) whose regulariser runs the
+    patched path (3 width-wise windows, diffusion.py:85-155), configs/marmousi/red-diffeq.yaml."""
+    diff = ref.diffusion.GaussianDiffusion(_unet_dim8(), image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise").eval()
+    t0 = time.time()
+    ctx = dict(OPENFWI, ns=2)
+    save("loop_red_openfwi", reg=np.array("diffusion"),
+         **run_loop(ctx, "curvevel", 8890, "diffusion", ts=6, lr=0.03, lam=0.75, sigma=10.0,
+                    diffusion=diff, record=True))
+    print(f"  red openfwi loop {time.time() - t0:.1f}s")
+    t0 = time.time()
+    ctx = dict(OPENFWI, n_grid=190, ng=190, ns=2)
+    save("loop_red_marmousi", reg=np.array("diffusion"),
+         **run_loop(ctx, "curvefault", 8891, "diffusion", ts=3, lr=0.03, lam=0.75, sigma=20.0, nz=70,
+                    diffusion=diff, record=True))
+    print(f"  red marmousi loop {time.time() - t0:.1f}s")
+
+
+def gen_initial():
+    """prepare_initial_model (utils/data_trans.py:65-107), all three initial_type branches."""
+    out = {}
+    for i, (fam, nz, nx) in enumerate([("curvefault", 70, 70), ("flatvel", 70, 190)]):
+        v = synthetic.make_model(fam, nz, nx, seed=40 + i, batch=1)
+        out[f"v{i}"] = v
+        out[f"v{i}_smoothed"] = ref.data_trans.prepare_initial_model(torch.from_numpy(v), "smoothed",
+                                                                     sigma=10.0).numpy()
+        out[f"v{i}_homogeneous"] = ref.data_trans.prepare_initial_model(torch.from_numpy(v), "homogeneous").numpy()
+        out[f"v{i}_linear"] = ref.data_trans.prepare_initial_model(torch.from_numpy(v), "linear").numpy()
+    save("initial_models", **out)
+
+
+def gen_ckpt():
+    """dim-64 checkpoint round trip (the reference architecture, 296 state_dict keys): weights from
+    tests/golden/ckpt_weights.py, schedule buffers from a LINEAR beta schedule, loaded into the
+    reference's default (sigmoid) GaussianDiffusion the way scripts/run_inversion.py:63-67 does, so
+    the checkpoint's buffers override the computed ones.  Records eps-hat, pred_noise / pred_x_start
+    of model_predictions(clip_x_start=True, rederive_pred_noise=True) for 2 inputs."""
+    from ckpt_weights import synth_param
+    torch.manual_seed(0)
+    net = ref.diffusion.Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1, flash_attn=False)
+    diff = ref.diffusion.GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise")
+    lin = ref.diffusion.GaussianDiffusion(ref.diffusion.Unet(dim=8, dim_mults=(1, 2, 4, 8), channels=1),
+                                          image_size=72, timesteps=1000, sampling_timesteps=250,
+                                          objective="pred_noise", beta_schedule="linear")
+    sd = diff.state_dict()
+    new = {}
+    bufs = {}
+    for k, v in sd.items():
+        if k.startswith("model."):
+            new[k] = torch.from_numpy(synth_param(k, v.shape))
+        else:
+            new[k] = lin.state_dict()[k].clone()
+            bufs["buf." + k] = new[k].numpy()
+    diff.load_state_dict(new)
+    diff.eval()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(2, 1, 72, 72, generator=g).clamp(-3, 3)
+    t = torch.tensor([40, 650])
+    with torch.no_grad():
+        eps = diff.model(x, t, None)
+        pred = diff.model_predictions(x, t, x_self_cond=None, clip_x_start=True, rederive_pred_noise=True)
+    save("ckpt_dim64", x=x.numpy(), t=t.numpy(), eps=eps.numpy(), pred_noise=pred.pred_noise.numpy(),
+         pred_x_start=pred.pred_x_start.numpy(), keys=np.array(list(sd.keys())),
+         shapes=np.array([list(v.shape) + [0] * (4 - v.dim()) for v in sd.values()]), **bufs)
 
 
 def _unet_dim8(seed=0):
@@ -350,7 +487,7 @@ def gen_ilvr():
 
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
             loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi,
-            ilvr=gen_ilvr)
+            ilvr=gen_ilvr, loop_rng=gen_loop_rng, loop_red=gen_loop_red, initial=gen_initial, ckpt=gen_ckpt)
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

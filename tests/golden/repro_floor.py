@@ -1,0 +1,123 @@
+#!/usr/bin/env python
+"""Reproducibility floor of the reference's own inversion loop (runs the REFERENCE, in this
+container only; writes tests/golden/loop_tv_long.npz and tests/golden/repro_floor.json).
+
+The north_star bar is "velocity-model RMSE within 1e-4 of the reference".  The loop is sensitive
+to fp32 summation order: sign() in the L1 / TV gradients flips on ulp-level differences and Adam
+turns each flip into a +-lr step.  This script measures how far the REFERENCE drifts from itself
+on a TV trajectory of 30 iterations (OpenFWI FlatVel, ns = 2, nt = 1000):
+
+  a. reference engine + reference operator, torch intra-op threads = 8 (the fixture);
+  b. the same with 1 thread (a different reduction split in autograd / conv backward);
+  c. reference engine driven by the oracle operator (oracle/fwi_oracle.c: the kernels' op order).
+
+Per-iteration models are captured at the operator's input (x0_pred[:, :, 1:-1, 1:-1] == mu for TV).
+The GPU test (tests/test_gpu_fwi.py::test_tv_long_trajectory_floor) compares the HIP engine with
+run (a) per iteration against max(1e-4, the measured a-vs-b / a-vs-c drift).
+
+Run:  python tests/golden/repro_floor.py
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+import make_golden as G  # noqa: E402
+
+CTX = dict(G.OPENFWI, ns=2)
+TS = 30
+
+
+class _Capture:
+    """Wraps an operator; records each call's input (the iteration's model)."""
+
+    def __init__(self, op):
+        self.op, self.models = op, []
+
+    def to(self, device):
+        return self
+
+    def __call__(self, v):
+        self.models.append(v.detach().numpy().copy())
+        return self.op(v)
+
+
+class _OracleOp(torch.autograd.Function):
+    @staticmethod
+    def forward(c, v, f):
+        seis, cf = f.forward(v.detach().contiguous().numpy().astype(np.float32), keep_history=True)
+        c.f, c.cf = f, cf
+        return torch.from_numpy(seis)
+
+    @staticmethod
+    def backward(c, g):
+        gA, gK, gb = c.f.adjoint(c.cf, g.contiguous().numpy())
+        out = torch.from_numpy(c.f.finalize(c.cf, gA, gK, gb))
+        c.cf = None
+        return out, None
+
+
+class _OracleFWI:
+    def __init__(self, ctx):
+        from oracle import oracle as O
+        self.f = O.OracleFWI(ctx, 1)
+
+    def __call__(self, v):
+        return _OracleOp.apply(v, self.f)
+
+
+def run(op, threads):
+    torch.set_num_threads(threads)
+    v_true = G.synthetic.make_model("flatvel", 70, 70, seed=8888, batch=1)
+    torch.set_num_threads(8)
+    y = torch.from_numpy(G.run_forward(CTX, v_true))          # forward is bit-exact at any thread count
+    torch.set_num_threads(threads)
+    init = G.ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=10.0)
+    mu0 = torch.nn.functional.pad(init, (1, 1, 1, 1), "constant", 0)
+    eng = G.ref.inversion.InversionEngine(G._NoDiffusion(), G.ref.ssim.SSIM(window_size=11), "tv")
+    cap = _Capture(op)
+    torch.manual_seed(1234)
+    mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), y, cap, ts=TS, lr=0.03, reg_lambda=0.01,
+                            regularization="tv")
+    models = np.stack(cap.models[1:] + [mu.detach().numpy()])   # model after iteration k, k = 1..TS
+    return dict(v_true=v_true, y=y.numpy(), mu0=mu0.numpy(), models=models, hist=hist[0])
+
+
+def rmse(a, b):
+    return np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2, axis=tuple(range(1, a.ndim))))
+
+
+def main():
+    t0 = time.time()
+    a = run(G.make_fwi(CTX), 8)
+    print(f"a (reference, 8 threads) {time.time() - t0:.0f}s", flush=True)
+    t0 = time.time()
+    b = run(G.make_fwi(CTX), 1)
+    print(f"b (reference, 1 thread) {time.time() - t0:.0f}s", flush=True)
+    t0 = time.time()
+    c = run(_OracleFWI(CTX), 8)
+    print(f"c (reference engine + oracle operator) {time.time() - t0:.0f}s", flush=True)
+    ab, ac = rmse(a["models"], b["models"]), rmse(a["models"], c["models"])
+    rep = {"trajectory": "TV, OpenFWI FlatVel seed 8888, ns=2, nt=1000, lr=0.03, lambda=0.01, ts=30",
+           "rmse_ref8_vs_ref1_per_iter": ab.tolist(), "rmse_ref_vs_oracle_op_per_iter": ac.tolist(),
+           "max_ref8_vs_ref1": float(ab.max()), "max_ref_vs_oracle_op": float(ac.max()),
+           "final_ref8_vs_ref1": float(ab[-1]), "final_ref_vs_oracle_op": float(ac[-1])}
+    json.dump(rep, open(os.path.join(HERE, "repro_floor.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in rep.items() if not k.endswith("per_iter")}, indent=1))
+    h = a["hist"]
+    G.save("loop_tv_long", reg=np.array("tv"), v_true=a["v_true"], y=a["y"], mu0=a["mu0"],
+           models=a["models"], mu=a["models"][-1], floor_ref1=ab.astype(np.float64), floor_oracle=ac.astype(np.float64),
+           params=np.array([TS, 0.03, 0.01, 10.0, 0, 0.0]),
+           **{k: np.array(h[k]) for k in ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")},
+           **G.ctx_arrays(CTX))
+
+
+if __name__ == "__main__":
+    main()

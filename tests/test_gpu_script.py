@@ -118,3 +118,37 @@ def test_run_bench_script_tiny_dataset(cuda, tmp_path, method):
                             "mae", "rmse"}
     assert z["result"].shape == (70, 70) and z["rmse"].shape == (3,)
     assert np.isfinite(z["result"]).all() and np.abs(z["result"]).max() <= 1.0
+
+
+def test_checkpoint_round_trip_dim64(cuda, tmp_path):
+    """A dim-64 checkpoint in the reference's layout ({"model": GaussianDiffusion.state_dict(), ...},
+    models/diffusion.py:617-625) read by the drop-in loader (reference run_inversion.py:63-67):
+    all 296 keys load, the checkpoint's schedule buffers (a LINEAR beta schedule) override the
+    sigmoid ones the constructor computes, and eps-hat / model_predictions match the reference's
+    outputs for the same weights (tests/golden/ckpt_dim64.npz, tests/golden/ckpt_weights.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from ckpt_weights import synth_param
+    from conftest import load_golden
+    from red_diffeq import get_config
+    z = load_golden("ckpt_dim64")
+    sd = {}
+    for k, shp in zip(z["keys"], z["shapes"]):
+        k = str(k)
+        sd[k] = (torch.from_numpy(z["buf." + k]) if "buf." + k in z.files
+                 else torch.from_numpy(synth_param(k, [int(s) for s in shp if s])))
+    path = tmp_path / "model-x.pt"
+    torch.save({"step": 7, "model": sd, "version": "2.1.1"}, path)
+    cfg = get_config()
+    cfg.diffusion.model_path = str(path)
+    diff = _script().load_diffusion_model(cfg, cuda)
+    assert torch.equal(diff.alphas_cumprod.cpu(), torch.from_numpy(z["buf.alphas_cumprod"]))
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["t"]).to(cuda)
+    with torch.no_grad():
+        eps = diff.model(x, t, None)
+        pred = diff.model_predictions(x, t, x_self_cond=None, clip_x_start=True, rederive_pred_noise=True)
+    for got, key in ((eps, "eps"), (pred.pred_noise, "pred_noise"), (pred.pred_x_start, "pred_x_start")):
+        ref = torch.from_numpy(z[key]).to(cuda)
+        err = (got - ref).abs().max().item()
+        assert err <= 2e-4 * ref.abs().max().item(), (key, err)

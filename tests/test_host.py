@@ -47,6 +47,55 @@ def test_oracle_geometry_matches_product():
     np.testing.assert_array_equal(O.ricker(15.0, 1e-3, 1000), ricker(15.0, 1e-3, 1000))
 
 
+@pytest.mark.parametrize("name", ["loop_noise_small", "loop_laplace_small"])
+def test_noise_and_missing_traces_vs_reference(name):
+    """add_noise_to_seismic + missing_trace (utils/data_trans.py:33-62,110-153) with the reference's
+    draws replayed: same draw order (noise, then one randperm per model), same arithmetic
+    (Gaussian scale / Laplace inverse transform), the same receivers zeroed for every shot."""
+    from conftest import replay_draws
+    from red_diffeq.utils.data_trans import add_noise_to_seismic, missing_trace
+    z = load_golden(name)
+    std, missing = float(z["params"][5]), int(z["params"][4])
+    with replay_draws(z):
+        y = add_noise_to_seismic(torch.from_numpy(z["y"]), std, noise_type=str(z["noise_type"]))
+        y, mask = missing_trace(y, missing, return_mask=True)
+    assert np.array_equal(y.numpy(), z["y_noisy"])
+    assert np.array_equal(mask.numpy(), z["mask"])
+    m = z["mask"]
+    assert (m == m[:, :1]).all() and (m == m[:, :, :1]).all()     # per receiver, not per shot/time
+    assert ((m[:, 0, 0] == 0).sum(1) == missing).all()
+
+
+def test_prepare_initial_model_vs_reference():
+    from red_diffeq.utils.data_trans import prepare_initial_model
+    z = load_golden("initial_models")
+    for i in range(2):
+        v = torch.from_numpy(z[f"v{i}"])
+        assert np.array_equal(prepare_initial_model(v, "smoothed", sigma=10.0).numpy(), z[f"v{i}_smoothed"])
+        assert np.array_equal(prepare_initial_model(v, "homogeneous").numpy(), z[f"v{i}_homogeneous"])
+        assert np.array_equal(prepare_initial_model(v, "linear").numpy(), z[f"v{i}_linear"])
+    with pytest.raises(AssertionError):
+        prepare_initial_model(v, "constant")
+
+
+def test_checkpoint_fixture_keys_and_weights_regenerate():
+    """The dim-64 checkpoint fixture's 296 keys / shapes are this package's GaussianDiffusion
+    state_dict, and tests/golden/ckpt_weights.py regenerates every weight deterministically."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from ckpt_weights import synth_param
+    from red_diffeq.models.diffusion import GaussianDiffusion, Unet
+    z = load_golden("ckpt_dim64")
+    d = GaussianDiffusion(Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1), image_size=72, timesteps=1000,
+                          sampling_timesteps=250, objective="pred_noise")
+    sd = d.state_dict()
+    assert list(sd.keys()) == [str(k) for k in z["keys"]] and len(sd) == 296
+    for k, shp in zip(z["keys"], z["shapes"]):
+        assert tuple(sd[str(k)].shape) == tuple(int(s) for s in shp if s) or sd[str(k)].dim() == 0
+    a = synth_param("model.init_conv.weight", (64, 1, 7, 7))
+    assert np.array_equal(a, synth_param("model.init_conv.weight", (64, 1, 7, 7)))
+
+
 def test_configs_load_unchanged():
     from red_diffeq.config import get_config, load_config, save_config
     cfg_dir = os.path.join(ROOT, "tests", "golden", "configs")
