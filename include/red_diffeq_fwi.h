@@ -94,7 +94,9 @@ int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the
  * device, with 64 x 96 regions if they fit, else 64 x 64; 12 / 8 = only that region height;
- * 0 = always the chunked launches.  Identical results in every mode. */
+ * 0 = always the chunked launches.  Identical results in every mode.  -1 (fault-path tests only):
+ * persistent launches oversubscribed to twice the resident capacity, so they report "not resident"
+ * through the status word instead of computing. */
 int rdq_fwi_set_persistent(rdq_fwi_plan *plan, int32_t mode);
 /* Synchronises `stream` and reports (then clears) a persistent-kernel hand-off timeout:
  * 0, or RDQ_E_HANDOFF when some launch since the last call gave up waiting for a neighbour. */
@@ -103,6 +105,12 @@ int rdq_fwi_status(rdq_fwi_plan *plan, hipStream_t stream);
  * (1 = neighbour timeout, 2 = launch not resident), [16..23] workgroups per XCD of the last
  * persistent launch. */
 int rdq_fwi_debug_words(rdq_fwi_plan *plan, uint32_t out[32]);
+/* Caller-owned status words (device memory, >= 64 uint32, zeroed by the caller; NULL = the plan's
+ * own): word 0 is non-zero once a persistent launch gave up (1 = neighbour hand-off timeout,
+ * 2 = launch not resident) and stays so until the caller clears it.  Lets the caller read it
+ * stream-ordered without a host sync (e.g. as the Adam guard of rdq_adam_step, or copied
+ * asynchronously to pinned host memory).  Replaces the plan's internal words for later launches. */
+int rdq_fwi_set_status_buffer(rdq_fwi_plan *plan, uint32_t *words);
 /* Which kernels a forward / adjoint call for batch B runs: out = {forward persistent region
  * height in waves (0 = chunked), the same for the adjoint, forward steps per epoch/launch,
  * adjoint steps per epoch/launch}. */

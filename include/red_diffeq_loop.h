@@ -26,10 +26,12 @@ extern "C" {
  *   m = lerp(m, g, 1 - beta1);  v = v * beta2 + (1 - beta2) g g
  *   p = p + step_size * m / (sqrt(v) / bc2_sqrt + eps)
  * step_size = -lr / (1 - beta1^t) and bc2_sqrt = sqrt(1 - beta2^t) are computed by the caller in
- * double precision exactly as torch.optim.Adam does (torch/optim/adam.py, _multi_tensor_adam). */
+ * double precision exactly as torch.optim.Adam does (torch/optim/adam.py, _multi_tensor_adam).
+ * guard (nullable, device): when *guard != 0 the step leaves param / exp_avg / exp_avg_sq untouched
+ * (the FWI status word: a gradient from a failed persistent launch is never applied). */
 int rdq_adam_step(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq, float beta1,
                   float beta2, float eps, float step_size, float bc2_sqrt, int32_t clamp, float lo, float hi,
-                  hipStream_t stream);
+                  const uint32_t *guard, hipStream_t stream);
 
 /* MAE, RMSE, SSIM of pred (B,1,H,W) given by element strides (any view, e.g. mu[:, :, 1:-1, 1:-1])
  * against true_norm (contiguous B,1,H,W, already v_normalize'd), SSIM on (x + 1) / 2.

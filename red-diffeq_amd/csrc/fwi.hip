@@ -1527,11 +1527,13 @@ struct rdq_fwi_plan {
     int Hp, Wp, ld, nrec;
     int *d_isx = nullptr, *d_rcv_start = nullptr, *d_rcv_list = nullptr;
     float *d_wav = nullptr;     // fp32 wavelet [nt] (persistent kernels)
-    unsigned *d_status = nullptr;   // hand-off timeout word (rdq_fwi_status)
+    unsigned *d_status = nullptr;   // status words in use: d_status_own or a caller buffer (rdq_fwi_set_status_buffer)
+    unsigned *d_status_own = nullptr;
     unsigned long long *d_prof = nullptr;   // phase counters (rdq_fwi_set_profile): fwd, then adj
     std::vector<unsigned long long> prof_host;
     bool graphs = true;
-    int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves)
+    int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves),
+                                // -1: persistent launches oversubscribed 2x past residency (fault-path test)
     int xcd_mode = 1;           // persistent kernels: XCD-local slices with L2 hand-offs (pt_assign)
     int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
     int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
@@ -1713,6 +1715,11 @@ unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
                                  : capacity_nw<8>(const_cast<rdq_fwi_plan *>(p), adj, T);
         if (want > grid && (int)want <= cap) grid = want;
     }
+    if (p->persist == -1) {   // fault-path test: a grid the device cannot hold resident at once
+        const int cap = NW == 12 ? capacity_nw<12>(const_cast<rdq_fwi_plan *>(p), adj, T)
+                                 : capacity_nw<8>(const_cast<rdq_fwi_plan *>(p), adj, T);
+        grid = std::max(grid, 2u * (unsigned)std::max(cap, 1));
+    }
     return grid;
 }
 
@@ -1723,7 +1730,7 @@ int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
 {
     if (!p->persist) return 0;
     const int T = adj ? p->adj_T : p->fwd_T;
-    const int want = p->persist;   // 1 = auto, 8 / 12 = forced
+    const int want = p->persist == -1 ? 1 : p->persist;   // 1 = auto, 8 / 12 = forced
     if (want == 1 || want == 12) {
         const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw<12>(p, adj, T));
         if (k > 0) { if (per) *per = k; return 12; }
@@ -1980,6 +1987,7 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
     for (int v : p->isx) if (v < 0 || v >= p->Wp) { delete p; return RDQ_E_INVALID; }
     for (int v : p->igx) if (v < 0 || v >= p->Wp) { delete p; return RDQ_E_INVALID; }
     if (geom->isz < 0 || geom->isz >= p->Hp || geom->igz < 0 || geom->igz >= p->Hp) { delete p; return RDQ_E_INVALID; }
+    if (p->Wp > FIN_MAXW) { delete p; return RDQ_E_INVALID; }   // gradient finalize holds a padded row in LDS
     p->g.isx = p->isx.data();
     p->g.igx = p->igx.data();
     p->g.wavelet = p->wav.data();
@@ -1997,8 +2005,9 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
     if (e == hipSuccess) e = hipMemcpy(p->d_rcv_list, order.data(), sizeof(int) * geom->ng, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_wav, sizeof(float) * geom->nt);
     if (e == hipSuccess) e = hipMemcpy(p->d_wav, p->wavf.data(), sizeof(float) * geom->nt, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_status, 256);
-    if (e == hipSuccess) e = hipMemset(p->d_status, 0, 256);
+    if (e == hipSuccess) e = hipMalloc(&p->d_status_own, 256);
+    if (e == hipSuccess) e = hipMemset(p->d_status_own, 0, 256);
+    p->d_status = p->d_status_own;
     if (e != hipSuccess) { rdq_fwi_plan_destroy(p); return -(int)e; }
     *out = p;
     return 0;
@@ -2015,7 +2024,7 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
     if (p->d_rcv_start) (void)hipFree(p->d_rcv_start);
     if (p->d_rcv_list) (void)hipFree(p->d_rcv_list);
     if (p->d_wav) (void)hipFree(p->d_wav);
-    if (p->d_status) (void)hipFree(p->d_status);
+    if (p->d_status_own) (void)hipFree(p->d_status_own);
     if (p->d_prof) (void)hipFree(p->d_prof);
     delete p;
     return 0;
@@ -2060,7 +2069,7 @@ int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 
 int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 {
-    if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12)) return RDQ_E_INVALID;
+    if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12 && mode != -1)) return RDQ_E_INVALID;
     if (p->persist != mode) {
         drop_graphs(p);
         p->cache.clear();
@@ -2127,6 +2136,17 @@ int rdq_fwi_status(rdq_fwi_plan *p, hipStream_t st)
         RDQ_CHECK(hipStreamSynchronize(st));
         return RDQ_E_HANDOFF;
     }
+    return 0;
+}
+
+int rdq_fwi_set_status_buffer(rdq_fwi_plan *p, uint32_t *words)
+{
+    if (!p) return RDQ_E_INVALID;
+    if (p->d_status != (words ? words : p->d_status_own)) {
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->d_status = words ? words : p->d_status_own;
     return 0;
 }
 

@@ -24,8 +24,10 @@ constexpr int RDQ_E_INVALID = -10001;
 
 __global__ __launch_bounds__(256) void k_adam(int64_t n, float *__restrict__ p, const float *__restrict__ g,
                                               float *__restrict__ m, float *__restrict__ v, float beta1, float beta2,
-                                              float eps, float step_size, float bc2_sqrt, int clamp, float lo, float hi)
+                                              float eps, float step_size, float bc2_sqrt, int clamp, float lo, float hi,
+                                              const uint32_t *__restrict__ guard)
 {
+    if (guard && *guard != 0u) return;   // gradient of a failed persistent FWI launch: skip the step
     const float w = 1.0f - beta1, omb2 = 1.0f - beta2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float gi = g[i];
@@ -150,12 +152,12 @@ extern "C" {
 
 int rdq_adam_step(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq, float beta1,
                   float beta2, float eps, float step_size, float bc2_sqrt, int32_t clamp, float lo, float hi,
-                  hipStream_t stream)
+                  const uint32_t *guard, hipStream_t stream)
 {
     if (n < 1 || !param || !grad || !exp_avg || !exp_avg_sq) return RDQ_E_INVALID;
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
     hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, stream, n, param, grad, exp_avg, exp_avg_sq, beta1,
-                       beta2, eps, step_size, bc2_sqrt, clamp, lo, hi);
+                       beta2, eps, step_size, bc2_sqrt, clamp, lo, hi, guard);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

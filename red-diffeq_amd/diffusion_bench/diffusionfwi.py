@@ -160,12 +160,16 @@ class DiffusionFWI:
                             grad_max = torch.max(torch.abs(mu_opt.grad)).item()
                         if grad_clip is not None and grad_clip > 0 and grad_max is not None and grad_max > 0:
                             torch.nn.utils.clip_grad_norm_([mu_opt], grad_clip * grad_max)
-                    opt.step()
+                    # a gradient from a failed persistent FWI launch is never applied (device guard)
+                    opt.step(guard=getattr(fwi_forward, "status_word", lambda: None)())
                     if model_blur:
                         with torch.no_grad():
                             mu_opt.data = _blur3(mu_opt.data).clamp_(-1.0, 1.0).contiguous()
                             opt.param = mu_opt
                 current = mu_opt.detach()
+                check = getattr(fwi_forward, "check", None)
+                if callable(check):
+                    check()      # one sync per reverse step: raise before the next step builds on it
             else:
                 current = denoised.detach()
             with torch.no_grad():

@@ -51,6 +51,7 @@ SIGNATURES = {
     "rdq_fwi_set_persistent": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_status": (c_int32, [c_void_p, c_void_p]),
     "rdq_fwi_debug_words": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "rdq_fwi_set_status_buffer": (c_int32, [c_void_p, c_void_p]),
     "rdq_fwi_set_profile": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_profile_waves": (c_int32, [c_void_p, c_int32, ctypes.POINTER(ctypes.c_uint64), c_size_t]),
     "rdq_fwi_launch_info": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_int32)]),
@@ -97,7 +98,7 @@ SIGNATURES = {
                                    c_void_p, c_void_p]),
     # include/red_diffeq_loop.h
     "rdq_adam_step": (c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_float,
-                                c_float, c_int32, c_float, c_float, c_void_p]),
+                                c_float, c_int32, c_float, c_float, c_void_p, c_void_p]),
     "rdq_metrics_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "rdq_metrics": (c_int32, [c_int32, c_int32, c_int32, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p, c_void_p,
                               c_void_p]),

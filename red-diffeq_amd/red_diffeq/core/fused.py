@@ -50,7 +50,9 @@ class FusedAdamClamp:
         self.param.grad = None
 
     @torch.no_grad()
-    def step(self, lr=None):
+    def step(self, lr=None, guard=None):
+        """guard: optional device int32 word; when it is non-zero at execution time the step is a
+        no-op on the device (rdq_adam_step), e.g. the FWI status word of a failed persistent launch."""
         if lr is not None:
             self.lr = float(lr)
         g = self.param.grad
@@ -66,7 +68,7 @@ class FusedAdamClamp:
         _hip.check(_hip.lib().rdq_adam_step(p.numel(), _hip.ptr(p), _hip.ptr(g), _hip.ptr(self.exp_avg),
                                             _hip.ptr(self.exp_avg_sq), self.beta1, self.beta2, self.eps,
                                             step_size, bc2 ** 0.5, int(self.clamp is not None), float(lo),
-                                            float(hi), _hip.stream_of(p)), "rdq_adam_step")
+                                            float(hi), _hip.ptr(guard), _hip.stream_of(p)), "rdq_adam_step")
 
 
 def metrics(pred, true_norm):

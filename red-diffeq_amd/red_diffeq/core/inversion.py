@@ -7,10 +7,16 @@ x0[:, :, 1:-1, 1:-1]) -> L1 misfit -> regulariser -> backward (HIP adjoint) -> A
 
 Shot-parallel inversion: when ``fwi_forward.shots`` covers a subset of the sources
 and a torch.distributed process group is initialised, each rank models its shots only; the
-misfit is normalised by the global observation count; the data-term gradient is summed over
-ranks by ONE all-reduce inside backward (``_GradAllReduce``); the regulariser, Adam and the
-metrics run replicated (identical seeds -> identical draws on every rank).
+misfit is normalised by the global observation count (computed from the full, replicated mask:
+no communication); the data-term gradient is summed over ranks by ONE all-reduce inside backward
+(``_GradAllReduce``); the regulariser, Adam and the metrics run replicated (identical seeds ->
+identical draws on every rank).
+
+Persistent-kernel failure (a neighbour hand-off or residency timeout of the single-launch FWI
+kernels, reported through the plan's status word) is handled inside the loop, without a host sync
+per iteration: see ``_FaultMonitor``.
 """
+import warnings
 from typing import Optional
 
 import torch
@@ -26,22 +32,30 @@ from .losses import LossCalculator
 
 
 class _GradAllReduce(torch.autograd.Function):
-    """Identity forward; backward sums the incoming gradient over the process group."""
+    """Identity forward; backward sums the incoming gradient over the process group.  With a
+    fault monitor, the local FWI status word rides along as one extra element of the same
+    all-reduce, so every rank sees (and its Adam guard acts on) any rank's failed launch."""
 
     @staticmethod
-    def forward(ctx, x, group):
-        ctx.group = group
+    def forward(ctx, x, group, monitor):
+        ctx.group, ctx.monitor = group, monitor
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
-        g = g.contiguous()
-        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
-        return g, None
+        mon = ctx.monitor
+        if mon is None:
+            g = g.contiguous()
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
+            return g, None, None
+        buf = torch.cat([g.reshape(-1), mon.local_word().to(g.dtype)])
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=ctx.group)
+        mon.global_word.copy_(buf[-1:])          # != 0 iff some rank's launch failed
+        return buf[:-1].view_as(g), None, None
 
 
-def grad_all_reduce(x, group=None):
-    return _GradAllReduce.apply(x, group)
+def grad_all_reduce(x, group=None, monitor=None):
+    return _GradAllReduce.apply(x, group, monitor)
 
 
 def shot_slice(fwi_forward, ns_total):
@@ -50,6 +64,65 @@ def shot_slice(fwi_forward, ns_total):
     if shots is None or (shots[0] == 0 and shots[1] == ns_total):
         return None
     return shots
+
+
+class _FaultMonitor:
+    """Stream-ordered watch over the FWI operator's status word (include/red_diffeq_fwi.h,
+    rdq_fwi_set_status_buffer).
+
+    * Adam guard: every iteration's fused Adam step reads the word on the device and is a no-op
+      when it is set, so a gradient from a failed persistent launch never reaches mu or the Adam
+      moments (the word is sticky: every later iteration is skipped too).
+    * Detection: the word is copied asynchronously into pinned host memory after each step; at the
+      start of iteration it the host reads iteration it-2's copy (already complete: the GPU is at
+      most two iterations behind, so no extra stall), and everything at the end of the loop.
+    * Recovery: the engine rewinds its host state (Adam step count, LR schedule, RNG) to the first
+      failed iteration, switches the operator to its chunked kernels and replays from there.
+    Sharded runs guard on the all-reduced word (``_GradAllReduce``), identical on every rank."""
+
+    def __init__(self, fwi_forward, ts, device, sharded):
+        self.fwi = fwi_forward
+        self.sharded = sharded
+        self.host = torch.zeros(ts, dtype=torch.int32, pin_memory=True)
+        self.events = [None] * ts
+        self.global_word = torch.zeros(1, dtype=torch.int32, device=device)
+        self._zero = torch.zeros(1, dtype=torch.int32, device=device)
+        self.checked = 0
+        self.recovered = False
+
+    def local_word(self):
+        w = self.fwi.status_word()
+        return self._zero if w is None else w
+
+    def guard(self):
+        return self.global_word if self.sharded else self.local_word()
+
+    def record(self, it):
+        self.host[it:it + 1].copy_(self.guard(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[it] = ev
+
+    def first_fault(self, upto):
+        """First iteration <= upto whose guard copy is set (None if none); waits for those copies."""
+        for j in range(self.checked, upto + 1):
+            self.events[j].synchronize()
+            if int(self.host[j]) != 0:
+                return j
+            self.checked = j + 1
+        return None
+
+    def recover(self, k, ts):
+        if self.recovered:
+            raise RuntimeError(f"FWI kernels failed again at iteration {k} after the fallback to the chunked path")
+        warnings.warn(f"persistent FWI launch failed at iteration {k} (status word set); the gradient was "
+                      "not applied; replaying from that iteration on the chunked kernels", RuntimeWarning)
+        self.fwi.fallback_to_chunked()
+        self.global_word.zero_()
+        self.host[k:].zero_()
+        self.events[k:] = [None] * (ts - k)
+        self.checked = k
+        self.recovered = True
 
 
 class InversionEngine:
@@ -103,7 +176,7 @@ class InversionEngine:
         shots = shot_slice(fwi_forward, y.shape[1])
         sharded = shots is not None and dist.is_available() and dist.is_initialized()
         if shots is not None:
-            if sharded:   # global observation count, constant over the loop: one all-reduce
+            if sharded:   # global observation count from the full (replicated) mask: no communication
                 nobs = mask.reshape(B, -1).sum(1).clamp(min=1.0)
                 loss_calc.global_nobs = nobs
             y = y[:, shots[0]:shots[1]].contiguous()
@@ -113,46 +186,81 @@ class InversionEngine:
         elif missing_number == 0:
             mask = None
 
-        pbar = tqdm(range(ts), desc="Optimizing", unit="step", disable=not self.show_progress)
-        for it in pbar:
-            if regularization == "diffusion":
-                noise_x0 = torch.randn(mu.shape, device=mu.device, dtype=mu.dtype)
-                x0_pred = mu + self.regularization_method.sigma_x0 * noise_x0
-            else:
-                x0_pred = mu
-            v_in = x0_pred[:, :, 1:-1, 1:-1]
-            if sharded:
-                v_in = grad_all_reduce(v_in, process_group)
-            predicted = fwi_forward(v_in)
-            loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
-            reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
-            total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
+        monitor = None
+        if callable(getattr(fwi_forward, "status_word", None)) and mu.is_cuda:
+            check = getattr(fwi_forward, "check", None)
+            if callable(check):
+                check()          # a failure before the loop (e.g. while making y) is the caller's
+            monitor = _FaultMonitor(fwi_forward, ts, self.device, sharded)
+        diffusion = regularization == "diffusion"
+        snaps = [None] * ts
 
-            optimizer.zero_grad()
-            total_loss.sum().backward()
-            optimizer.step()                       # + clamp_(-1, 1), inversion.py:87-90
-            optimizer.lr = scheduler.step()
-
-            with torch.no_grad():
-                row = hist_dev[it]
-                row[3:6] = fused_metrics(mu[:, :, 1:-1, 1:-1], true_norm)[[2, 0, 1]]   # ssim, mae, rmse
-                obs_log = loss_obs.detach()
+        pbar = tqdm(total=ts, desc="Optimizing", unit="step", disable=not self.show_progress)
+        it = 0
+        while True:
+            while it < ts:
+                k = monitor.first_fault(it - 2) if monitor is not None else None
+                if k is not None:
+                    it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar)
+                    continue
+                if monitor is not None:   # host state at the start of the iteration (for a replay)
+                    snaps[it] = (optimizer.t, scheduler.lr, scheduler.last_epoch, optimizer.lr,
+                                 torch.cuda.get_rng_state(mu.device) if diffusion else None)
+                if diffusion:
+                    noise_x0 = torch.randn(mu.shape, device=mu.device, dtype=mu.dtype)
+                    x0_pred = mu + self.regularization_method.sigma_x0 * noise_x0
+                else:
+                    x0_pred = mu
+                v_in = x0_pred[:, :, 1:-1, 1:-1]
                 if sharded:
-                    obs_log = obs_log.clone()
-                    dist.all_reduce(obs_log, group=process_group)
-                row[0] = obs_log + reg_lambda * reg_loss.detach()
-                row[1] = obs_log
-                row[2] = reg_loss.detach()
-            if self.show_progress:
-                h = row.cpu().numpy()
-                post = {"MAE": float(h[4].mean()), "RMSE": float(h[5].mean()), "SSIM": float(h[3].mean())}
-                if time_tensor is not None:
-                    post["t"] = int(round(time_tensor.float().mean().item()))
-                pbar.set_postfix(post)
+                    v_in = grad_all_reduce(v_in, process_group, monitor)
+                predicted = fwi_forward(v_in)
+                loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
+                reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
+                total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
 
-        check = getattr(fwi_forward, "check", None)   # persistent-kernel hand-off status (one sync)
-        if callable(check):
-            check()
+                optimizer.zero_grad()
+                total_loss.sum().backward()
+                optimizer.step(guard=None if monitor is None else monitor.guard())   # + clamp_(-1, 1)
+                optimizer.lr = scheduler.step()
+                if monitor is not None:
+                    monitor.record(it)
+
+                with torch.no_grad():
+                    row = hist_dev[it]
+                    row[3:6] = fused_metrics(mu[:, :, 1:-1, 1:-1], true_norm)[[2, 0, 1]]   # ssim, mae, rmse
+                    obs_log = loss_obs.detach()
+                    if sharded:
+                        obs_log = obs_log.clone()
+                        dist.all_reduce(obs_log, group=process_group)
+                    row[0] = obs_log + reg_lambda * reg_loss.detach()
+                    row[1] = obs_log
+                    row[2] = reg_loss.detach()
+                if self.show_progress:
+                    h = row.cpu().numpy()
+                    post = {"MAE": float(h[4].mean()), "RMSE": float(h[5].mean()), "SSIM": float(h[3].mean())}
+                    if time_tensor is not None:
+                        post["t"] = int(round(time_tensor.float().mean().item()))
+                    pbar.set_postfix(post)
+                pbar.update(1)
+                it += 1
+            k = monitor.first_fault(ts - 1) if monitor is not None else None
+            if k is None:
+                break
+            it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar)
+        pbar.close()
+
         H = hist_dev.cpu().numpy()
         results = [{k: [H[t, j, i] for t in range(ts)] for j, k in enumerate(keys)} for i in range(B)]
         return mu[:, :, 1:-1, 1:-1], results
+
+    @staticmethod
+    def _rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar):
+        """Restore the host state of iteration k (mu and the Adam moments are untouched: every step
+        since the failure was skipped on the device) and switch to the chunked kernels."""
+        monitor.recover(k, ts)
+        optimizer.t, scheduler.lr, scheduler.last_epoch, optimizer.lr, rng = snaps[k]
+        if rng is not None:
+            torch.cuda.set_rng_state(rng, optimizer.param.device)
+        pbar.n = k
+        return k

@@ -67,6 +67,11 @@ class FwiPlan:
             _hip.check(self.lib.rdq_fwi_plan_create(ctypes.byref(g), ctypes.byref(h)), "rdq_fwi_plan_create")
         self.handle = h
         self._sizes = {}
+        # status words in torch memory (caller-owned, rdq_fwi_set_status_buffer): word 0 != 0 once a
+        # persistent launch gave up; read stream-ordered (Adam guard, async host copies)
+        self.status_t = torch.zeros(64, dtype=torch.int32, device=device)
+        _hip.check(self.lib.rdq_fwi_set_status_buffer(self.handle, _hip.ptr(self.status_t)),
+                   "rdq_fwi_set_status_buffer")
 
     def sizes(self, B):
         if B not in self._sizes:
@@ -87,7 +92,8 @@ class FwiPlan:
 
     def set_persistent(self, enable):
         """True / 1: persistent launches when they fit (64 x 96 regions first); 12 / 8: persistent with
-        that region height only; False / 0: chunked launches.  Results are identical in every mode."""
+        that region height only; False / 0: chunked launches.  Results are identical in every mode.
+        -1 (fault-path tests): persistent launches oversubscribed past residency, which fail."""
         mode = int(enable) if not isinstance(enable, bool) else int(enable)
         _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, mode), "rdq_fwi_set_persistent")
 
@@ -240,6 +246,7 @@ class FWIForward(nn.Module):
         # shot-parallel sharding: this operator models only shots[start:stop]
         self.shots = (0, len(ctx["sx"])) if shots is None else (int(shots[0]), int(shots[1]))
         self._plans = {}
+        self._last = None
 
     # --- reference helpers kept with their signatures -------------------------------------
     def ricker(self, f, dt, nt):
@@ -300,6 +307,7 @@ class FWIForward(nn.Module):
                 v = self.v_denorm_func(v)     # arbitrary user callable: autograd through torch
             vel_mode = 1
         plan = self._plan(v.shape[2], v.shape[3], v.device)
+        self._last = plan
         s = _FWIFunction.apply(v, plan, vel_mode)
         return self.s_norm_func(s) if self.normalize else s
 
@@ -308,6 +316,18 @@ class FWIForward(nn.Module):
         (synchronises the current stream)."""
         for plan in self._plans.values():
             plan.status()
+
+    def status_word(self):
+        """Device int32 view (1,) of the status word of the plan the last call used (None before the
+        first call): non-zero once a persistent launch gave up.  Stream-ordered, no sync."""
+        return None if self._last is None else self._last.status_t[:1]
+
+    def fallback_to_chunked(self):
+        """After a persistent-launch failure: every plan runs the chunked (non-resident) kernels from
+        now on, and the status words are cleared (stream-ordered)."""
+        for plan in self._plans.values():
+            plan.set_persistent(False)
+            plan.status_t.zero_()
 
     def coefficients(self, v):
         """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""

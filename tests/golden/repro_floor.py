@@ -12,10 +12,15 @@ on a TV trajectory of 30 iterations (OpenFWI FlatVel, ns = 2, nt = 1000):
   c. reference engine driven by the oracle operator (oracle/fwi_oracle.c: the kernels' op order).
 
 Per-iteration models are captured at the operator's input (x0_pred[:, :, 1:-1, 1:-1] == mu for TV).
-The GPU test (tests/test_gpu_fwi.py::test_tv_long_trajectory_floor) compares the HIP engine with
-run (a) per iteration against max(1e-4, the measured a-vs-b / a-vs-c drift).
+The GPU tests (tests/test_gpu_loop_parity.py::test_tv_long_trajectory_floor,
+tests/test_gpu_fwi.py::test_inversion_loop_vs_reference) hold the HIP engine's final model to
+max(1e-4, 2 x the measured a-vs-c drift): run b showed the reference bitwise reproducible across
+thread counts, so the only floor is the summation order of a different (correct) fp32 operator.
 
-Run:  python tests/golden/repro_floor.py
+It also records, for each round-1 loop fixture, the RMSE between the reference's final model and
+the reference engine driven by the oracle operator ("oracle_op_floor_per_fixture").
+
+Run:  python tests/golden/repro_floor.py [fixtures]
 """
 import json
 import os
@@ -90,11 +95,35 @@ def run(op, threads):
     return dict(v_true=v_true, y=y.numpy(), mu0=mu0.numpy(), models=models, hist=hist[0])
 
 
+def fixture_floor(name):
+    """RMSE between a round-1 loop fixture's final model (reference engine + reference operator) and
+    the reference engine driven by the oracle operator on the same inputs."""
+    z = np.load(os.path.join(HERE, name + ".npz"))
+    ctx = {k[4:]: (z[k].item() if z[k].ndim == 0 else z[k]) for k in z.files if k.startswith("ctx_")}
+    ts, lr, lam, sigma, missing, noise_std = z["params"]
+    reg = str(z["reg"])
+    reg = None if reg == "none" else reg
+    eng = G.ref.inversion.InversionEngine(G._NoDiffusion(), G.ref.ssim.SSIM(window_size=11), reg)
+    torch.manual_seed(1234)
+    mu, _ = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]), torch.from_numpy(z["y"]),
+                         _Capture(_OracleFWI(ctx)), ts=int(ts), lr=float(lr), reg_lambda=float(lam),
+                         regularization=reg)
+    return float(rmse(mu.detach().numpy(), z["mu"])[0])
+
+
 def rmse(a, b):
     return np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2, axis=tuple(range(1, a.ndim))))
 
 
 def main():
+    if sys.argv[1:] == ["fixtures"]:      # refresh only the per-fixture floors
+        p = os.path.join(HERE, "repro_floor.json")
+        rep = json.load(open(p))
+        rep["oracle_op_floor_per_fixture"] = {n: fixture_floor(n) for n in
+                                              ("loop_tv_openfwi", "loop_l2_small", "loop_none_small")}
+        json.dump(rep, open(p, "w"), indent=1)
+        print(rep["oracle_op_floor_per_fixture"])
+        return
     t0 = time.time()
     a = run(G.make_fwi(CTX), 8)
     print(f"a (reference, 8 threads) {time.time() - t0:.0f}s", flush=True)
@@ -109,6 +138,8 @@ def main():
            "rmse_ref8_vs_ref1_per_iter": ab.tolist(), "rmse_ref_vs_oracle_op_per_iter": ac.tolist(),
            "max_ref8_vs_ref1": float(ab.max()), "max_ref_vs_oracle_op": float(ac.max()),
            "final_ref8_vs_ref1": float(ab[-1]), "final_ref_vs_oracle_op": float(ac[-1])}
+    rep["oracle_op_floor_per_fixture"] = {n: fixture_floor(n) for n in
+                                          ("loop_tv_openfwi", "loop_l2_small", "loop_none_small")}
     json.dump(rep, open(os.path.join(HERE, "repro_floor.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in rep.items() if not k.endswith("per_iter")}, indent=1))
     h = a["hist"]

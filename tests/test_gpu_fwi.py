@@ -5,11 +5,14 @@ Bars: forward seismograms BIT-EXACT vs the reference; adjoint accumulator gA bit
 oracle; velocity gradient within fp32 tolerance of the reference autograd (rel-L2 < 5e-5) and
 of the oracle (rel-L2 < 1e-6); TV inversion trajectory: final-model RMSE difference < 1e-4
 (north_star tolerance)."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import ctx_of, load_golden, vnorm
+from conftest import GOLDEN, ctx_of, load_golden, vnorm
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -364,11 +367,16 @@ def test_inversion_loop_vs_reference(cuda, name):
     # north_star criterion: the velocity-model RMSE (vs truth, the reference's own metric) agrees
     # within 1e-4 at every iteration (measured: ~1e-7)
     assert np.abs(np.array(h["rmse"]) - z["rmse"]).max() < 1e-4
-    # model-space difference: dominated by a few cells where sign() in the TV / L1 gradient flips
-    # on fp32-level differences and Adam turns the flip into a +-lr step.  The oracle driven by the
-    # REFERENCE engine shows the same 1.2e-4 on loop_tv_openfwi ("Parity").
+    # model space: RMSE vs the reference's final model <= max(1e-4, 2 x the measured floor), the
+    # floor being the reference ENGINE driven by the oracle operator (a correct fp32 restatement
+    # with another summation order) vs the reference itself: sign() in the TV / L1 gradients flips
+    # on ulp-level differences and Adam turns a flip into a +-lr step (tests/golden/repro_floor.py;
+    # loop_tv_openfwi 1.24e-4, loop_l2_small 2.2e-5, loop_none_small 1.6e-6)
+    floor = json.load(open(os.path.join(GOLDEN, "repro_floor.json")))["oracle_op_floor_per_fixture"][name]
     d = np.abs(mu - z["mu"])
-    assert float(np.sqrt(np.mean(d ** 2))) < 3e-4, float(np.sqrt(np.mean(d ** 2)))
+    rm = float(np.sqrt(np.mean(d ** 2)))
+    print(f"{name}: velocity-model RMSE vs the reference {rm:.3e} (floor {floor:.3e})")
+    assert rm <= max(1e-4, 2.0 * floor), (rm, floor)
     assert float(np.median(d)) < 1e-5, float(np.median(d))
     for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
         np.testing.assert_allclose(np.array(h[k], np.float64), z[k].astype(np.float64), rtol=2e-4, atol=1e-6,

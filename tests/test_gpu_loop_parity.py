@@ -40,9 +40,11 @@ def dim8_diffusion(cuda):
                              objective="pred_noise").to(cuda).eval()
 
 
-def run_engine(cuda, z):
+def run_engine(cuda, z, fwi=None):
     from red_diffeq.core.inversion import InversionEngine
     from red_diffeq.utils.ssim import SSIM
+    if fwi is None:
+        fwi = make_fwi(ctx_of(z))
     ts, lr, lam, sigma, missing, noise_std = z["params"]
     reg = str(z["reg"])
     reg = None if reg == "none" else reg
@@ -55,7 +57,7 @@ def run_engine(cuda, z):
                           sigma_x0=float(z["sigma_x0"]), show_progress=False)
     with replay_draws(z):
         mu, hist = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
-                                torch.from_numpy(z["y"]).to(cuda), make_fwi(ctx_of(z)), ts=int(ts), lr=float(lr),
+                                torch.from_numpy(z["y"]).to(cuda), fwi, ts=int(ts), lr=float(lr),
                                 reg_lambda=float(lam), missing_number=int(missing), noise_std=float(noise_std),
                                 noise_type=str(z["noise_type"]), regularization=reg)
     return mu.detach().cpu().numpy(), hist
@@ -80,13 +82,16 @@ def test_loop_vs_reference_with_recorded_draws(cuda, name):
 
 def test_tv_long_trajectory_floor(cuda):
     """30 TV iterations: the HIP engine's model vs the reference's, per iteration, against the
-    reference's own drift between 1 and 8 threads and between its operator and the oracle's
-    (tests/golden/repro_floor.json).  The final model is held to max(1e-4, 2 x that floor)."""
+    reference's own drift between 1 and 8 threads (measured: 0, bitwise) and between its operator and
+    the oracle's (measured: 3.1e-4 after 30 iterations, 3.6e-4 peak; tests/golden/repro_floor.json).
+    The final model is held to max(1e-4, 2 x that floor): the floor is one sample of a
+    chaotic drift (another correct operator lands elsewhere in the same range)."""
     z = load_golden("loop_tv_long")
     mu, hist = run_engine(cuda, _with_defaults(z))
     rep = json.load(open(os.path.join(GOLDEN, "repro_floor.json")))
     floor = max(rep["final_ref8_vs_ref1"], rep["final_ref_vs_oracle_op"])
     d = float(model_rmse(mu, z["mu"])[0])
+    print(f"loop_tv_long: velocity-model RMSE vs the reference {d:.3e} (oracle-operator floor {floor:.3e})")
     assert d <= max(1e-4, 2.0 * floor), (d, floor)
     np.testing.assert_allclose(np.array(hist[0]["rmse"], np.float64), z["rmse"].astype(np.float64), atol=1e-4)
 
@@ -100,6 +105,31 @@ class _with_defaults(dict):
         self.setdefault("sigma_x0", np.array(1e-4))
         self.setdefault("noise_type", np.array("gaussian"))
         self.files = list(self.keys())
+
+
+def test_persistent_failure_caught_inside_the_loop(cuda):
+    """A persistent launch that cannot be resident (rdq_fwi_set_persistent(-1): grid oversubscribed
+    2x past capacity, so the arrival barrier gives up and sets the status word) must never feed
+    Adam: the fused step is guarded on the device, the engine sees the word within two iterations,
+    rewinds to the failed iteration and replays on the chunked kernels.  The result is bitwise the
+    run that used the chunked kernels from the start, and within the fixture's measured floor of
+    the reference (tests/golden/repro_floor.json)."""
+    z = _with_defaults(load_golden("loop_tv_openfwi"))
+    fa = make_fwi(ctx_of(z))
+    fa._plan(70, 70, cuda).set_persistent(False)
+    mu_a, h_a = run_engine(cuda, z, fa)
+    fb = make_fwi(ctx_of(z))
+    pb = fb._plan(70, 70, cuda)
+    pb.set_persistent(-1)
+    with pytest.warns(RuntimeWarning, match="persistent FWI launch failed at iteration 0"):
+        mu_b, h_b = run_engine(cuda, z, fb)
+    assert not pb.launch_info(1)["fwd_persistent"]      # fell back to the chunked kernels
+    assert np.array_equal(mu_a, mu_b)
+    for k in h_a[0]:
+        assert np.array_equal(np.array(h_a[0][k]), np.array(h_b[0][k])), k
+    floor = json.load(open(os.path.join(GOLDEN, "repro_floor.json")))["oracle_op_floor_per_fixture"]
+    assert float(model_rmse(mu_b, z["mu"])[0]) <= max(1e-4, 2.0 * floor["loop_tv_openfwi"])
+    fb.check()                                          # status word cleared by the recovery
 
 
 def test_metrics_vs_reference_calculator(cuda):
