@@ -11,10 +11,15 @@ value = shot-timesteps/s over the whole job = N * ns_per_gpu * nt * B / (step ti
 ranks).  Weak scaling: every rank owns 8 shots of an 8N-shot survey.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--ns 8] [--no-cpu-baseline]
+
+--gpus N > 1 outside a torch.distributed launcher starts the N ranks itself (torch.distributed.run,
+one process per GPU, RCCL) as child processes; this parent never touches the GPU.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,6 +33,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "shot-timesteps/sec (fwd+adj) + per-iter FWI wallclock, OpenFWI 70×70"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3     # MI355X fp32 matrix peak, v_mfma_f32_*_f32 (MI355X_MICROARCH.md)
+UNET_GFLOP_72 = 18.17          # conv GFLOP of one 72x72 dim-64 U-Net forward
 
 
 def parse():
@@ -136,14 +143,61 @@ def red_loop_wallclock(dev, a, ns=32, family="curvevel"):
     return round((t_all - t_w) / a.steps * 1e3, 3)
 
 
+def launch_ranks(a):
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run and exit with their
+    status.  Only this process's children touch the GPUs (no exec from a GPU-initialised process)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def unet_rate(dev, reps=20):
+    """The configs[2] loop's U-Net forward (dim 64, 72x72, B = 1, fp32 as the reference), as the loop
+    runs it (hipGraph replay): ms, conv TFLOP/s and the fraction of the fp32 MFMA peak."""
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(0)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(dev).eval()
+    x = torch.randn(1, 1, 72, 72, device=dev)
+    t = torch.tensor([500], device=dev)
+    with torch.no_grad():
+        for _ in range(3):
+            net(x, t)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            net(x, t)
+        e1.record()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tfs = UNET_GFLOP_72 / (ms * 1e-3) / 1e3
+    return {"workload": "U-Net eps-predictor, dim 64, 72x72, B=1, fp32 (configs[2] loop)", "ms": round(ms, 4),
+            "conv_tflops": round(tfs, 2), "peak_tflops": FP32_MFMA_PEAK_TFS, "mfma_frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RDQ_BENCH_BACKEND=gloo: rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks
+    # share devices round-robin; RCCL needs one GPU per rank).  The driver's runs use RCCL.
+    backend = os.environ.get("RDQ_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     from red_diffeq.core.fused import CosineLR, FusedAdamClamp
@@ -159,6 +213,10 @@ def main():
     ctx = dict(n_grid=70, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns_tot)
     fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none,
                      shots=(rank * nsl, (rank + 1) * nsl))
+    if backend != "nccl" and world > torch.cuda.device_count():
+        # ranks share a GPU in the rehearsal: whole-chip persistent grids of two processes cannot be
+        # co-resident (they would report "not resident"), so the rehearsal runs the chunked kernels
+        fwi._plan(70, 70, dev).set_persistent(False)
     vtrue = make_model("flatvel", 70, 70, seed=8888, batch=B)
     vt = torch.from_numpy(vtrue)
     with torch.no_grad():
@@ -224,6 +282,19 @@ def main():
         print("after phases:", plan.debug_words(), file=sys.stderr, flush=True)
     fwi.check()
     fw_ms, adj_ms = float(np.median(fw_ms)), float(np.median(adj_ms))
+    allreduce_us = None
+    if world > 1:   # the one exchange per iteration: all-reduce of the B x 70 x 70 model gradient
+        g = torch.randn(B, 1, 70, 70, device=dev)
+        ts_ = []
+        for _ in range(25):
+            dist.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dist.all_reduce(g)
+            e1.record()
+            torch.cuda.synchronize()
+            ts_.append(e0.elapsed_time(e1) * 1e3)
+        allreduce_us = round(float(np.median(ts_[5:])), 2)
     info = plan.launch_info(B)
     T = info["adj_T"]
     if info["adj_persistent"]:
@@ -262,12 +333,15 @@ def main():
         "phases_ms": {"coeffs+forward": round(fw_ms, 3), "adjoint": round(adj_ms, 3),
                       "fwd_GBps_alg": round(fwd_bytes * nt / (fw_ms * 1e-3) / 1e9, 1)},
         "fwd_adj_only_shot_ts_per_s": round(nsl * nt * B / ((fw_ms + adj_ms) * 1e-3), 1),
+        "per_rank": {"shots": nsl, "allreduce_us": allreduce_us,
+                     "serial_tail_ms": round(t_step * 1e3 - fw_ms - adj_ms, 4)},
     }
     if not a.no_loop:
         # per-iteration wallclock of the drop-in loop itself (InversionEngine.optimize with TV,
         # metrics and histories included), the metric's second half
         out["per_iter_fwi_wallclock_ms"] = loop_wallclock(fwi, mu0, vt, y, a, dev, world)
     if world == 1 and not a.no_red:
+        out["unet"] = unet_rate(dev)
         out["configs2_red_loop"] = {"workload": "configs[2]: OpenFWI CurveVel-A 70x70, 32 shots, full RED-DiffEq "
                                                 "loop (fwd+adj + U-Net regulariser + Adam + metrics), random-init U-Net",
                                     "ms_per_iter": red_loop_wallclock(dev, a),

@@ -294,3 +294,26 @@ def test_ilvr_resampler_vs_reference_fixture():
         np.testing.assert_allclose(d.numpy(), z[f"rz_down{n}"], rtol=0, atol=1e-6)
         u = resize(torch.from_numpy(z[f"rz_down{n}"]), float(n), in_hw=(int(70 / n), int(70 / n)))
         np.testing.assert_allclose(u.numpy(), z[f"rz_up{n}"], rtol=0, atol=1e-6)
+
+
+def test_bench_launches_n_ranks_itself(monkeypatch):
+    """bench.py --gpus N outside a launcher starts N ranks via torch.distributed.run (child
+    processes; the parent never initialises the GPU) and exits with their status."""
+    import importlib.util
+    import subprocess
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    seen = {}
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.update(cmd=cmd, env=env) or 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
