@@ -203,10 +203,18 @@ void oracle_adjoint(const oracle_geom *g, const float *alpha, const float *temp1
                         float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;
                         float l = temp1[ci] * L1[off + i]; const float l2 = temp2[ci] * L2[off + i];
                         l = l - l2; l = l + nb;
-                        if (rec && z == g->igz)
+                        if (rec && z == g->igz) {   /* R^T dseis: the column's receivers summed first
+                                                       (index backward = index_put(accumulate) into zeros) */
+                            int any = 0;
+                            float dsum = 0.0f;
                             for (int r = 0; r < g->ng; ++r)
-                                if (g->igx[r] == x)
-                                    l = l + dseis[(((size_t)b * ns + s) * nrec + kr) * g->ng + r];
+                                if (g->igx[r] == x) {
+                                    const float d = dseis[(((size_t)b * ns + s) * nrec + kr) * g->ng + r];
+                                    dsum = any ? dsum + d : d;
+                                    any = 1;
+                                }
+                            if (any) l = l + dsum;
+                        }
                         L0[off + i] = l;
                         float s1 = AT(pp, zm1, x) + AT(pp, zp1, x); s1 = s1 + AT(pp, z, xm1); s1 = s1 + AT(pp, z, xp1);
                         float s2 = AT(pp, zm2, x) + AT(pp, zp2, x); s2 = s2 + AT(pp, z, xm2); s2 = s2 + AT(pp, z, xp2);

@@ -223,6 +223,8 @@ struct TBGeo {
     int tiles_x, ntiles;                 // tile grid of this launch's blocking depth
     size_t cstride, slice, level;        // level = B*ns*slice (one time level of all slices)
     const int *isx, *rcv_start, *rcv_list;
+    const int *rlane;                    // [Wp] adjoint residual index of a column (-1: no receiver)
+    int dstride;                         // residual row stride: ng, or ncolr after the fold
 };
 
 struct FwdTBArgs {
@@ -312,6 +314,14 @@ __device__ __forceinline__ TileId decode_tile(int L, int tiles_x, int ntiles, in
     t.ty = t.tile / tiles_x;
     t.tx = t.tile - t.ty * tiles_x;
     return t;
+}
+
+// record index of time step n under sample_temporal st (-1: not a recorded step); st == 1, the
+// reference default, needs no integer division
+__device__ __forceinline__ int rec_index(int n, int st)
+{
+    if (st == 1) return n;
+    return (n % st) == 0 ? n / st : -1;
 }
 
 // cheap wrap for |v| < a few n (general v handled by the loops)
@@ -490,10 +500,9 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         gal[r] = ((rin & (1u << r)) && xin) ? a.gA[so + o] : 0.0f;
     }
     const bool scol = gx == isx;
-    const int rs = rmask ? g.rcv_start[gx] : 0, re = rmask ? g.rcv_start[gx + 1] : 0;
-    const int rcv0 = rs < re ? g.rcv_list[rs] : -1;      // this lane's (usually only) receiver
-    const bool rmulti = __any(re - rs > 1);
-    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.ng;
+    // residual of this lane's column: one receiver's dseis, or several receivers' folded sum
+    const int rcv0 = rmask ? g.rlane[gx] : -1;
+    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
     // gbeta of this shot accumulates in a register over the launch's steps (same order as a
     // per-step read-modify-write of a.gbeta[bs]), stored once at the end
     const bool gbl = (smask & rin) && scol && xin;       // the source cell is this lane's own cell
@@ -529,7 +538,7 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
         }
         // this step's receiver residual, loaded before the stencil so its latency hides under it
         const bool rstep = rmask && ((k - 1) % g.st) == 0;   // wave-uniform
-        const float dsv = (rstep && rcv0 >= 0) ? DSb[(size_t)((k - 1) / g.st) * g.ng + rcv0] : -0.0f;
+        const float dsv = (rstep && rcv0 >= 0) ? DSb[(size_t)((k - 1) / g.st) * g.dstride + rcv0] : -0.0f;
         float q[TB_R];
 #pragma unroll
         for (int r = 0; r < TB_R; ++r) q[r] = A[r] * cur[r];
@@ -556,13 +565,6 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 #pragma unroll
             for (int r = 0; r < TB_R; ++r)
                 if (rmask & (1u << r)) prv[r] = prv[r] + dsv;     // -0 on lanes without a receiver
-            if (rmulti) {
-                const float *DS = DSb + (size_t)((k - 1) / g.st) * g.ng;
-#pragma unroll
-                for (int r = 0; r < TB_R; ++r)
-                    if (rmask & (1u << r))
-                        for (int j = rs + 1; j < re; ++j) prv[r] = prv[r] + DS[g.rcv_list[j]];
-            }
         }
         // gradient accumulators on the interior (P halo rows came with the same exchange)
 #pragma unroll
@@ -796,7 +798,11 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
     }                                                                                               \
     const size_t so = (size_t)bs * g.slice;                                                         \
     const int vo16 = gx * 16;                                                                       \
-    const bool hx = !xin && cx, xb = xin && bx;
+    const bool hx = !xin && cx, xb = xin && bx;                                                     \
+    /* hand-off lane offsets (OOB: no access) */                                                    \
+    const int vo_hx = hx ? vo16 : OOB, vo_cx = cx ? vo16 : OOB;                                     \
+    const int vo_xin = xin ? vo16 : OOB, vo_xb = xb ? vo16 : OOB;                                   \
+    const bool keep_in = xin || cx;
 #define PT_ROFS(r) (wrap_row(uz0 + (r), g.Hp) * g.ld)
 
 // Reload the halo cells of two levels V0/V1 from the granule slot GR (16-byte two-level granules),
@@ -808,33 +814,36 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
 #define PT_SWEEP(GR, TAG, V0, V1, SG)                                                               \
     {                                                                                               \
         unsigned long long t0_ = 0;                                                                 \
-        const unsigned long long ts_ = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;               \
+        const unsigned long long ts_ = prof ? __builtin_amdgcn_s_memrealtime() : 0;                 \
         for (unsigned pass_ = 0; live; ++pass_) {                                                   \
             /* the loads of a group of SG rows are all issued before any is checked: lanes        \
                without a halo cell in a row load from an out-of-range offset (no memory access,   \
                returns 0) instead of branching, which would make the compiler wait vmcnt(0) after \
-               each load (one serial L2 round trip per row).  SG < R bounds the registers held.  */ \
+               each load (one serial L2 round trip per row).  SG < R bounds the registers held.   \
+               The row classes are laundered per pass so no per-row lane mask stays live (SGPR    \
+               pressure) across the time loop.                                                    */ \
+            unsigned rin_ = rin, rcy_ = rcy;                                                        \
+            LAUNDER(rin_); LAUNDER(rcy_);                                                           \
             bool ok_ = true;                                                                        \
             _Pragma("unroll") for (int g_ = 0; g_ < R; g_ += (SG)) {                                \
                 u32x4 x_[(SG)];                                                                     \
+                int o_[(SG)];                                                                       \
                 _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
                     const int r = g_ + i_;                                                          \
-                    const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                  \
-                    if (!rowin_ && !rowcy_) continue;             /* wave-uniform */               \
-                    x_[i_] = gran_get(GR, (rowin_ ? hx : cx) ? vo16 : OOB, PT_ROFS(r) * 16);        \
+                    const bool rowin_ = (rin_ >> r) & 1u, rowcy_ = (rcy_ >> r) & 1u;                \
+                    o_[i_] = rowin_ ? vo_hx : (rowcy_ ? vo_cx : OOB);                               \
+                    x_[i_] = gran_get(GR, o_[i_], PT_ROFS(r) * 16);                                 \
                 }                                                                                   \
                 _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
                     const int r = g_ + i_;                                                          \
-                    const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                  \
-                    if (!rowin_ && !rowcy_) continue;                                               \
-                    const bool nd_ = rowin_ ? hx : cx;                                              \
+                    const bool nd_ = o_[i_] != OOB;                                                 \
                     ok_ = ok_ && (!nd_ || (x_[i_].y == (TAG) && x_[i_].w == (TAG)));                \
                     PT_AT(V0, r) = nd_ ? __uint_as_float(x_[i_].x) : PT_AT(V0, r);                  \
                     PT_AT(V1, r) = nd_ ? __uint_as_float(x_[i_].z) : PT_AT(V1, r);                  \
                 }                                                                                   \
             }                                                                                       \
-            const bool done_ = RDQ_EXP_SWEEP_ONCE || __all(ok_);                                     \
-            if (a.prof && pass_ == 0) tfp += __builtin_amdgcn_s_memrealtime() - ts_;                 \
+            const bool done_ = __all(ok_);                                                          \
+            if (prof && pass_ == 0) tfp += __builtin_amdgcn_s_memrealtime() - ts_;                   \
             if (done_) { npass += pass_ + 1; break; }                                               \
             if (pass_ == 0) t0_ = __builtin_amdgcn_s_memrealtime();                                 \
             if ((pass_ & 15) == 15) {                                                               \
@@ -851,24 +860,40 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
             }                                                                                       \
             __builtin_amdgcn_s_sleep(1);                                                            \
         }                                                                                           \
+        /* cells outside the next epoch's dependence cone: zeroed (bounded garbage) */             \
+        unsigned rin_ = rin, rcy_ = rcy;                                                            \
+        LAUNDER(rin_); LAUNDER(rcy_);                                                               \
         _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
-            const bool rowin_ = (rin >> r) & 1u, rowcy_ = (rcy >> r) & 1u;                          \
-            if (rowin_ ? (!xin && !cx) : (!rowcy_ || !cx)) { PT_AT(V0, r) = 0.0f; PT_AT(V1, r) = 0.0f; } \
+            const bool rowin_ = (rin_ >> r) & 1u, rowcy_ = (rcy_ >> r) & 1u;                        \
+            const bool keep_ = rowin_ ? keep_in : (rowcy_ && cx);                                   \
+            PT_AT(V0, r) = keep_ ? PT_AT(V0, r) : 0.0f;                                             \
+            PT_AT(V1, r) = keep_ ? PT_AT(V1, r) : 0.0f;                                             \
         }                                                                                           \
     }
 
-// publish the own-interior border cells of two levels
+// publish the own-interior border cells of two levels (rows: interior; lanes: the interior
+// columns of border rows, else the border columns)
 #define PT_PUBLISH(GR, TAG, V0, V1)                                                                 \
-    _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                 \
-        if (!((rin >> r) & 1u)) continue;                                                           \
-        if (((rby >> r) & 1u) ? xin : xb) {                                                         \
-            if (gl2) gran_put_l2(GR, vo16, PT_ROFS(r) * 16, (TAG), PT_AT(V0, r), PT_AT(V1, r));     \
-            else gran_put(GR, vo16, PT_ROFS(r) * 16, (TAG), PT_AT(V0, r), PT_AT(V1, r));            \
+    {                                                                                               \
+        unsigned rin_ = rin, rby_ = rby;                                                            \
+        LAUNDER(rin_); LAUNDER(rby_);                                                               \
+        if (gl2) {                                                                                  \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
+                if (!((rin_ >> r) & 1u)) continue;                                                  \
+                gran_put_l2(GR, ((rby_ >> r) & 1u) ? vo_xin : vo_xb, PT_ROFS(r) * 16, (TAG),        \
+                            PT_AT(V0, r), PT_AT(V1, r));                                            \
+            }                                                                                       \
+        } else {                                                                                    \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
+                if (!((rin_ >> r) & 1u)) continue;                                                  \
+                gran_put(GR, ((rby_ >> r) & 1u) ? vo_xin : vo_xb, PT_ROFS(r) * 16, (TAG),           \
+                         PT_AT(V0, r), PT_AT(V1, r));                                               \
+            }                                                                                       \
         }                                                                                           \
     }
 
 #define PT_PROF(ACC)                                                                                \
-    if (a.prof) { const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); ACC += now_ - tm; tm = now_; }
+    if (prof) { const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); ACC += now_ - tm; tm = now_; }
 
 // Re-materialise a wave-uniform value inside the time loop: stops the compiler from hoisting the
 // per-row compares on it out of the loop as live 64-bit lane masks (which spill to VGPR lanes and
@@ -929,8 +954,8 @@ struct FwdPtArgs {
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(PRV, r)), HR, hv[r], 0, RDQ_HIST_CP); \
         }                                                                                           \
-        if (rrow >= 0 && (n % g.st) == 0) {                                                         \
-            float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;                           \
+        if (rrow >= 0 && rec_index(n, g.st) >= 0) {                                                 \
+            float *SK = a.seis + ((size_t)bs * g.nrec + rec_index(n, g.st)) * g.ng;                 \
             int rr_ = rrow;                                                                         \
             LAUNDER(rr_);                                                                           \
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
@@ -944,9 +969,10 @@ struct FwdPtArgs {
     }
 
 #define PT_AT(V, r) V[(r) & 3][(r) >> 2]       // row r of a row-pair array
-template <int T, int NW>
+template <int T, int NW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 {
+    unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     __shared__ float xch[2][NW][4][64];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW)
@@ -982,7 +1008,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     for (int r = 0; r < R; ++r) hv[r] = (((rin >> r) & 1u) && xin) ? (PT_ROFS(r) + gx) * 4 : OOB;
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
-    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
     // The next epoch's wavelet samples are loaded right after the hand-off sweep (FWD_ISSUE), not
     // before it, so the granule loads do not queue behind them.
@@ -1017,18 +1043,18 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
 #undef FWD_ISSUE
     PT_PROF(tsw)
-    if (a.prof && lane == 0) {
-        atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
-        atomicAdd(a.prof + 4, tfp); atomicAdd(a.prof + 5, npass);
+    if (prof && lane == 0) {
+        atomicAdd(prof + 0, tsw); atomicAdd(prof + 1, tst); atomicAdd(prof + 2, tpb); atomicAdd(prof + 3, 1ull);
+        atomicAdd(prof + 4, tfp); atomicAdd(prof + 5, npass);
         if (blockIdx.x < PROF_WAVES / 16) {
-            unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
+            unsigned long long *raw = prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
             raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
         }
     }
 }
 #undef FWD_STEP
-#undef PT_AT
-#define PT_AT(V, r) V[r]                         // adjoint: plain per-row arrays
+// The adjoint keeps the forward's row-pair packing (PT_AT(V, r) = V[r & 3][r >> 2]): every add /
+// mul / fma of the step and of the gradient is one v_pk_*_f32 for two rows.
 
 struct AdjPtArgs {
     TBGeo g;
@@ -1046,148 +1072,184 @@ struct AdjPtArgs {
     int xcd_mode;
 };
 
-// P_{k-1} (history slot K) rows uz0-2 .. uz0+9 into PD
-#define ADJ_PLOAD(PD, K)                                                                            \
-    if (!RDQ_EXP_NOPLOAD) {                                                                         \
-        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(K) * L + so);                   \
-        _Pragma("unroll") for (int i = 0; i < PR; ++i)                                              \
-            PD[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(HR, pv[i], 0, RDQ_HLOAD_CP));  \
+__device__ __forceinline__ float bload_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, CP_NT));
+}
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// P_{k-1}, rows uz0-2 .. uz0+9 of one step: slab rows 0..7 as row pairs PC[i] = {i, i+4}, the
+// stencil's halo rows as PH = {-2, -1, 8, 9}.  HR = the epoch's history descriptor, SOFF = the
+// step's slot offset inside it (bytes): one 64-bit descriptor per epoch, not per step.
+#define ADJ_PLOAD(PC, PH, HR, SOFF)                                                                 \
+    {                                                                                               \
+        const int so_ = (SOFF);                                                                     \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            PC[i].x = bload_nt(HR, pv[i + 2], so_);                                                 \
+            PC[i].y = bload_nt(HR, pv[i + 6], so_);                                                 \
+        }                                                                                           \
+        PH[0] = bload_nt(HR, pv[0], so_); PH[1] = bload_nt(HR, pv[1], so_);                         \
+        PH[2] = bload_nt(HR, pv[10], so_); PH[3] = bload_nt(HR, pv[11], so_);                       \
     }
 
-// one adjoint step k; CUR = L_{k+1}, PRV = L_{k+2} -> L_k, P = P_{k-1} rows -2..9
-#define ADJ_STEP(CUR, PRV, P, PN)                                                                   \
-    {                                                                                               \
-        if (t + 1 < T && !RDQ_EXP_NOINEPOCH) ADJ_PLOAD(PN, k - 1)  /* OOB offsets off the interior */ \
-        const float dcur = dv[t];                                                                   \
-        float q[R];                                                                                 \
-        _Pragma("unroll") for (int r = 0; r < R; ++r) q[r] = A[r] * CUR[r];                         \
-        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0], q[1], q[R - 2], q[R - 1]);      \
-        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                             \
-            TB_VERT(q, r, h4, qm2, qm1, qp1, qp2)                                                   \
-            const float qc = q[r];                                                                  \
-            const float xl1 = dpp_shr1(qc), xr1 = dpp_shl1(qc);                                     \
-            const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                                   \
-            float n1 = qm1 + qp1; n1 = n1 + xl1; n1 = n1 + xr1;                                     \
-            float n2 = qm2 + qp2; n2 = n2 + xl2; n2 = n2 + xr2;                                     \
+// vertical neighbours of row pair i in a row-pair field X whose four outer rows are in
+// eU1 = {-1, 3}, eU2 = {-2, 2}, eD1 = {4, 8}, eD2 = {5, 9}
+#define PAIR_VERT(X, i, m1, p1, m2, p2)                                                             \
+    const f32x2 m1 = (i) >= 1 ? X[(i) - 1] : eU1;                                                   \
+    const f32x2 p1 = (i) <= 2 ? X[(i) + 1] : eD1;                                                   \
+    const f32x2 m2 = (i) >= 2 ? X[(i) - 2] : ((i) == 1 ? eU1 : eU2);                                \
+    const f32x2 p2 = (i) <= 1 ? X[(i) + 2] : ((i) == 2 ? eD1 : eD2);
+
+// gradient accumulation of one step (interior rows are the ones stored; every row of a wave that
+// has interior rows is computed: no per-row branch).  CU = L_{k+1}, LN = L_k, P / PH = P_{k-1}.
+//   gA_s += L_k (2c1 P + c2 S1(P) + c3 S2(P)),  GK += P (L_{k+1} - L_k)  (x K once at the end),
+//   gbeta[s] += L_k(src) w[k-1]
+#define ADJ_GRAD(CU, LN, P, PH, WK)                                                                 \
+    if (grad) {                                                                                     \
+        const f32x2 eU1 = {PH[1], P[3].x}, eU2 = {PH[0], P[2].x};                                   \
+        const f32x2 eD1 = {P[0].y, PH[2]}, eD2 = {P[1].y, PH[3]};                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            PAIR_VERT(P, i, m1, p1, m2, p2)                                                         \
+            const f32x2 c = P[i];                                                                   \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
+            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
+            f32x2 s1 = m1 + p1; s1 = s1 + xl1; s1 = s1 + xr1;                                       \
+            f32x2 s2 = m2 + p2; s2 = s2 + xl2; s2 = s2 + xr2;                                       \
+            const f32x2 l = LN[i];                                                                  \
             if constexpr (FMA) {                                                                    \
-                const float nb = __builtin_fmaf(C3, n2, C2 * n1);                                   \
-                PRV[r] = __builtin_fmaf(T1v[r], CUR[r], __builtin_fmaf(-T2v[r], PRV[r], nb));       \
+                const f32x2 lap = fma2(kC3, s2, kC2 * s1);                                          \
+                const f32x2 d = fma2(kC1X2, c, lap);                                                \
+                GA[i] = fma2(l, d, GA[i]);                                                          \
+                GK[i] = fma2(c, CU[i] - l, GK[i]);                                                  \
             } else {                                                                                \
-                float nb = C2 * n1; const float nb2 = C3 * n2; nb = nb + nb2;                       \
-                float l = T1v[r] * CUR[r]; const float l2 = T2v[r] * PRV[r]; l = l - l2; l = l + nb; \
-                PRV[r] = l;                                                                         \
-            }                                                                                       \
-        }                                                                                           \
-        if (rmask && ((k - 1) % g.st) == 0) {        /* uniform: receiver row waves */             \
-            unsigned rm_ = rmask;                                                                   \
-            LAUNDER(rm_);                                                                           \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if ((rm_ >> r) & 1u) PRV[r] = PRV[r] + dcur;     /* -0 on lanes without a receiver */ \
-            if (rmulti) {                                /* several receivers in one column */      \
-                const float *DS = DSb + (size_t)((k - 1) / g.st) * g.ng;                            \
-                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
-                    if ((rm_ >> r) & 1u)                                                            \
-                        for (int jj = rs + 1; jj < re; ++jj) PRV[r] = PRV[r] + DS[g.rcv_list[jj]];  \
-            }                                                                                       \
-        }                                                                                           \
-        if (grad) {                                                                                 \
-            unsigned rin_ = rin;                                                                    \
-            LAUNDER(rin_);                                                                          \
-            _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
-                if (!full && !((rin_ >> r) & 1u)) continue;                                        \
-                const float pc = P[r + 2];                                                          \
-                const float xl1 = dpp_shr1(pc), xr1 = dpp_shl1(pc);                                 \
-                const float xl2 = dpp_shr1(xl1), xr2 = dpp_shl1(xr1);                               \
-                float s1 = P[r + 1] + P[r + 3]; s1 = s1 + xl1; s1 = s1 + xr1;                       \
-                float s2 = P[r] + P[r + 4]; s2 = s2 + xl2; s2 = s2 + xr2;                           \
-                const float l = PRV[r];                                                             \
-                if constexpr (FMA) {                                                                \
-                    const float lap = __builtin_fmaf(C3, s2, C2 * s1);                              \
-                    const float d = __builtin_fmaf(C1X2, pc, lap);                                  \
-                    GA[r] = __builtin_fmaf(l, d, GA[r]);                                            \
-                    GK[r] = __builtin_fmaf(pc, CUR[r] - l, GK[r]);   /* x K at the end */          \
-                } else {                                                                            \
-                    float lap = C2 * s1; const float lq = C3 * s2; lap = lap + lq;                  \
-                    float d = C1X2 * pc; d = d + lap;                                               \
-                    const float c = l * d;                                                          \
-                    GA[r] = GA[r] + c;                                                              \
-                    float kk = KP[r] * pc; const float dl = CUR[r] - l; kk = kk * dl;               \
-                    if (xin) ksum += (double)kk;                                                    \
+                f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;                    \
+                f32x2 d = kC1X2 * c; d = d + lap;                                                   \
+                const f32x2 cc = l * d;                                                             \
+                GA[i] = GA[i] + cc;                                                                 \
+                f32x2 kk = KP[i] * c; const f32x2 dl = CU[i] - l; kk = kk * dl;                     \
+                if (xin) {                                                                          \
+                    if ((rin >> i) & 1u) ksum += (double)kk.x;                                      \
+                    if ((rin >> (i + 4)) & 1u) ksum += (double)kk.y;                                \
                 }                                                                                   \
             }                                                                                       \
-            if (smask) {                             /* gbeta: the source cell's lane only */      \
-                unsigned sm_ = smask;                                                               \
-                LAUNDER(sm_);                                                                       \
-                const float wk = wv[t];                                                             \
-                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
-                    if ((sm_ >> r) & 1u) { const float gb = scol ? PRV[r] * wk : -0.0f; gbacc = gbacc + gb; } \
+        }                                                                                           \
+        if (srow >= 0) {                             /* gbeta: the source cell's lane only */      \
+            int sr_ = srow;                                                                         \
+            LAUNDER(sr_);                                                                           \
+            float ls_ = 0.0f;                                                                       \
+            _Pragma("unroll") for (int r = 0; r < R; ++r) if (r == sr_) ls_ = PT_AT(LN, r);         \
+            const float gb = scol ? ls_ * (WK) : -0.0f;                                             \
+            gbacc = gbacc + gb;                                                                     \
+        }                                                                                           \
+    }
+
+// one adjoint step k: CUR = L_{k+1}, PRV = L_{k+2} -> L_k; P / PH = P_{k-1}; the
+// next step's P_{k-2} is prefetched into PN / PHN.  The gradient of the epoch's last step is
+// deferred past the publish (see k_adj_pt).
+#define ADJ_STEP(CUR, PRV, P, PH, PN, PHN)                                                          \
+    {                                                                                               \
+        if (t + 1 < T) ADJ_PLOAD(PN, PHN, HRe, (T - 2 - t) * L4)                                    \
+        const float dcur = dv[t];                                                                   \
+        f32x2 q[4];                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[2].y, q[3].y);      \
+        const f32x2 eU1 = {h4.u1, q[3].x}, eU2 = {h4.u2, q[2].x};                                   \
+        const f32x2 eD1 = {q[0].y, h4.d1}, eD2 = {q[1].y, h4.d2};                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            PAIR_VERT(q, i, m1, p1, m2, p2)                                                         \
+            const f32x2 c = q[i];                                                                   \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
+            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
+            f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
+            f32x2 n2 = m2 + p2; n2 = n2 + xl2; n2 = n2 + xr2;                                       \
+            if constexpr (FMA) {                                                                    \
+                const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                           \
+                PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                           \
+            } else {                                                                                \
+                f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;                     \
+                f32x2 l = T1v[i] * CUR[i]; const f32x2 l2 = T2v[i] * PRV[i]; l = l - l2; l = l + nb; \
+                PRV[i] = l;                                                                         \
             }                                                                                       \
         }                                                                                           \
+        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+            int rr_ = rrow;                                                                         \
+            LAUNDER(rr_);                                                                           \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if (r == rr_) PT_AT(PRV, r) = PT_AT(PRV, r) + dcur;   /* -0 off the receivers */     \
+        }                                                                                           \
+        if (t + 1 < T || last) ADJ_GRAD(CUR, PRV, P, PH, wv[t])                                     \
     }
 
 // Adjoint, persistent.  Per step k = nt..1:
 //   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
 //   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k),
 //   gbeta[s] += L_k(src) w[k-1]        (interior cells; accumulators in registers for all nt steps)
-// P_{k-1} comes from the history: each wave loads its interior rows +-2 (12 rows) one step ahead
-// into alternating register arrays (no copies, so the wait lands at the gradient, not at the
-// step's start) and needs no LDS exchange for it.
-template <int T, int NW, bool FMA>
+// P_{k-1} comes from the history: each wave loads its rows +-2 one step ahead into alternating
+// register arrays and needs no LDS exchange for it.  Per epoch of T steps: steps, publish of the
+// border, then the LAST step's gradient (it needs no neighbour data: the interior L_k, L_{k+1} and
+// the wave's own history rows), and only then the hand-off sweep — the gradient's VALU work fills
+// the time the neighbours' granules take to arrive.
+template <int T, int NW, bool FMA, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 {
-    constexpr int PR = TB_R + 4;
+    unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     __shared__ float xch[2][NW][4][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    float A[R], T1v[R], T2v[R], KP[R], L0[R], L1[R], GA[R], GK[R];
-    unsigned smask = 0, rmask = 0;
+    f32x2 A[4], T1v[4], T2v[4], KP[4], L0[4], L1[4], GA[4], GK[4];
+    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2};
+    int srow = -1, rrow = -1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int gz = wrap_row(uz0 + r, g.Hp);
         const int o = gz * g.ld + gx;
-        A[r] = AL[o]; T1v[r] = AL[g.cstride + o]; T2v[r] = AL[2 * g.cstride + o]; KP[r] = AL[3 * g.cstride + o];
-        L0[r] = 0.0f; L1[r] = 0.0f;                       // L_{nt+1} = L_{nt+2} = 0
-        GA[r] = 0.0f; GK[r] = 0.0f;
-        if (gz == g.isz && ((rin >> r) & 1u)) smask |= 1u << r;
-        if (gz == g.igz) rmask |= 1u << r;
+        PT_AT(A, r) = AL[o]; PT_AT(T1v, r) = AL[g.cstride + o]; PT_AT(T2v, r) = AL[2 * g.cstride + o];
+        if constexpr (!FMA) PT_AT(KP, r) = AL[3 * g.cstride + o];
+        PT_AT(L0, r) = 0.0f; PT_AT(L1, r) = 0.0f;         // L_{nt+1} = L_{nt+2} = 0
+        PT_AT(GA, r) = 0.0f; PT_AT(GK, r) = 0.0f;
+        if (gz == g.isz && ((rin >> r) & 1u)) srow = r;
+        if (gz == g.igz) rrow = r;
     }
     const bool scol = xin && gx == g.isx[s];
-    const bool full = rin == 0xFFu;
-    int rs = 0, re = 0, rcv0 = -1;
-    if (rmask) {
-        rs = g.rcv_start[gx]; re = g.rcv_start[gx + 1];
-        rcv0 = rs < re ? g.rcv_list[rs] : -1;
-    }
-    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.ng;
+    // residual of this lane's column: one receiver's dseis, or several receivers' folded sum
+    const int rcv0 = rrow >= 0 ? g.rlane[gx] : -1;
+    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
     // dseis[k-1] of this lane's receiver; -0 (x + -0 == x bitwise) where there is none.  An
     // unconditional buffer load (OOB offset: no memory access) keeps every wave's vmcnt count equal.
 #define DLOAD(KK)                                                                                   \
     ({                                                                                              \
-        const bool ok_ = rcv0 >= 0 && (KK) >= 1 && (((KK) - 1) % g.st) == 0;                        \
-        const float v_ = bload(DSR, ok_ ? (((KK) - 1) / g.st * g.ng + rcv0) * 4 : OOB, 0);          \
+        const int ri_ = (KK) >= 1 ? rec_index((KK) - 1, g.st) : -1;                                 \
+        const bool ok_ = rcv0 >= 0 && ri_ >= 0;                                                     \
+        const float v_ = bload(DSR, ok_ ? (ri_ * g.dstride + rcv0) * 4 : OOB, 0);                   \
         ok_ ? v_ : -0.0f;                                                                           \
     })
-    const bool rmulti = __any(re - rs > 1);
     const bool grad = rin != 0;                           // uniform: this wave has interior rows
     double ksum = 0.0;
     float gbacc = 0.0f;
     const size_t L = g.level;
-    float PA[PR], PB[PR];
-    int pv[PR];                                           // P row (uz0 - 2 + i) offset of this lane
+    const int L4 = (int)(L * 4);                          // bytes per history slot (< 2 GB: resident surveys)
+    f32x2 PA[4], PB[4];
+    float PHA[4], PHB[4];
+    int pv[12];                                           // P row (uz0 - 2 + i) offset of this lane
 #pragma unroll
-    for (int i = 0; i < PR; ++i) {
-        PA[i] = 0.0f; PB[i] = 0.0f;
-        pv[i] = grad ? (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4 : OOB;   // OOB: no memory access
-    }
+    for (int i = 0; i < 12; ++i) pv[i] = grad ? (wrap_row(uz0 + i - 2, g.Hp) * g.ld + gx) * 4 : OOB;
+    // history descriptor of the epoch whose first step is KN: slots KN - T + 1 .. KN (step t of the
+    // epoch reads slot KN - t at byte offset (T - 1 - t) * L4)
+#define HIST_RSRC(KN) rsrc_of(a.hist + (ptrdiff_t)((KN) - (T - 1)) * (ptrdiff_t)L + (ptrdiff_t)so)
     // Per-epoch inputs (the first step's history slice P, the receiver residuals dseis[k-1] and the
     // wavelet w[k-1] of the epoch's T steps) are issued right behind the hand-off loads of the
     // previous epoch's sweep (ADJ_ISSUE), so the sweep does not wait for this HBM traffic; inside an
     // epoch a step waits only for its own P (prefetched one step ahead).
     float wv[T], dv[T];
-    ADJ_PLOAD(PA, a.nt)
+    {
+        const __amdgpu_buffer_rsrc_t H0 = HIST_RSRC(a.nt);
+        ADJ_PLOAD(PA, PHA, H0, (T - 1) * L4)
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         wv[t] = a.wav[max(a.nt - t - 1, 0)];
@@ -1195,36 +1257,45 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
 #define ADJ_ISSUE                                                                                   \
-    ADJ_PLOAD(PA, kn)                                                                               \
-    _Pragma("unroll") for (int t = 0; t < T; ++t) {                                                 \
-        wv[t] = a.wav[max(kn - t - 1, 0)];                                                          \
-        dv[t] = DLOAD(kn - t);                                                                      \
+    {                                                                                               \
+        const __amdgpu_buffer_rsrc_t HN = HIST_RSRC(kn);                                            \
+        ADJ_PLOAD(PA, PHA, HN, (T - 1) * L4)                                                        \
+        _Pragma("unroll") for (int t = 0; t < T; ++t) {                                             \
+            wv[t] = a.wav[max(kn - t - 1, 0)];                                                      \
+            dv[t] = DLOAD(kn - t);                                                                  \
+        }                                                                                           \
     }
     const int nep = (a.nt + T - 1) / T;
     bool live = true;
-    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
     for (int e = 0; e < nep; ++e) {
+        const int ke = a.nt - e * T;                      // first step k of this epoch
+        const bool last = e + 1 == nep;
+        const __amdgpu_buffer_rsrc_t HRe = HIST_RSRC(ke);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int j = e * T + t;
             if (j >= a.nt) break;
-            const int k = a.nt - j;
-            if (t & 1) ADJ_STEP(L0, L1, PB, PA)
-            else ADJ_STEP(L1, L0, PA, PB)
+            const int k = ke - t;
+            if (t & 1) ADJ_STEP(L0, L1, PB, PHB, PA, PHA)
+            else ADJ_STEP(L1, L0, PA, PHA, PB, PHB)
         }
-        if (T & 1) {   // keep "L1 = newest, PA = next step's P" at every epoch boundary
+        if (T & 1) {   // keep "L1 = newest, PB = the last step's P, PA = free" at every epoch boundary
 #pragma unroll
-            for (int r = 0; r < R; ++r) { const float tmp = L0[r]; L0[r] = L1[r]; L1[r] = tmp; }
-#pragma unroll
-            for (int i = 0; i < PR; ++i) { const float tmp = PA[i]; PA[i] = PB[i]; PB[i] = tmp; }
+            for (int i = 0; i < 4; ++i) {
+                const f32x2 tl = L0[i]; L0[i] = L1[i]; L1[i] = tl;
+                const f32x2 tp = PA[i]; PA[i] = PB[i]; PB[i] = tp;
+                const float th = PHA[i]; PHA[i] = PHB[i]; PHB[i] = th;
+            }
         }
         PT_PROF(tst)
-        if (e + 1 < nep) {
+        if (!last) {
             const unsigned tag = (unsigned)(e + 1);
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, L0, L1)
-            const int kn = a.nt - (e + 1) * T;            // first step k of the next epoch
+            ADJ_GRAD(L0, L1, PB, PHB, wv[T - 1])          // the deferred last step (no neighbour data)
+            const int kn = ke - T;                        // first step k of the next epoch
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             ADJ_ISSUE
@@ -1233,25 +1304,29 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
 #undef DLOAD
 #undef ADJ_ISSUE
-    if (a.prof && lane == 0) {
-        atomicAdd(a.prof + 0, tsw); atomicAdd(a.prof + 1, tst); atomicAdd(a.prof + 2, tpb); atomicAdd(a.prof + 3, 1ull);
-        atomicAdd(a.prof + 4, tfp); atomicAdd(a.prof + 5, npass);
+#undef HIST_RSRC
+    if (prof && lane == 0) {
+        atomicAdd(prof + 0, tsw); atomicAdd(prof + 1, tst); atomicAdd(prof + 2, tpb); atomicAdd(prof + 3, 1ull);
+        atomicAdd(prof + 4, tfp); atomicAdd(prof + 5, npass);
         if (blockIdx.x < PROF_WAVES / 16) {
-            unsigned long long *raw = a.prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
+            unsigned long long *raw = prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
             raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
         }
     }
     if (xin) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if ((rin >> r) & 1u) a.gA[so + (size_t)PT_ROFS(r) + gx] = GA[r];
+            if ((rin >> r) & 1u) a.gA[so + (size_t)PT_ROFS(r) + gx] = PT_AT(GA, r);
     }
-    if (smask && scol) a.gbeta[bs] = gbacc;
+    if (srow >= 0 && scol) a.gbeta[bs] = gbacc;
     if constexpr (FMA) {   // gk = sum K * (sum_k P (L_{k+1} - L_k)) over the own cells
         if (xin) {
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                if ((rin >> r) & 1u) ksum += (double)KP[r] * (double)GK[r];
+                if ((rin >> r) & 1u) {
+                    const float kp = AL[3 * g.cstride + PT_ROFS(r) + gx];
+                    ksum += (double)kp * (double)PT_AT(GK, r);
+                }
         }
     }
     // deterministic workgroup reduction of the sponge-coefficient partial sum
@@ -1265,7 +1340,10 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
 }
 #undef ADJ_STEP
+#undef ADJ_GRAD
 #undef ADJ_PLOAD
+#undef PAIR_VERT
+#undef PT_AT
 #undef PT_SWEEP
 #undef PT_PUBLISH
 #undef PT_PROF
@@ -1273,6 +1351,26 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 #undef PT_REGION_INIT
 #undef LAUNDER
 #undef TB_VERT
+
+// Receivers sharing a padded column (ng > nx, or repeated gx): their residuals at one (model, shot,
+// record) summed in receiver order into one value per column, the gradient the reference's
+// indexing backward builds (index_put with accumulate into zeros, pde.py:82-83), so the time-loop
+// kernels inject one value per lane and step with no per-receiver loop.
+__global__ __launch_bounds__(256) void k_rcv_fold(const float *__restrict__ ds, float *__restrict__ out,
+                                                  const int *__restrict__ colx, const int *__restrict__ rcv_start,
+                                                  const int *__restrict__ rcv_list, int ng, int ncolr, size_t rows)
+{
+    const size_t n = rows * (size_t)ncolr;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = i / ncolr;
+        const int c = (int)(i - row * ncolr), x = colx[c];
+        const float *d = ds + row * ng;
+        const int r0 = rcv_start[x], r1 = rcv_start[x + 1];
+        float v = d[rcv_list[r0]];
+        for (int j = r0 + 1; j < r1; ++j) v = v + d[rcv_list[j]];
+        out[i] = v;
+    }
+}
 
 // --------------------------------------------------------------------------------------- K4
 struct FinArgs {
@@ -1526,6 +1624,10 @@ struct rdq_fwi_plan {
     std::vector<float> wavf;
     int Hp, Wp, ld, nrec;
     int *d_isx = nullptr, *d_rcv_start = nullptr, *d_rcv_list = nullptr;
+    int *d_rlane = nullptr;     // [Wp] adjoint residual index per column (receiver id, or folded column)
+    int *d_colx = nullptr;      // [ncolr] padded column of each receiver column (fold)
+    int ncolr = 0;              // columns holding a receiver
+    bool rmulti = false;        // some column holds several receivers: residuals folded per column
     float *d_wav = nullptr;     // fp32 wavelet [nt] (persistent kernels)
     unsigned *d_status = nullptr;   // status words in use: d_status_own or a caller buffer (rdq_fwi_set_status_buffer)
     unsigned *d_status_own = nullptr;
@@ -1537,6 +1639,7 @@ struct rdq_fwi_plan {
     int xcd_mode = 1;           // persistent kernels: XCD-local slices with L2 hand-offs (pt_assign)
     int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
     int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
+    int cap_adjf8[TB_MAXT + 1] = {0}, cap_adjf12[TB_MAXT + 1] = {0};
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
@@ -1565,6 +1668,7 @@ TBGeo tb_geo(const rdq_fwi_plan *p, int B)
     g.cstride = (size_t)B * g.slice;
     g.level = (size_t)B * g.ns * g.slice;
     g.isx = p->d_isx; g.rcv_start = p->d_rcv_start; g.rcv_list = p->d_rcv_list;
+    g.rlane = p->d_rlane; g.dstride = p->rmulti ? p->ncolr : p->g.ng;
     g.s_off = 0; g.ns_grp = p->g.ns;
     return g;
 }
@@ -1670,11 +1774,12 @@ template <int NW>
 int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
 {
     int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
+    int *cf = NW == 12 ? p->cap_adjf12 : p->cap_adjf8;   // both adjoint variants: the launch must fit either
     switch (T) {
-    case 1: return adj ? resident_capacity(k_adj_pt<1, NW, false>, 64 * NW, c[1]) : resident_capacity(k_fwd_pt<1, NW>, 64 * NW, c[1]);
-    case 2: return adj ? resident_capacity(k_adj_pt<2, NW, false>, 64 * NW, c[2]) : resident_capacity(k_fwd_pt<2, NW>, 64 * NW, c[2]);
-    case 3: return adj ? resident_capacity(k_adj_pt<3, NW, false>, 64 * NW, c[3]) : resident_capacity(k_fwd_pt<3, NW>, 64 * NW, c[3]);
-    default: return adj ? resident_capacity(k_adj_pt<4, NW, false>, 64 * NW, c[4]) : resident_capacity(k_fwd_pt<4, NW>, 64 * NW, c[4]);
+    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false, false>, 64 * NW, c[1]), resident_capacity(k_adj_pt<1, NW, true, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
+    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false, false>, 64 * NW, c[2]), resident_capacity(k_adj_pt<2, NW, true, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
+    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false, false>, 64 * NW, c[3]), resident_capacity(k_adj_pt<3, NW, true, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
+    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false, false>, 64 * NW, c[4]), resident_capacity(k_adj_pt<4, NW, true, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
     }
 }
 
@@ -1746,11 +1851,15 @@ template <int NW>
 void launch_fwd_pt(int T, dim3 grid, hipStream_t st, const FwdPtArgs &a)
 {
     const dim3 blk(64 * NW);
+    if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW, true>), grid, blk, 0, st, a);
+        return;
+    }
     switch (T) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<1, NW>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<2, NW>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<3, NW>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<1, NW, false>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<2, NW, false>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<3, NW, false>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW, false>), grid, blk, 0, st, a); break;
     }
 }
 
@@ -1758,11 +1867,15 @@ template <int NW, bool F>
 void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
 {
     const dim3 blk(64 * NW);
+    if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F, true>), grid, blk, 0, st, a);
+        return;
+    }
     switch (T) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, F>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, F>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, F>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, F, false>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, F, false>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, F, false>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F, false>), grid, blk, 0, st, a); break;
     }
 }
 
@@ -1997,12 +2110,26 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return p->igx[a] < p->igx[b]; });
     for (int r = 0; r < geom->ng; ++r) start[p->igx[r] + 1]++;
     for (int x = 0; x < p->Wp; ++x) start[x + 1] += start[x];
+    // adjoint residual per column: the receiver's own dseis, or (several receivers in one column)
+    // their residuals folded in receiver order into one value per column (k_rcv_fold)
+    std::vector<int> rlane(p->Wp, -1), colx;
+    for (int x = 0; x < p->Wp; ++x) {
+        if (start[x + 1] - start[x] > 1) p->rmulti = true;
+        if (start[x + 1] > start[x]) colx.push_back(x);
+    }
+    p->ncolr = (int)colx.size();
+    for (int c = 0; c < p->ncolr; ++c) rlane[colx[c]] = p->rmulti ? c : order[start[colx[c]]];
     hipError_t e = hipMalloc(&p->d_isx, sizeof(int) * geom->ns);
     if (e == hipSuccess) e = hipMalloc(&p->d_rcv_start, sizeof(int) * (p->Wp + 1));
     if (e == hipSuccess) e = hipMalloc(&p->d_rcv_list, sizeof(int) * geom->ng);
     if (e == hipSuccess) e = hipMemcpy(p->d_isx, p->isx.data(), sizeof(int) * geom->ns, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_rcv_start, start.data(), sizeof(int) * (p->Wp + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_rcv_list, order.data(), sizeof(int) * geom->ng, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_rlane, sizeof(int) * p->Wp);
+    if (e == hipSuccess) e = hipMemcpy(p->d_rlane, rlane.data(), sizeof(int) * p->Wp, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_colx, sizeof(int) * std::max(p->ncolr, 1));
+    if (e == hipSuccess && p->ncolr)
+        e = hipMemcpy(p->d_colx, colx.data(), sizeof(int) * p->ncolr, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_wav, sizeof(float) * geom->nt);
     if (e == hipSuccess) e = hipMemcpy(p->d_wav, p->wavf.data(), sizeof(float) * geom->nt, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_status_own, 256);
@@ -2023,6 +2150,8 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
     if (p->d_isx) (void)hipFree(p->d_isx);
     if (p->d_rcv_start) (void)hipFree(p->d_rcv_start);
     if (p->d_rcv_list) (void)hipFree(p->d_rcv_list);
+    if (p->d_rlane) (void)hipFree(p->d_rlane);
+    if (p->d_colx) (void)hipFree(p->d_colx);
     if (p->d_wav) (void)hipFree(p->d_wav);
     if (p->d_status_own) (void)hipFree(p->d_status_own);
     if (p->d_prof) (void)hipFree(p->d_prof);
@@ -2168,6 +2297,7 @@ int rdq_fwi_sizes(const rdq_fwi_plan *p, int32_t B, rdq_fwi_sizes_t *o)
     o->seis = (size_t)B * ns * p->nrec * p->g.ng * sizeof(float);
     o->history = (size_t)(p->g.nt + 2) * B * ns * slice * sizeof(float);
     o->ring = 4 * (size_t)B * ns * slice * sizeof(unsigned long long);
+    if (p->rmulti) o->ring += (size_t)B * ns * p->nrec * p->ncolr * sizeof(float);   // folded residuals
     o->gA = (size_t)B * ns * slice * sizeof(float);
     o->gk_part = (size_t)B * ns * adj_blocks(p) * sizeof(double);
     o->gbeta = (size_t)B * ns * sizeof(float);
@@ -2227,6 +2357,14 @@ int rdq_fwi_adjoint(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, cons
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !hist || !dseis || !ring || !gA || !gk || !gbeta || B < 1) return RDQ_E_INVALID;
+    if (p->rmulti) {   // several receivers in a column: fold the residuals per column (ring tail)
+        float *fold = ring + 8 * (size_t)B * p->g.ns * p->Hp * p->ld;
+        const size_t rows = (size_t)B * p->g.ns * p->nrec, n = rows * p->ncolr;
+        hipLaunchKernelGGL(k_rcv_fold, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                           dseis, fold, p->d_colx, p->d_rcv_start, p->d_rcv_list, p->g.ng, p->ncolr, rows);
+        RDQ_CHECK(hipGetLastError());
+        dseis = fold;
+    }
     int per = 0;
     if (const int nw = persistent_nw(p, B, true, &per))
         return launch_adjoint_pt(p, B, nw, per, coeffs, hist, dseis, ring, gA, gk, gbeta, st);

@@ -295,10 +295,12 @@ def test_batch_and_dot_product_openfwi_ns8(cuda):
     seis = fwi(vv)
     w = torch.randn_like(seis)
     (seis * w).sum().backward()
+    fwi.check()
     g = vv.grad.double()
     dv = 5e-3 * torch.randn_like(v)
     with torch.no_grad():
         lhs = (((fwi(v + dv).double() - fwi(v - dv).double()) / 2) * w.double()).sum()
+    fwi.check()
     rhs = (g * dv.double()).sum()
     assert abs(lhs - rhs) / abs(rhs) < 2e-2, (lhs.item(), rhs.item())
     with torch.no_grad():
