@@ -3,14 +3,15 @@
 // Reference behaviour (SimingShan/red-diffeq):
 //   K3 rdq_fwi_coeffs      red_diffeq/solvers/pde.py:91 (replicate pad), 38-52 (get_Abc),
 //                          63-71 (alpha/temp1/temp2/beta), utils/data_trans.py:13-15 (denorm)
-//   K1 rdq_fwi_forward     pde.py:74-86, one fused launch per time step (stencil + periodic wrap
-//                          + source injection + receiver sampling + history store)
+//   K1 rdq_fwi_forward     pde.py:74-86: the whole nt-step time loop (stencil + periodic wrap + source
+//                          injection + receiver sampling + history store) in ONE persistent launch when
+//                          the survey fits resident (k_fwd_pt), else launches of T steps (k_fwd_tb)
 //   K2 rdq_fwi_adjoint     the autograd backward of pde.py:74-86 (discrete adjoint)
 //   K4 rdq_fwi_grad_finalize  chain rule back to v_norm incl. the vmin/argmin sponge term
 //
 // fp32 operation order follows the reference expression order exactly and the file is built
-// with -ffp-contract=off, so K1 reproduces the reference seismograms bit-for-bit and K2 matches
-// the oracle's gA accumulator bit-for-bit (tests/test_gpu_parity.py).
+// with -ffp-contract=off, so K1 reproduces the reference seismograms bit-for-bit and K2's
+// exact-order variant matches the oracle's gA accumulator bit-for-bit (tests/test_gpu_fwi.py).
 //
 // Data layout (HBM): padded grid Hp x Wp with row pitch ld = roundup(Wp, 64) floats (256-B
 // aligned rows -> every row of a 64-wide tile is 1 or 2 full 128-B lines).
@@ -267,9 +268,7 @@ __device__ __forceinline__ Halo4 exchange_nw(float (*xch)[NW][4][64], int buf, i
     xch[buf][w][1][lane] = top1;
     xch[buf][w][2][lane] = bot1;
     xch[buf][w][3][lane] = bot0;
-#ifndef RDQ_EXP_NOBARRIER        // timing experiments only (tools/exp_variants.sh): wrong results
     __syncthreads();
-#endif
     Halo4 h;
     const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
     h.u2 = xch[buf][wu][2][lane];
@@ -633,32 +632,11 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
 //
 // Granule buffer (inside the caller's `ring`): [2 epoch parity][B][ns][Hp][ld] x 16-B granules,
 // zeroed before each launch; tag = epoch index (>= 1) so a zeroed granule never matches.
-// timing-experiment knockouts (0 in the product build; tools/exp_variants.sh builds the others)
-#ifndef RDQ_EXP_SWEEP_ONCE
-#define RDQ_EXP_SWEEP_ONCE 0
-#endif
-#ifndef RDQ_EXP_NOPLOAD
-#define RDQ_EXP_NOPLOAD 0
-#endif
-#ifndef RDQ_HLOAD_CP
-#define RDQ_HLOAD_CP CP_NT    // history loads: non-temporal (read once; keeps the hand-off lines in L2)
-#endif
-#ifndef RDQ_HIST_CP
-#define RDQ_HIST_CP CP_NT     // history stores: non-temporal (re-read only by the adjoint, GBs later)
-#endif
-#ifndef RDQ_EXP_NOSTORE
-#define RDQ_EXP_NOSTORE 0
-#endif
-constexpr int CP_SC1 = 16;
-#ifndef RDQ_EXP_NOINEPOCH
-#define RDQ_EXP_NOINEPOCH 0   // timing experiment: skip the in-epoch history prefetch (wrong results)
-#endif
-#ifndef PT_ADJ_SG
-#define PT_ADJ_SG 4   // adjoint hand-off sweep: rows per load group (register budget)
-#endif
+constexpr int CP_SC1 = 16;                            // buffer cache policy: sc1 (write-through / L1 bypass)
+constexpr int PT_ADJ_SG = 8;                          // adjoint hand-off sweep: rows per load group
 constexpr size_t PROF_RAW = 8;                        // per-wave records after the 4 summary words
 constexpr size_t PROF_WAVES = 4096 * 16;              // blocks x waves recorded
-constexpr size_t PROF_WORDS = PROF_RAW + PROF_WAVES * 3;   // per kernel (fwd, then adj)                           // buffer cache policy: sc1 (write-through / L1 bypass)
+constexpr size_t PROF_WORDS = PROF_RAW + PROF_WAVES * 3;   // per kernel (fwd, then adj)
 constexpr unsigned long long PT_TIMEOUT_TICKS = 20000000ull;   // 200 ms of s_memrealtime (100 MHz)
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -931,10 +909,10 @@ struct FwdPtArgs {
             const f32x2 p2 = i <= 1 ? CUR[i + 2] : (i == 2 ? eD1 : eD2);                            \
             const f32x2 c = CUR[i];                                                                 \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
-            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
-            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
             f32x2 s1 = m1 + p1; s1 = s1 + xl1; s1 = s1 + xr1;                                       \
-            f32x2 s2 = m2 + p2; s2 = s2 + xl2; s2 = s2 + xr2;                                       \
+            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            s2.x = s2.x + dpp_shr1(xl1.x); s2.y = s2.y + dpp_shr1(xl1.y);                           \
+            s2.x = s2.x + dpp_shl1(xr1.x); s2.y = s2.y + dpp_shl1(xr1.y);                           \
             f32x2 lap = kC2 * s1; const f32x2 l2 = kC3 * s2; lap = lap + l2;                        \
             f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
             const f32x2 a3 = A[i] * lap;                                                            \
@@ -948,11 +926,11 @@ struct FwdPtArgs {
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
                 if ((sm_ >> r) & 1u) PT_AT(PRV, r) = PT_AT(PRV, r) + add;                                         \
         }                                                                                           \
-        if (!RDQ_EXP_NOSTORE && a.hist) {   /* own cells only; issued at once (the faster of the     \
+        if (a.hist) {                       /* own cells only; issued at once (the faster of the     \
                                                store placements measured: tools/exp_variants.sh) */ \
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
             _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(PRV, r)), HR, hv[r], 0, RDQ_HIST_CP); \
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(PRV, r)), HR, hv[r], 0, CP_NT); \
         }                                                                                           \
         if (rrow >= 0 && rec_index(n, g.st) >= 0) {                                                 \
             float *SK = a.seis + ((size_t)bs * g.nrec + rec_index(n, g.st)) * g.ng;                 \
@@ -1112,10 +1090,10 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
             PAIR_VERT(P, i, m1, p1, m2, p2)                                                         \
             const f32x2 c = P[i];                                                                   \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
-            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
-            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
             f32x2 s1 = m1 + p1; s1 = s1 + xl1; s1 = s1 + xr1;                                       \
-            f32x2 s2 = m2 + p2; s2 = s2 + xl2; s2 = s2 + xr2;                                       \
+            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            s2.x = s2.x + dpp_shr1(xl1.x); s2.y = s2.y + dpp_shr1(xl1.y);                           \
+            s2.x = s2.x + dpp_shl1(xr1.x); s2.y = s2.y + dpp_shl1(xr1.y);                           \
             const f32x2 l = LN[i];                                                                  \
             if constexpr (FMA) {                                                                    \
                 const f32x2 lap = fma2(kC3, s2, kC2 * s1);                                          \
@@ -1160,10 +1138,10 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
             PAIR_VERT(q, i, m1, p1, m2, p2)                                                         \
             const f32x2 c = q[i];                                                                   \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
-            const f32x2 xl2 = {dpp_shr1(xl1.x), dpp_shr1(xl1.y)};                                   \
-            const f32x2 xr2 = {dpp_shl1(xr1.x), dpp_shl1(xr1.y)};                                   \
             f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
-            f32x2 n2 = m2 + p2; n2 = n2 + xl2; n2 = n2 + xr2;                                       \
+            f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
+            n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
             if constexpr (FMA) {                                                                    \
                 const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                           \
                 PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                           \
@@ -1339,6 +1317,230 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
 }
+// ---- FMA build of the persistent adjoint: the gradient from the history's time recurrence.
+// The forward's own update P_k = T1 P_{k-1} - T2 P_{k-2} + A lap'(P_{k-1}) (+ beta w[k-1] at the
+// source cell, pde.py:79-81) gives the stencil term the gradient needs without a stencil:
+//   lap'(P_{k-1}) = (P_k - T1 P_{k-1} + T2 P_{k-2} - src) / A,   d = 2c1 P_{k-1} + lap'(P_{k-1})
+// so a step's gradient is 7 packed ops per row pair (no DPP, no P halo rows, 8 history rows per
+// wave and step instead of 12).  The history values are the forward's own, so the identity holds
+// up to the rounding of P_k's last add (fp32 tolerance, like the FMA contraction of the step).
+// The window lives in four row-pair buffers Q0..Q3 that rotate by one per step (step t of an
+// epoch: P_k, P_{k-1}, P_{k-2} = Q[t], Q[t+1], Q[t+2] mod 4, prefetch into Q[t+3]): no copies for
+// T = 4; other depths restore the order once per epoch.
+
+#define ADJR_LOAD(PD, HR, SOFF)                                                                     \
+    {                                                                                               \
+        const int so_ = (SOFF);                                                                     \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            PD[i].x = bload_nt(HR, pr[i], so_);                                                     \
+            PD[i].y = bload_nt(HR, pr[i + 4], so_);                                                 \
+        }                                                                                           \
+    }
+
+// gradient of step k (CU = L_{k+1}, LN = L_k; wavelet sample WK = w[k-1]; window P0 = P_k,
+// P1 = P_{k-1}, P2 = P_{k-2})
+#define ADJR_GRAD(CU, LN, WK, P0, P1, P2)                                                           \
+    if (grad) {                                                                                     \
+        f32x2 u[4];                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            u[i] = fma2(-T1v[i], P1[i], P0[i]);                                                     \
+            u[i] = fma2(T2v[i], P2[i], u[i]);                                                       \
+        }                                                                                           \
+        if (srow >= 0) {                             /* the forward's source add, undone */        \
+            int sr_ = srow;                                                                         \
+            LAUNDER(sr_);                                                                           \
+            const float sa_ = scol ? bsrc * (WK) : 0.0f;                                            \
+            float ls_ = 0.0f;                                                                       \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if (r == sr_) { PT_AT(u, r) = PT_AT(u, r) - sa_; ls_ = PT_AT(LN, r); }              \
+            const float gb = scol ? ls_ * (WK) : -0.0f;                                             \
+            gbacc = gbacc + gb;                                                                     \
+        }                                                                                           \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            const f32x2 d = fma2(kC1X2, P1[i], u[i] * rA[i]);                                       \
+            GA[i] = fma2(LN[i], d, GA[i]);                                                          \
+            GK[i] = fma2(P1[i], CU[i] - LN[i], GK[i]);                                              \
+        }                                                                                           \
+    }
+
+// one adjoint step k: CUR = L_{k+1}, PRV = L_{k+2} -> L_k; window P0 / P1 / P2 as ADJR_GRAD;
+// history slot k-2 (the next step's P_{k-3}) prefetched into PN
+#define ADJR_STEP(CUR, PRV, P0, P1, P2, PN)                                                         \
+    {                                                                                               \
+        if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
+        const float dcur = dv[t];                                                                   \
+        f32x2 q[4];                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[2].y, q[3].y);      \
+        const f32x2 eU1 = {h4.u1, q[3].x}, eU2 = {h4.u2, q[2].x};                                   \
+        const f32x2 eD1 = {q[0].y, h4.d1}, eD2 = {q[1].y, h4.d2};                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+            PAIR_VERT(q, i, m1, p1, m2, p2)                                                         \
+            const f32x2 c = q[i];                                                                   \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
+            f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
+            n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
+            const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
+            PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
+        }                                                                                           \
+        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+            int rr_ = rrow;                                                                         \
+            LAUNDER(rr_);                                                                           \
+            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
+                if (r == rr_) PT_AT(PRV, r) = PT_AT(PRV, r) + dcur;   /* -0 off the receivers */     \
+        }                                                                                           \
+        if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
+    }
+
+template <int T, int NW, bool PROF>
+__global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
+{
+    unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
+    __shared__ float xch[2][NW][4][64];
+    __shared__ double red[64 * NW];
+    const TBGeo &g = a.g;
+    PT_REGION_INIT(NW)
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    f32x2 A[4], rA[4], T1v[4], T2v[4], L0[4], L1[4], GA[4], GK[4];
+    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2};
+    int srow = -1, rrow = -1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int gz = wrap_row(uz0 + r, g.Hp);
+        const int o = gz * g.ld + gx;
+        PT_AT(A, r) = AL[o]; PT_AT(T1v, r) = AL[g.cstride + o]; PT_AT(T2v, r) = AL[2 * g.cstride + o];
+        PT_AT(rA, r) = 1.0f / PT_AT(A, r);
+        PT_AT(L0, r) = 0.0f; PT_AT(L1, r) = 0.0f;         // L_{nt+1} = L_{nt+2} = 0
+        PT_AT(GA, r) = 0.0f; PT_AT(GK, r) = 0.0f;
+        if (gz == g.isz && ((rin >> r) & 1u)) srow = r;
+        if (gz == g.igz) rrow = r;
+    }
+    const int isx = g.isx[s];
+    const bool scol = xin && gx == isx;
+    const float bsrc = srow >= 0 ? AL[4 * g.cstride + (size_t)g.isz * g.ld + isx] : 0.0f;   // beta at the source
+    const int rcv0 = rrow >= 0 ? g.rlane[gx] : -1;
+    const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
+    const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
+#define DLOAD(KK)                                                                                   \
+    ({                                                                                              \
+        const int ri_ = (KK) >= 1 ? rec_index((KK) - 1, g.st) : -1;                                 \
+        const bool ok_ = rcv0 >= 0 && ri_ >= 0;                                                     \
+        const float v_ = bload(DSR, ok_ ? (ri_ * g.dstride + rcv0) * 4 : OOB, 0);                   \
+        ok_ ? v_ : -0.0f;                                                                           \
+    })
+    const bool grad = rin != 0;                           // uniform: this wave has interior rows
+    float gbacc = 0.0f;
+    const size_t L = g.level;
+    const int L4 = (int)(L * 4);                          // bytes per history slot (< 2 GB: resident surveys)
+    f32x2 Q0[4], Q1[4], Q2[4], Q3[4];
+    int pr[8];                                            // history offset of (own row r, lane)
+#pragma unroll
+    for (int r = 0; r < R; ++r) pr[r] = grad ? (PT_ROFS(r) + gx) * 4 : OOB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { Q0[i] = 0.0f; Q1[i] = 0.0f; Q2[i] = 0.0f; Q3[i] = 0.0f; }
+    // history descriptor of the epoch whose first step is KN: its prefetches read slots
+    // KN - 2 .. KN - T - 1, step t at byte offset (T - 1 - t) * L4
+#define HIST_RSRC(KN) rsrc_of(a.hist + (ptrdiff_t)((KN) - T - 1) * (ptrdiff_t)L + (ptrdiff_t)so)
+    float wv[T], dv[T];
+    if (grad) {   // window of the first step k = nt: slots nt + 1, nt, nt - 1
+        const __amdgpu_buffer_rsrc_t H0 = rsrc_of(a.hist + (ptrdiff_t)(a.nt - 1) * (ptrdiff_t)L + (ptrdiff_t)so);
+        ADJR_LOAD(Q0, H0, 2 * L4)
+        ADJR_LOAD(Q1, H0, L4)
+        ADJR_LOAD(Q2, H0, 0)
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        wv[t] = a.wav[max(a.nt - t - 1, 0)];
+        dv[t] = DLOAD(a.nt - t);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+#define ADJ_ISSUE                                                                                   \
+    _Pragma("unroll") for (int t = 0; t < T; ++t) {                                                 \
+        wv[t] = a.wav[max(kn - t - 1, 0)];                                                          \
+        dv[t] = DLOAD(kn - t);                                                                      \
+    }
+    const int nep = (a.nt + T - 1) / T;
+    bool live = true;
+    unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
+    for (int e = 0; e < nep; ++e) {
+        const int ke = a.nt - e * T;                      // first step k of this epoch
+        const bool last = e + 1 == nep;
+        const __amdgpu_buffer_rsrc_t HRe = HIST_RSRC(ke);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int j = e * T + t;
+            if (j >= a.nt) break;
+            const int k = ke - t;
+            if ((t & 3) == 0) ADJR_STEP(L1, L0, Q0, Q1, Q2, Q3)
+            else if ((t & 3) == 1) ADJR_STEP(L0, L1, Q1, Q2, Q3, Q0)
+            else if ((t & 3) == 2) ADJR_STEP(L1, L0, Q2, Q3, Q0, Q1)
+            else ADJR_STEP(L0, L1, Q3, Q0, Q1, Q2)
+        }
+        if (T & 1) {   // keep "L1 = newest" at every epoch boundary
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { const f32x2 tl = L0[i]; L0[i] = L1[i]; L1[i] = tl; }
+        }
+        // the last step's window (step T - 1: Q[T-1], Q[T], Q[T+1] mod 4), for the deferred gradient
+#define QW(o) (((T - 1 + (o)) & 3) == 0 ? Q0 : ((T - 1 + (o)) & 3) == 1 ? Q1 : ((T - 1 + (o)) & 3) == 2 ? Q2 : Q3)
+        PT_PROF(tst)
+        if (!last) {
+            const unsigned tag = (unsigned)(e + 1);
+            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
+            PT_PUBLISH(GR, tag, L0, L1)
+            ADJR_GRAD(L0, L1, wv[T - 1], QW(0), QW(1), QW(2))   // the deferred last step (no neighbour data)
+            const int kn = ke - T;                        // first step k of the next epoch
+            PT_PROF(tpb)
+            PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
+            ADJ_ISSUE
+            PT_PROF(tsw)
+        }
+        if constexpr ((T & 3) != 0) {   // restore Q0 = the next epoch's P_k
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x2 a0 = QW(1)[i], a1 = QW(2)[i], a2 = QW(3)[i], a3 = QW(4)[i];
+                Q0[i] = a0; Q1[i] = a1; Q2[i] = a2; Q3[i] = a3;
+            }
+        }
+    }
+#undef QW
+#undef DLOAD
+#undef ADJ_ISSUE
+#undef HIST_RSRC
+    if (prof && lane == 0) {
+        atomicAdd(prof + 0, tsw); atomicAdd(prof + 1, tst); atomicAdd(prof + 2, tpb); atomicAdd(prof + 3, 1ull);
+        atomicAdd(prof + 4, tfp); atomicAdd(prof + 5, npass);
+        if (blockIdx.x < PROF_WAVES / 16) {
+            unsigned long long *raw = prof + PROF_RAW + ((size_t)blockIdx.x * 16 + w) * 3;   // per wave
+            raw[0] = tsw; raw[1] = tst; raw[2] = tpb;
+        }
+    }
+    double ksum = 0.0;                                    // gk = sum K * (sum_k P (L_{k+1} - L_k))
+    if (xin) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if ((rin >> r) & 1u) {
+                a.gA[so + (size_t)PT_ROFS(r) + gx] = PT_AT(GA, r);
+                const float kp = AL[3 * g.cstride + PT_ROFS(r) + gx];
+                ksum += (double)kp * (double)PT_AT(GK, r);
+            }
+    }
+    if (srow >= 0 && scol) a.gbeta[bs] = gbacc;
+    // deterministic workgroup reduction of the sponge-coefficient partial sum
+    const int tid = threadIdx.x;
+    red[tid] = ksum;
+    __syncthreads();
+    for (int w2 = 512; w2 > 0; w2 >>= 1) {
+        if (tid < w2 && tid + w2 < 64 * NW) red[tid] += red[tid + w2];
+        __syncthreads();
+    }
+    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
+}
+#undef ADJR_STEP
+#undef ADJR_GRAD
+#undef ADJR_LOAD
 #undef ADJ_STEP
 #undef ADJ_GRAD
 #undef ADJ_PLOAD
@@ -1776,10 +1978,10 @@ int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
     int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
     int *cf = NW == 12 ? p->cap_adjf12 : p->cap_adjf8;   // both adjoint variants: the launch must fit either
     switch (T) {
-    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false, false>, 64 * NW, c[1]), resident_capacity(k_adj_pt<1, NW, true, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
-    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false, false>, 64 * NW, c[2]), resident_capacity(k_adj_pt<2, NW, true, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
-    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false, false>, 64 * NW, c[3]), resident_capacity(k_adj_pt<3, NW, true, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
-    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false, false>, 64 * NW, c[4]), resident_capacity(k_adj_pt<4, NW, true, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
+    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false, false>, 64 * NW, c[1]), resident_capacity(k_adj_pr<1, NW, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
+    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false, false>, 64 * NW, c[2]), resident_capacity(k_adj_pr<2, NW, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
+    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false, false>, 64 * NW, c[3]), resident_capacity(k_adj_pr<3, NW, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
+    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false, false>, 64 * NW, c[4]), resident_capacity(k_adj_pr<4, NW, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
     }
 }
 
@@ -1868,14 +2070,15 @@ void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
 {
     const dim3 blk(64 * NW);
     if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F, true>), grid, blk, 0, st, a);
+        if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false, true>), grid, blk, 0, st, a);
         return;
     }
     switch (T) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, F, false>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, F, false>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, F, false>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, F, false>), grid, blk, 0, st, a); break;
+    case 1: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<1, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, false, false>), grid, blk, 0, st, a); break;
+    case 2: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<2, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, false, false>), grid, blk, 0, st, a); break;
+    case 3: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<3, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, false, false>), grid, blk, 0, st, a); break;
+    default: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false, false>), grid, blk, 0, st, a); break;
     }
 }
 

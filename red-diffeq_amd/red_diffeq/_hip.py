@@ -11,8 +11,6 @@ import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libred_diffeq_hip.so")
-if os.environ.get("RDQ_EXP_LIB"):        # timing experiments only (tools/exp_variants.sh)
-    LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "exp", os.environ["RDQ_EXP_LIB"])
 
 c_int32, c_int64, c_float, c_double, c_size_t, c_void_p = (
     ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)

@@ -52,8 +52,7 @@ for T, G in cfgs:
             fw.append(ev[0].elapsed_time(ev[1]))
             ad.append(ev[1].elapsed_time(ev[2]))
         del hist
-    if not os.environ.get("RDQ_EXP_LIB"):
-        plan.status()
+    plan.status()
     fw, ad = sorted(fw)[len(fw) // 2], sorted(ad)[len(ad) // 2]
     res.append({"T": T, "persistent": G, "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
                 "shot_ts_per_s": round(a.ns * a.nt * a.B / ((fw + ad) * 1e-3))})
