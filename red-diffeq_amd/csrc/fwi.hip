@@ -1095,21 +1095,14 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
             s2.x = s2.x + dpp_shr1(xl1.x); s2.y = s2.y + dpp_shr1(xl1.y);                           \
             s2.x = s2.x + dpp_shl1(xr1.x); s2.y = s2.y + dpp_shl1(xr1.y);                           \
             const f32x2 l = LN[i];                                                                  \
-            if constexpr (FMA) {                                                                    \
-                const f32x2 lap = fma2(kC3, s2, kC2 * s1);                                          \
-                const f32x2 d = fma2(kC1X2, c, lap);                                                \
-                GA[i] = fma2(l, d, GA[i]);                                                          \
-                GK[i] = fma2(c, CU[i] - l, GK[i]);                                                  \
-            } else {                                                                                \
-                f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;                    \
-                f32x2 d = kC1X2 * c; d = d + lap;                                                   \
-                const f32x2 cc = l * d;                                                             \
-                GA[i] = GA[i] + cc;                                                                 \
-                f32x2 kk = KP[i] * c; const f32x2 dl = CU[i] - l; kk = kk * dl;                     \
-                if (xin) {                                                                          \
-                    if ((rin >> i) & 1u) ksum += (double)kk.x;                                      \
-                    if ((rin >> (i + 4)) & 1u) ksum += (double)kk.y;                                \
-                }                                                                                   \
+            f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;                        \
+            f32x2 d = kC1X2 * c; d = d + lap;                                                       \
+            const f32x2 cc = l * d;                                                                 \
+            GA[i] = GA[i] + cc;                                                                     \
+            f32x2 kk = KP[i] * c; const f32x2 dl = CU[i] - l; kk = kk * dl;   /* fp32 term */       \
+            if (xin) {                                                       /* fp64 sum */        \
+                if ((rin >> i) & 1u) ksum += (double)kk.x;                                          \
+                if ((rin >> (i + 4)) & 1u) ksum += (double)kk.y;                                    \
             }                                                                                       \
         }                                                                                           \
         if (srow >= 0) {                             /* gbeta: the source cell's lane only */      \
@@ -1142,14 +1135,9 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
             f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
             n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
             n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
-            if constexpr (FMA) {                                                                    \
-                const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                           \
-                PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                           \
-            } else {                                                                                \
-                f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;                     \
-                f32x2 l = T1v[i] * CUR[i]; const f32x2 l2 = T2v[i] * PRV[i]; l = l - l2; l = l + nb; \
-                PRV[i] = l;                                                                         \
-            }                                                                                       \
+            f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;                         \
+            f32x2 l = T1v[i] * CUR[i]; const f32x2 l2 = T2v[i] * PRV[i]; l = l - l2; l = l + nb;     \
+            PRV[i] = l;                                                                             \
         }                                                                                           \
         if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
             int rr_ = rrow;                                                                         \
@@ -1160,7 +1148,8 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
         if (t + 1 < T || last) ADJ_GRAD(CUR, PRV, P, PH, wv[t])                                     \
     }
 
-// Adjoint, persistent.  Per step k = nt..1:
+// Adjoint, persistent, in the oracle's exact fp32 operation order (rdq_fwi_set_variant flag 2: the
+// bitwise tests; the default build is k_adj_pr below).  Per step k = nt..1:
 //   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
 //   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k),
 //   gbeta[s] += L_k(src) w[k-1]        (interior cells; accumulators in registers for all nt steps)
@@ -1169,7 +1158,7 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
 // border, then the LAST step's gradient (it needs no neighbour data: the interior L_k, L_{k+1} and
 // the wave's own history rows), and only then the hand-off sweep — the gradient's VALU work fills
 // the time the neighbours' granules take to arrive.
-template <int T, int NW, bool FMA, bool PROF>
+template <int T, int NW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
@@ -1178,7 +1167,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[4], T1v[4], T2v[4], KP[4], L0[4], L1[4], GA[4], GK[4];
+    f32x2 A[4], T1v[4], T2v[4], KP[4], L0[4], L1[4], GA[4];
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2};
     int srow = -1, rrow = -1;
 #pragma unroll
@@ -1186,9 +1175,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         const int gz = wrap_row(uz0 + r, g.Hp);
         const int o = gz * g.ld + gx;
         PT_AT(A, r) = AL[o]; PT_AT(T1v, r) = AL[g.cstride + o]; PT_AT(T2v, r) = AL[2 * g.cstride + o];
-        if constexpr (!FMA) PT_AT(KP, r) = AL[3 * g.cstride + o];
+        PT_AT(KP, r) = AL[3 * g.cstride + o];
         PT_AT(L0, r) = 0.0f; PT_AT(L1, r) = 0.0f;         // L_{nt+1} = L_{nt+2} = 0
-        PT_AT(GA, r) = 0.0f; PT_AT(GK, r) = 0.0f;
+        PT_AT(GA, r) = 0.0f;
         if (gz == g.isz && ((rin >> r) & 1u)) srow = r;
         if (gz == g.igz) rrow = r;
     }
@@ -1297,16 +1286,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             if ((rin >> r) & 1u) a.gA[so + (size_t)PT_ROFS(r) + gx] = PT_AT(GA, r);
     }
     if (srow >= 0 && scol) a.gbeta[bs] = gbacc;
-    if constexpr (FMA) {   // gk = sum K * (sum_k P (L_{k+1} - L_k)) over the own cells
-        if (xin) {
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if ((rin >> r) & 1u) {
-                    const float kp = AL[3 * g.cstride + PT_ROFS(r) + gx];
-                    ksum += (double)kp * (double)PT_AT(GK, r);
-                }
-        }
-    }
     // deterministic workgroup reduction of the sponge-coefficient partial sum
     const int tid = threadIdx.x;
     red[tid] = ksum;
@@ -1978,10 +1957,10 @@ int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
     int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
     int *cf = NW == 12 ? p->cap_adjf12 : p->cap_adjf8;   // both adjoint variants: the launch must fit either
     switch (T) {
-    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false, false>, 64 * NW, c[1]), resident_capacity(k_adj_pr<1, NW, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
-    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false, false>, 64 * NW, c[2]), resident_capacity(k_adj_pr<2, NW, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
-    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false, false>, 64 * NW, c[3]), resident_capacity(k_adj_pr<3, NW, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
-    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false, false>, 64 * NW, c[4]), resident_capacity(k_adj_pr<4, NW, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
+    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false>, 64 * NW, c[1]), resident_capacity(k_adj_pr<1, NW, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
+    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false>, 64 * NW, c[2]), resident_capacity(k_adj_pr<2, NW, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
+    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false>, 64 * NW, c[3]), resident_capacity(k_adj_pr<3, NW, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
+    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false>, 64 * NW, c[4]), resident_capacity(k_adj_pr<4, NW, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
     }
 }
 
@@ -2071,14 +2050,14 @@ void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
     const dim3 blk(64 * NW);
     if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
         if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, true>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, true>), grid, blk, 0, st, a);
         return;
     }
     switch (T) {
-    case 1: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<1, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, false, false>), grid, blk, 0, st, a); break;
-    case 2: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<2, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, false, false>), grid, blk, 0, st, a); break;
-    case 3: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<3, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, false, false>), grid, blk, 0, st, a); break;
-    default: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false, false>), grid, blk, 0, st, a); break;
+    case 1: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<1, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, false>), grid, blk, 0, st, a); break;
+    case 2: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<2, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, false>), grid, blk, 0, st, a); break;
+    case 3: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<3, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, false>), grid, blk, 0, st, a); break;
+    default: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false>), grid, blk, 0, st, a); break;
     }
 }
 

@@ -10,6 +10,7 @@ import math
 import torch
 
 from .. import _hip
+from .. import ops  # noqa: F401  (registers torch.ops.red_diffeq.*)
 
 
 class CosineLR:
@@ -72,14 +73,7 @@ class FusedAdamClamp:
 
 
 def metrics(pred, true_norm):
-    """(mae, rmse, ssim) per model, (3, B) float32 on the device, no host sync."""
+    """(mae, rmse, ssim) per model, (3, B) float32 on the device, no host sync
+    (torch.ops.red_diffeq.metrics, K12)."""
     _hip.require_device(pred)
-    B, _, H, W = pred.shape
-    t = true_norm.contiguous()
-    L = _hip.lib()
-    ws = torch.empty(int(L.rdq_metrics_ws_bytes(B, H, W)), dtype=torch.uint8, device=pred.device)
-    out = torch.empty(3, B, dtype=torch.float32, device=pred.device)
-    strides = (ctypes.c_int64 * 4)(*pred.stride())
-    _hip.check(L.rdq_metrics(B, H, W, _hip.ptr(pred), strides, _hip.ptr(t), _hip.ptr(out), _hip.ptr(ws),
-                             _hip.stream_of(pred)), "rdq_metrics")
-    return out
+    return torch.ops.red_diffeq.metrics(pred, true_norm)

@@ -4,44 +4,29 @@ from typing import Optional
 import torch
 
 from .. import _hip
+from .. import ops  # noqa: F401  (registers torch.ops.red_diffeq.*)
 from ..regularization.base import RegularizationMethod
 
 
 class _L1Misfit(torch.autograd.Function):
-    """Per-model masked L1 misfit: forward rdq_l1_forward, backward rdq_l1_backward
-    (dpred = sign(pred - y) * mask * gout / nobs, exactly the autograd of losses.py:27-39)."""
+    """Per-model masked L1 misfit: forward torch.ops.red_diffeq.l1_misfit (K5), backward
+    l1_misfit_backward (dpred = sign(pred - y) * mask * gout / nobs, exactly the autograd of
+    losses.py:27-39).  nobs_override: the global observation count of a shot-sharded survey."""
 
     @staticmethod
     def forward(ctx, pred, y, mask, nobs_override):
         _hip.require_device(pred, y, mask)
-        pred = pred.float().contiguous()
-        y = y.float().contiguous()
-        mask = None if mask is None else mask.float().contiguous()
-        B = pred.shape[0]
-        n = pred.numel() // B
-        L = _hip.lib()
-        loss = torch.empty(B, dtype=torch.float32, device=pred.device)
-        nobs = torch.empty(B, dtype=torch.float32, device=pred.device)
-        part = torch.empty(int(L.rdq_l1_partial_bytes(B, n)), dtype=torch.uint8, device=pred.device)
-        _hip.check(L.rdq_l1_forward(B, n, _hip.ptr(pred), _hip.ptr(y), _hip.ptr(mask), _hip.ptr(loss),
-                                    _hip.ptr(nobs), _hip.ptr(part), _hip.stream_of(pred)), "rdq_l1_forward")
+        loss, nobs = torch.ops.red_diffeq.l1_misfit(pred, y, mask)
         if nobs_override is not None:          # shot-parallel: normalise by the global count
             loss = loss * (nobs / nobs_override)
             nobs = nobs_override.float().contiguous()
         ctx.save_for_backward(pred, y, mask, nobs)
-        ctx.n = n
         return loss
 
     @staticmethod
     def backward(ctx, gout):
         pred, y, mask, nobs = ctx.saved_tensors
-        B = pred.shape[0]
-        dpred = torch.empty_like(pred)
-        gout = gout.float().contiguous()
-        _hip.check(_hip.lib().rdq_l1_backward(B, ctx.n, _hip.ptr(pred), _hip.ptr(y), _hip.ptr(mask),
-                                              _hip.ptr(nobs), _hip.ptr(gout), _hip.ptr(dpred),
-                                              _hip.stream_of(pred)), "rdq_l1_backward")
-        return dpred, None, None, None
+        return torch.ops.red_diffeq.l1_misfit_backward(pred, y, mask, nobs, gout), None, None, None
 
 
 def l1_misfit(predicted, target, mask=None, nobs=None):

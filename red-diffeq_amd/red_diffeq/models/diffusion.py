@@ -251,8 +251,19 @@ class Unet(nn.Module):
         with ops.precision(self.precision):
             return self._forward(x, time, x_self_cond)
 
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .float() may move or replace the parameters: captured graphs hold the
+        # old addresses, so bump the weights generation (the graph cache key)
+        self._wgen = getattr(self, "_wgen", 0) + 1
+        return super()._apply(fn, *args, **kwargs)
+
     def _weights_version(self):
-        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+        """Graph-cache key of the weights.  A replay reads the parameters' live storage, so in-place
+        updates (optimizer steps, load_state_dict) need no recapture in fp32; the bf16 path reads
+        packed copies, so there the parameters' version counters are part of the key."""
+        if self.precision == "bf16":
+            return (getattr(self, "_wgen", 0), tuple(p._version for p in self.parameters()))
+        return getattr(self, "_wgen", 0)
 
     def _graphed(self, x, time):
         key = (tuple(x.shape), x.dtype, x.device, self.precision, time.dtype)

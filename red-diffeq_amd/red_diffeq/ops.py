@@ -1,0 +1,543 @@
+"""PyTorch custom operators over the C ABI (torch.ops.red_diffeq.*).
+
+Every HIP entry point the product path uses is registered with torch.library: a schema, the
+ROCm implementation (the ctypes call into libred_diffeq_hip.so on the tensor's current stream), a
+fake (meta) implementation giving output shapes without running anything, and for the FWI
+operator an autograd formula whose backward is the hand-written adjoint.  The ops are
+functional (fresh outputs, no input mutation), so torch.library.opcheck, FakeTensor tracing and
+torch.compile see them as ordinary operators instead of opaque ctypes calls.
+
+  FWI (include/red_diffeq_fwi.h; a plan is referred to by an integer handle, FwiPlan.op_id)
+    red_diffeq::fwi_coeffs(v, plan, vel_mode) -> (coeffs, vstat)                   K3
+    red_diffeq::fwi_forward(coeffs, plan, B, keep_history) -> (seis, history)      K1
+    red_diffeq::fwi_adjoint(coeffs, history, dseis, plan, B) -> (gA, gk, gbeta)    K2
+    red_diffeq::fwi_grad_finalize(coeffs, vstat, gA, gk, gbeta, plan, B, vel_mode) -> grad   K4
+    red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
+        differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
+  U-Net (include/red_diffeq_unet.h)
+    conv2d_mfma, gn_silu, rmsnorm, linear, sinusoidal_emb, linear_attn, attn, red_q_sample, red_eps
+  loop (include/red_diffeq_loop.h)
+    l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
+
+No CPU implementation is registered: a CPU tensor reaching an op raises (no fallback).
+"""
+import ctypes
+import weakref
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+from torch.utils.weak import WeakIdKeyDictionary
+
+from . import _hip
+
+LIB = "red_diffeq"
+_PLANS = {}           # op handle -> weakref(FwiPlan); FwiPlan.__del__ unregisters
+
+
+def register_plan(plan):
+    h = id(plan)
+    _PLANS[h] = weakref.ref(plan)
+    return h
+
+
+def unregister_plan(h):
+    _PLANS.pop(h, None)
+
+
+def _plan(h):
+    ref = _PLANS.get(int(h))
+    p = ref() if ref is not None else None
+    if p is None:
+        raise RuntimeError(f"red_diffeq: unknown FWI plan handle {h}")
+    return p
+
+
+def _f32(n, dev):
+    return torch.empty(int(n) // 4, dtype=torch.float32, device=dev)
+
+
+# ------------------------------------------------------------------------------------------ FWI
+@torch.library.custom_op(f"{LIB}::fwi_coeffs", mutates_args=())
+def fwi_coeffs(v: Tensor, plan: int, vel_mode: int) -> Tuple[Tensor, Tensor]:
+    p = _plan(plan)
+    _hip.require_device(v)
+    B = v.shape[0]
+    sz = p.sizes(B)
+    coeffs = _f32(sz.coeffs, v.device)
+    vstat = torch.empty(int(sz.vstat), dtype=torch.uint8, device=v.device)
+    strides = (ctypes.c_int64 * 4)(*v.stride())
+    _hip.check(p.lib.rdq_fwi_coeffs(p.handle, B, _hip.ptr(v), strides, vel_mode, _hip.ptr(coeffs), _hip.ptr(vstat),
+                                    _hip.stream_of(v)), "rdq_fwi_coeffs")
+    return coeffs, vstat
+
+
+@fwi_coeffs.register_fake
+def _(v, plan, vel_mode):
+    sz = _plan(plan).sizes(v.shape[0])
+    return (v.new_empty(int(sz.coeffs) // 4, dtype=torch.float32),
+            v.new_empty(int(sz.vstat), dtype=torch.uint8))
+
+
+def _seis_shape(p, B):
+    return (B, p.ns, p.sizes(B).nrec, p.ng)
+
+
+@torch.library.custom_op(f"{LIB}::fwi_forward", mutates_args=())
+def fwi_forward(coeffs: Tensor, plan: int, B: int, keep_history: bool) -> Tuple[Tensor, Tensor]:
+    p = _plan(plan)
+    _hip.require_device(coeffs)
+    sz = p.sizes(B)
+    seis = torch.empty(_seis_shape(p, B), dtype=torch.float32, device=coeffs.device)
+    hist = _f32(sz.history if keep_history else 0, coeffs.device)
+    ring = _f32(sz.ring, coeffs.device)
+    _hip.check(p.lib.rdq_fwi_forward(p.handle, B, _hip.ptr(coeffs), _hip.ptr(seis),
+                                     _hip.ptr(hist) if keep_history else ctypes.c_void_p(0), _hip.ptr(ring),
+                                     _hip.stream_of(coeffs)), "rdq_fwi_forward")
+    return seis, hist
+
+
+@fwi_forward.register_fake
+def _(coeffs, plan, B, keep_history):
+    p = _plan(plan)
+    sz = p.sizes(B)
+    return (coeffs.new_empty(_seis_shape(p, B)),
+            coeffs.new_empty(int(sz.history) // 4 if keep_history else 0))
+
+
+@torch.library.custom_op(f"{LIB}::fwi_adjoint", mutates_args=())
+def fwi_adjoint(coeffs: Tensor, history: Tensor, dseis: Tensor, plan: int, B: int) -> Tuple[Tensor, Tensor, Tensor]:
+    p = _plan(plan)
+    _hip.require_device(coeffs, history, dseis)
+    sz = p.sizes(B)
+    if dseis.shape != _seis_shape(p, B) or history.numel() * 4 != sz.history:
+        raise ValueError("fwi_adjoint: dseis / history do not match the plan")
+    dseis = dseis.float().contiguous()
+    ring = _f32(sz.ring, coeffs.device)
+    gA = _f32(sz.gA, coeffs.device)
+    gk = torch.empty(int(sz.gk_part) // 8, dtype=torch.float64, device=coeffs.device)
+    gb = _f32(sz.gbeta, coeffs.device)
+    _hip.check(p.lib.rdq_fwi_adjoint(p.handle, B, _hip.ptr(coeffs), _hip.ptr(history), _hip.ptr(dseis),
+                                     _hip.ptr(ring), _hip.ptr(gA), _hip.ptr(gk), _hip.ptr(gb),
+                                     _hip.stream_of(coeffs)), "rdq_fwi_adjoint")
+    return gA, gk, gb
+
+
+@fwi_adjoint.register_fake
+def _(coeffs, history, dseis, plan, B):
+    sz = _plan(plan).sizes(B)
+    return (coeffs.new_empty(int(sz.gA) // 4), coeffs.new_empty(int(sz.gk_part) // 8, dtype=torch.float64),
+            coeffs.new_empty(int(sz.gbeta) // 4))
+
+
+@torch.library.custom_op(f"{LIB}::fwi_grad_finalize", mutates_args=())
+def fwi_grad_finalize(coeffs: Tensor, vstat: Tensor, gA: Tensor, gk: Tensor, gbeta: Tensor, plan: int, B: int,
+                      vel_mode: int) -> Tensor:
+    p = _plan(plan)
+    _hip.require_device(coeffs, gA)
+    sz = p.sizes(B)
+    colsum = torch.empty(int(sz.colsum) // 8, dtype=torch.float64, device=coeffs.device)
+    out = torch.empty(B, 1, p.nz, p.nx, dtype=torch.float32, device=coeffs.device)
+    _hip.check(p.lib.rdq_fwi_grad_finalize(p.handle, B, _hip.ptr(coeffs), _hip.ptr(vstat), _hip.ptr(gA), _hip.ptr(gk),
+                                           _hip.ptr(gbeta), vel_mode, _hip.ptr(colsum), _hip.ptr(out),
+                                           _hip.stream_of(coeffs)), "rdq_fwi_grad_finalize")
+    return out
+
+
+@fwi_grad_finalize.register_fake
+def _(coeffs, vstat, gA, gk, gbeta, plan, B, vel_mode):
+    p = _plan(plan)
+    return coeffs.new_empty(B, 1, p.nz, p.nx)
+
+
+@torch.library.custom_op(f"{LIB}::fwi", mutates_args=())
+def fwi(v: Tensor, plan: int, vel_mode: int, keep_history: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """seis = FWM(v) (K3 + K1); coeffs / vstat / history are returned for the backward."""
+    coeffs, vstat = fwi_coeffs(v, plan, vel_mode)
+    seis, hist = fwi_forward(coeffs, plan, v.shape[0], keep_history)
+    return seis, coeffs, vstat, hist
+
+
+@fwi.register_fake
+def _(v, plan, vel_mode, keep_history):
+    coeffs, vstat = _fake_coeffs(v, plan)
+    seis, hist = _fake_forward(coeffs, plan, v.shape[0], keep_history)
+    return seis, coeffs, vstat, hist
+
+
+def _fake_coeffs(v, plan):
+    sz = _plan(plan).sizes(v.shape[0])
+    return v.new_empty(int(sz.coeffs) // 4, dtype=torch.float32), v.new_empty(int(sz.vstat), dtype=torch.uint8)
+
+
+def _fake_forward(coeffs, plan, B, keep_history):
+    p = _plan(plan)
+    sz = p.sizes(B)
+    return coeffs.new_empty(_seis_shape(p, B)), coeffs.new_empty(int(sz.history) // 4 if keep_history else 0)
+
+
+def _fwi_setup(ctx, inputs, output):
+    v, plan, vel_mode, keep_history = inputs
+    _, coeffs, vstat, hist = output
+    if not keep_history:
+        ctx.plan = None
+        return
+    ctx.plan, ctx.vel_mode, ctx.B = plan, vel_mode, v.shape[0]
+    ctx.coeffs, ctx.vstat, ctx.hist = coeffs, vstat, hist
+
+
+def _fwi_backward(ctx, gseis, _gc, _gv, _gh):
+    if ctx.plan is None:
+        raise RuntimeError("red_diffeq::fwi was called with keep_history=False; no gradient is available")
+    gA, gk, gb = fwi_adjoint(ctx.coeffs, ctx.hist, gseis.contiguous(), ctx.plan, ctx.B)
+    ctx.hist = None                     # the largest buffer: released as soon as the adjoint has run
+    g = fwi_grad_finalize(ctx.coeffs, ctx.vstat, gA, gk, gb, ctx.plan, ctx.B, ctx.vel_mode)
+    return g, None, None, None
+
+
+fwi.register_autograd(_fwi_backward, setup_context=_fwi_setup)
+
+
+# ---------------------------------------------------------------------------------------- U-Net
+# bf16 weight packs, cached per weight TENSOR (weak keys: an entry dies with its tensor, so a new
+# tensor at a recycled address never sees a stale pack) and per (version, input split)
+_BF16_PACKS = WeakIdKeyDictionary()
+
+
+def _conv_desc(x, x2, weight, pad, mode):
+    cout, cin, kh, kw = weight.shape
+    if mode == 1:
+        H, W = x.shape[2] * 2, x.shape[3] * 2
+    elif mode == 2:
+        H, W = x.shape[2] // 2, x.shape[3] // 2
+    else:
+        H, W = x.shape[2], x.shape[3]
+    cin1 = x.shape[1] * (4 if mode == 2 else 1)
+    cin2 = x2.shape[1] if x2 is not None else 0
+    if cin1 + cin2 != cin:
+        raise ValueError(f"conv expects {cin} input channels, got {cin1}+{cin2}")
+    return _hip.ConvDesc(B=x.shape[0], cin1=cin1, cin2=cin2, H=H, W=W, cout=cout, kh=kh, kw=kw, pad=pad,
+                         in_mode=mode), (x.shape[0], cout, H, W)
+
+
+def _bf16_pack(weight, d, stream):
+    per = _BF16_PACKS.setdefault(weight, {})
+    key = (weight._version, d.cin1, d.cin2)
+    wp = per.get(key)
+    if wp is None:
+        per.clear()                      # older versions of this tensor are dead
+        L = _hip.lib()
+        wp = torch.empty(int(L.rdq_conv2d_bf16_wpack_bytes(ctypes.byref(d))), dtype=torch.uint8, device=weight.device)
+        _hip.check(L.rdq_conv2d_bf16_pack(ctypes.byref(d), _hip.ptr(weight.contiguous()), _hip.ptr(wp), stream),
+                   "rdq_conv2d_bf16_pack")
+        per[key] = wp
+    return wp
+
+
+def clear_bf16_packs():
+    """Drop the cached bf16 weight packs: needed after in-place updates through `.data`, which do
+    not bump a tensor's version counter."""
+    _BF16_PACKS.clear()
+
+
+def bf16_eligible(weight):
+    cout, cin, kh, kw = weight.shape
+    return cin * kh * kw >= 64 and cout >= 16
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_mfma", mutates_args=())
+def conv2d_mfma(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], residual: Optional[Tensor],
+                pad: int, mode: int, bf16: bool) -> Tensor:
+    """nn.Conv2d (stride 1) of the logical input cat(x', x2), x' = x | upsample2(x) | unshuffle2(x)
+    (mode 0 / 1 / 2), + bias + residual; fp32 MFMA, or bf16 operands with fp32 accumulation."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    d, shape = _conv_desc(x, x2, weight, pad, mode)
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    res = residual.contiguous() if residual is not None else None
+    L = _hip.lib()
+    st = _hip.stream_of(x)
+    if bf16 and bf16_eligible(weight):
+        wp = _bf16_pack(weight, d, st)
+        nws = int(L.rdq_conv2d_bf16_ws_bytes(ctypes.byref(d)))
+        ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+        _hip.check(L.rdq_conv2d_bf16(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(wp), _hip.ptr(bias),
+                                     _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, st), "rdq_conv2d_bf16")
+        return y
+    nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+    _hip.check(L.rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(weight.contiguous()), _hip.ptr(bias),
+                            _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, st), "rdq_conv2d")
+    return y
+
+
+@conv2d_mfma.register_fake
+def _(x, x2, weight, bias, residual, pad, mode, bf16):
+    _, shape = _conv_desc(x, x2, weight, pad, mode)
+    return x.new_empty(shape)
+
+
+@torch.library.custom_op(f"{LIB}::gn_silu", mutates_args=())
+def gn_silu(x: Tensor, weight: Tensor, bias: Tensor, scale_shift: Optional[Tensor], groups: int, eps: float) -> Tensor:
+    """GroupNorm(groups) -> x * (scale + 1) + shift -> SiLU; scale_shift (B, 2C), scale first."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    L = _hip.lib()
+    ws = torch.empty(max(8, int(L.rdq_group_norm_ws_bytes(B, C, H * W, groups))), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    _hip.check(L.rdq_group_norm_silu(B, C, H * W, groups, float(eps), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(bias),
+                                     _hip.ptr(ss), _hip.ptr(y), _hip.ptr(ws), _hip.stream_of(x)), "rdq_group_norm_silu")
+    return y
+
+
+@gn_silu.register_fake
+def _(x, weight, bias, scale_shift, groups, eps):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op(f"{LIB}::rmsnorm", mutates_args=())
+def rmsnorm(x: Tensor, g: Tensor, residual: Optional[Tensor]) -> Tensor:
+    """F.normalize(x, dim=1) * g * sqrt(C) [+ residual]."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = torch.empty_like(x)
+    res = residual.contiguous() if residual is not None else None
+    _hip.check(_hip.lib().rdq_rmsnorm(B, C, H * W, _hip.ptr(x), _hip.ptr(g), _hip.ptr(res), _hip.ptr(y),
+                                      _hip.stream_of(x)), "rdq_rmsnorm")
+    return y
+
+
+@rmsnorm.register_fake
+def _(x, g, residual):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op(f"{LIB}::linear", mutates_args=())
+def linear(x: Tensor, weight: Tensor, bias: Tensor, act_in: int, act_out: int) -> Tensor:
+    """act_out(Linear(act_in(x))); act 1 = SiLU on the input / GELU(erf) on the output."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    B, fin = x.shape
+    fout = weight.shape[0]
+    y = torch.empty(B, fout, device=x.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_linear(B, fin, fout, _hip.ptr(x), _hip.ptr(weight), _hip.ptr(bias), act_in, act_out,
+                                     _hip.ptr(y), _hip.stream_of(x)), "rdq_linear")
+    return y
+
+
+@linear.register_fake
+def _(x, weight, bias, act_in, act_out):
+    return x.new_empty(x.shape[0], weight.shape[0])
+
+
+@torch.library.custom_op(f"{LIB}::sinusoidal_emb", mutates_args=())
+def sinusoidal_emb(t: Tensor, dim: int, theta: float) -> Tensor:
+    _hip.require_device(t)
+    t = t.to(torch.int64).contiguous()
+    y = torch.empty(t.shape[0], dim, device=t.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_sinusoidal_emb(t.shape[0], dim, float(theta), _hip.ptr(t), _hip.ptr(y),
+                                             _hip.stream_of(t)), "rdq_sinusoidal_emb")
+    return y
+
+
+@sinusoidal_emb.register_fake
+def _(t, dim, theta):
+    return t.new_empty(t.shape[0], dim, dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::linear_attn", mutates_args=())
+def linear_attn(qkv: Tensor, mem_kv: Tensor, heads: int, scale: float) -> Tensor:
+    """LinearAttention core (diffusion.py:182-195): softmax(q) over d, softmax(k) over n with the
+    memory key/values, context, out = context^T q; qkv (B, 3*heads*dh, H, W) -> (B, heads*dh, H, W)."""
+    _hip.require_device(qkv)
+    qkv = qkv.contiguous()
+    B, C3, H, W = qkv.shape
+    dh = C3 // (3 * heads)
+    L = _hip.lib()
+    ws = torch.empty(int(L.rdq_linear_attention_ws_bytes(B, heads, dh, H * W, mem_kv.shape[-1])), dtype=torch.uint8,
+                     device=qkv.device)
+    out = torch.empty(B, heads * dh, H, W, device=qkv.device, dtype=torch.float32)
+    _hip.check(L.rdq_linear_attention(B, heads, dh, H * W, mem_kv.shape[-1], float(scale), _hip.ptr(qkv),
+                                      _hip.ptr(mem_kv.contiguous()), _hip.ptr(out), _hip.ptr(ws), _hip.stream_of(qkv)),
+               "rdq_linear_attention")
+    return out
+
+
+@linear_attn.register_fake
+def _(qkv, mem_kv, heads, scale):
+    B, C3, H, W = qkv.shape
+    return qkv.new_empty(B, C3 // 3, H, W)
+
+
+@torch.library.custom_op(f"{LIB}::attn", mutates_args=())
+def attn(qkv: Tensor, mem_kv: Tensor, heads: int) -> Tensor:
+    """Attention core with Attend(flash=False) (diffusion.py:209-218): softmax(q k^T d^-1/2) v over
+    the memory + image keys; qkv (B, 3*heads*dh, H, W) -> (B, heads*dh, H, W)."""
+    _hip.require_device(qkv)
+    qkv = qkv.contiguous()
+    B, C3, H, W = qkv.shape
+    dh = C3 // (3 * heads)
+    out = torch.empty(B, heads * dh, H, W, device=qkv.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_full_attention(B, heads, dh, H * W, mem_kv.shape[-2], _hip.ptr(qkv),
+                                             _hip.ptr(mem_kv.contiguous()), _hip.ptr(out), _hip.stream_of(qkv)),
+               "rdq_full_attention")
+    return out
+
+
+@attn.register_fake
+def _(qkv, mem_kv, heads):
+    B, C3, H, W = qkv.shape
+    return qkv.new_empty(B, C3 // 3, H, W)
+
+
+@torch.library.custom_op(f"{LIB}::red_q_sample", mutates_args=())
+def red_q_sample(x0: Tensor, t: Tensor, eps: Tensor, sqrt_ac: Tensor, sqrt_1mac: Tensor) -> Tensor:
+    """q_sample (diffusion.py:516-519) on the fp32 schedule buffers."""
+    _hip.require_device(x0)
+    x0, eps = x0.contiguous(), eps.contiguous()
+    xt = torch.empty_like(x0)
+    _hip.check(_hip.lib().rdq_red_q_sample(x0.shape[0], x0[0].numel(), _hip.ptr(sqrt_ac), _hip.ptr(sqrt_1mac),
+                                           _hip.ptr(t), _hip.ptr(x0), _hip.ptr(eps), _hip.ptr(xt),
+                                           _hip.stream_of(x0)), "rdq_red_q_sample")
+    return xt
+
+
+@red_q_sample.register_fake
+def _(x0, t, eps, sqrt_ac, sqrt_1mac):
+    return torch.empty_like(x0)
+
+
+@torch.library.custom_op(f"{LIB}::red_eps", mutates_args=())
+def red_eps(xt: Tensor, t: Tensor, eps_hat: Tensor, eps: Tensor, sqrt_recip_ac: Tensor,
+            sqrt_recipm1_ac: Tensor) -> Tensor:
+    """RED residual (eps' - eps): eps' re-derived from the clipped x0 (diffusion.py:393-419)."""
+    _hip.require_device(xt)
+    xt, eps_hat, eps = xt.contiguous(), eps_hat.contiguous(), eps.contiguous()
+    g = torch.empty_like(xt)
+    _hip.check(_hip.lib().rdq_red_epilogue(xt.shape[0], xt[0].numel(), _hip.ptr(sqrt_recip_ac),
+                                           _hip.ptr(sqrt_recipm1_ac), _hip.ptr(t), _hip.ptr(xt), _hip.ptr(eps_hat),
+                                           _hip.ptr(eps), _hip.ptr(g), _hip.stream_of(xt)), "rdq_red_epilogue")
+    return g
+
+
+@red_eps.register_fake
+def _(xt, t, eps_hat, eps, sqrt_recip_ac, sqrt_recipm1_ac):
+    return torch.empty_like(xt)
+
+
+# ----------------------------------------------------------------------------------------- loop
+@torch.library.custom_op(f"{LIB}::l1_misfit", mutates_args=())
+def l1_misfit(pred: Tensor, y: Tensor, mask: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
+    """K5: per-model sum(|y - pred| * mask) / max(#observed, 1) (losses.py:14-41) -> (loss, nobs)."""
+    _hip.require_device(pred, y, mask)
+    pred, y = pred.float().contiguous(), y.float().contiguous()
+    mask = mask.float().contiguous() if mask is not None else None
+    B = pred.shape[0]
+    n = pred.numel() // B
+    L = _hip.lib()
+    loss = torch.empty(B, dtype=torch.float32, device=pred.device)
+    nobs = torch.empty(B, dtype=torch.float32, device=pred.device)
+    part = torch.empty(int(L.rdq_l1_partial_bytes(B, n)), dtype=torch.uint8, device=pred.device)
+    _hip.check(L.rdq_l1_forward(B, n, _hip.ptr(pred), _hip.ptr(y), _hip.ptr(mask), _hip.ptr(loss), _hip.ptr(nobs),
+                                _hip.ptr(part), _hip.stream_of(pred)), "rdq_l1_forward")
+    return loss, nobs
+
+
+@l1_misfit.register_fake
+def _(pred, y, mask):
+    return pred.new_empty(pred.shape[0]), pred.new_empty(pred.shape[0])
+
+
+@torch.library.custom_op(f"{LIB}::l1_misfit_backward", mutates_args=())
+def l1_misfit_backward(pred: Tensor, y: Tensor, mask: Optional[Tensor], nobs: Tensor, gout: Tensor) -> Tensor:
+    """dL/dpred = sign(pred - y) * mask * gout / nobs (the autograd of losses.py:27-39)."""
+    _hip.require_device(pred, y)
+    pred, y = pred.float().contiguous(), y.float().contiguous()
+    mask = mask.float().contiguous() if mask is not None else None
+    B = pred.shape[0]
+    dpred = torch.empty_like(pred)
+    _hip.check(_hip.lib().rdq_l1_backward(B, pred.numel() // B, _hip.ptr(pred), _hip.ptr(y), _hip.ptr(mask),
+                                          _hip.ptr(nobs.float().contiguous()), _hip.ptr(gout.float().contiguous()),
+                                          _hip.ptr(dpred), _hip.stream_of(pred)), "rdq_l1_backward")
+    return dpred
+
+
+@l1_misfit_backward.register_fake
+def _(pred, y, mask, nobs, gout):
+    return torch.empty_like(pred, dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::smooth_reg", mutates_args=())
+def smooth_reg(mu: Tensor, kind: int) -> Tensor:
+    """K6: TV (kind 0) / Tikhonov (kind 1) per model on the padded model (benchmark.py:4-37)."""
+    _hip.require_device(mu)
+    m = mu.float().contiguous()
+    B, _, H, W = m.shape
+    loss = torch.empty(B, dtype=torch.float32, device=m.device)
+    _hip.check(_hip.lib().rdq_smooth_reg_forward(kind, B, H, W, _hip.ptr(m), _hip.ptr(loss), _hip.stream_of(m)),
+               "rdq_smooth_reg_forward")
+    return loss
+
+
+@smooth_reg.register_fake
+def _(mu, kind):
+    return mu.new_empty(mu.shape[0], dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::smooth_reg_backward", mutates_args=())
+def smooth_reg_backward(mu: Tensor, gout: Tensor, kind: int) -> Tensor:
+    _hip.require_device(mu)
+    m = mu.float().contiguous()
+    B, _, H, W = m.shape
+    grad = torch.empty_like(m)
+    _hip.check(_hip.lib().rdq_smooth_reg_backward(kind, B, H, W, _hip.ptr(m), _hip.ptr(gout.float().contiguous()),
+                                                  _hip.ptr(grad), _hip.stream_of(m)), "rdq_smooth_reg_backward")
+    return grad
+
+
+@smooth_reg_backward.register_fake
+def _(mu, gout, kind):
+    return torch.empty_like(mu, dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::metrics", mutates_args=())
+def metrics(pred: Tensor, true_norm: Tensor) -> Tensor:
+    """K12: (mae, rmse, ssim) per model as a (3, B) device tensor (metrics.py:13-46)."""
+    _hip.require_device(pred)
+    B, _, H, W = pred.shape
+    t = true_norm.contiguous()
+    L = _hip.lib()
+    ws = torch.empty(int(L.rdq_metrics_ws_bytes(B, H, W)), dtype=torch.uint8, device=pred.device)
+    out = torch.empty(3, B, dtype=torch.float32, device=pred.device)
+    strides = (ctypes.c_int64 * 4)(*pred.stride())
+    _hip.check(L.rdq_metrics(B, H, W, _hip.ptr(pred), strides, _hip.ptr(t), _hip.ptr(out), _hip.ptr(ws),
+                             _hip.stream_of(pred)), "rdq_metrics")
+    return out
+
+
+@metrics.register_fake
+def _(pred, true_norm):
+    return pred.new_empty(3, pred.shape[0], dtype=torch.float32)
+
+
+# ------------------------------------------------------------------ forward-only operators
+def _forward_only(op, name):
+    """The U-Net / regulariser operators are inference kernels (the RED gradient is
+    (eps_hat - eps).detach(), regularization/diffusion.py:75): they run with grad-requiring inputs
+    (module parameters) but have no backward; differentiating through one raises."""
+    def backward(ctx, *grads):
+        raise RuntimeError(f"red_diffeq::{name} has no backward (forward-only HIP kernel)")
+
+    def setup(ctx, inputs, output):
+        pass
+    op.register_autograd(backward, setup_context=setup)
+
+
+for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (gn_silu, "gn_silu"), (rmsnorm, "rmsnorm"), (linear, "linear"),
+                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (attn, "attn"),
+                   (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
+    _forward_only(_op, _name)

@@ -4,35 +4,27 @@ exactly like the reference."""
 import torch
 
 from .. import _hip
+from .. import ops  # noqa: F401  (registers torch.ops.red_diffeq.*)
 
 _TV, _L2 = 0, 1
 
 
 class _SmoothReg(torch.autograd.Function):
+    """torch.ops.red_diffeq.smooth_reg / smooth_reg_backward (K6)."""
+
     @staticmethod
     def forward(ctx, mu, kind):
         _hip.require_device(mu)
         if mu.dim() != 4 or mu.shape[1] != 1:
             raise ValueError(f"expected (B,1,H,W), got {tuple(mu.shape)}")
-        m = mu.float().contiguous()
-        B, _, H, W = m.shape
-        loss = torch.empty(B, dtype=torch.float32, device=m.device)
-        _hip.check(_hip.lib().rdq_smooth_reg_forward(kind, B, H, W, _hip.ptr(m), _hip.ptr(loss),
-                                                     _hip.stream_of(m)), "rdq_smooth_reg_forward")
-        ctx.save_for_backward(m)
+        ctx.save_for_backward(mu)
         ctx.kind = kind
-        return loss
+        return torch.ops.red_diffeq.smooth_reg(mu, kind)
 
     @staticmethod
     def backward(ctx, gout):
-        (m,) = ctx.saved_tensors
-        B, _, H, W = m.shape
-        grad = torch.empty_like(m)
-        gout = gout.float().contiguous()
-        _hip.check(_hip.lib().rdq_smooth_reg_backward(ctx.kind, B, H, W, _hip.ptr(m), _hip.ptr(gout),
-                                                      _hip.ptr(grad), _hip.stream_of(m)),
-                   "rdq_smooth_reg_backward")
-        return grad, None
+        (mu,) = ctx.saved_tensors
+        return torch.ops.red_diffeq.smooth_reg_backward(mu, gout, ctx.kind), None
 
 
 def total_variation_loss(mu: torch.Tensor) -> torch.Tensor:

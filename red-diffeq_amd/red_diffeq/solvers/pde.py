@@ -8,8 +8,9 @@ The compute is the MI355X HIP path (include/red_diffeq_fwi.h): coefficient field
 time loop (stencil + periodic wrap + source injection + receiver sampling + history store) in one
 persistent launch when the survey fits resident on the chip, else temporal-blocked launches of T
 steps replayed from a cached hipGraph (K1), and a hand-written discrete adjoint (K2 + K4) as the
-autograd backward — where the reference records a ~5 MB-per-shot-step autograd tape, this keeps
-one fp32 wavefield per step (store-all history).
+autograd backward of the custom operator torch.ops.red_diffeq.fwi (red_diffeq/ops.py) — where the
+reference records a ~5 MB-per-shot-step autograd tape, this keeps one fp32 wavefield per step
+(store-all history).
 """
 import ctypes
 import os
@@ -20,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _hip
+from .. import ops as _ops   # registers torch.ops.red_diffeq.*
 from ..utils.data_trans import v_denormalize
 
 
@@ -72,6 +74,7 @@ class FwiPlan:
         self.status_t = torch.zeros(64, dtype=torch.int32, device=device)
         _hip.check(self.lib.rdq_fwi_set_status_buffer(self.handle, _hip.ptr(self.status_t)),
                    "rdq_fwi_set_status_buffer")
+        self.op_id = _ops.register_plan(self)      # integer handle for torch.ops.red_diffeq.fwi*
 
     def sizes(self, B):
         if B not in self._sizes:
@@ -143,6 +146,7 @@ class FwiPlan:
                    "rdq_fwi_set_tuning")
 
     def __del__(self):
+        _ops.unregister_plan(getattr(self, "op_id", -1))
         h = getattr(self, "handle", None)
         if h is not None and h.value:
             try:
@@ -151,75 +155,19 @@ class FwiPlan:
                 pass
             self.handle = None
 
-    # ---- thin wrappers over the C ABI (all buffers torch-allocated on the plan's device) ----
-    def _f32(self, nbytes):
-        return torch.empty(int(nbytes) // 4, dtype=torch.float32, device=self.device)
-
+    # ---- the C ABI entry points as torch.ops.red_diffeq operators (red_diffeq/ops.py) ----
     def coeffs(self, v, vel_mode):
-        B = v.shape[0]
-        sz = self.sizes(B)
-        coeffs = self._f32(sz.coeffs)
-        vstat = torch.empty(int(sz.vstat), dtype=torch.uint8, device=self.device)
-        strides = (ctypes.c_int64 * 4)(*v.stride())
-        _hip.check(self.lib.rdq_fwi_coeffs(self.handle, B, _hip.ptr(v), strides, vel_mode,
-                                           _hip.ptr(coeffs), _hip.ptr(vstat), _hip.stream_of(v)),
-                   "rdq_fwi_coeffs")
-        return coeffs, vstat
+        return torch.ops.red_diffeq.fwi_coeffs(v, self.op_id, vel_mode)
 
     def forward(self, coeffs, B, keep_history):
-        sz = self.sizes(B)
-        seis = torch.empty(B, self.ns, sz.nrec, self.ng, dtype=torch.float32, device=self.device)
-        hist = self._f32(sz.history) if keep_history else None
-        ring = self._f32(sz.ring)
-        _hip.check(self.lib.rdq_fwi_forward(self.handle, B, _hip.ptr(coeffs), _hip.ptr(seis),
-                                            _hip.ptr(hist), _hip.ptr(ring), _hip.stream_of(coeffs)),
-                   "rdq_fwi_forward")
-        return seis, hist
+        seis, hist = torch.ops.red_diffeq.fwi_forward(coeffs, self.op_id, B, bool(keep_history))
+        return seis, (hist if keep_history else None)
 
     def adjoint(self, coeffs, hist, dseis, B):
-        sz = self.sizes(B)
-        ring = self._f32(sz.ring)
-        gA = self._f32(sz.gA)
-        gk = torch.empty(int(sz.gk_part) // 8, dtype=torch.float64, device=self.device)
-        gb = self._f32(sz.gbeta)
-        _hip.check(self.lib.rdq_fwi_adjoint(self.handle, B, _hip.ptr(coeffs), _hip.ptr(hist),
-                                            _hip.ptr(dseis), _hip.ptr(ring), _hip.ptr(gA), _hip.ptr(gk),
-                                            _hip.ptr(gb), _hip.stream_of(coeffs)), "rdq_fwi_adjoint")
-        return gA, gk, gb
+        return torch.ops.red_diffeq.fwi_adjoint(coeffs, hist, dseis, self.op_id, B)
 
     def finalize(self, coeffs, vstat, gA, gk, gb, B, vel_mode):
-        sz = self.sizes(B)
-        colsum = torch.empty(int(sz.colsum) // 8, dtype=torch.float64, device=self.device)
-        out = torch.empty(B, 1, self.nz, self.nx, dtype=torch.float32, device=self.device)
-        _hip.check(self.lib.rdq_fwi_grad_finalize(self.handle, B, _hip.ptr(coeffs), _hip.ptr(vstat),
-                                                  _hip.ptr(gA), _hip.ptr(gk), _hip.ptr(gb), vel_mode,
-                                                  _hip.ptr(colsum), _hip.ptr(out), _hip.stream_of(coeffs)),
-                   "rdq_fwi_grad_finalize")
-        return out
-
-
-class _FWIFunction(torch.autograd.Function):
-    """seis = FWM(v); backward = hand-written discrete adjoint (no autograd tape)."""
-
-    @staticmethod
-    def forward(ctx, v, plan, vel_mode):
-        B = v.shape[0]
-        coeffs, vstat = plan.coeffs(v, vel_mode)
-        keep = bool(ctx.needs_input_grad[0])
-        seis, hist = plan.forward(coeffs, B, keep_history=keep)
-        if keep:
-            ctx.plan, ctx.vel_mode, ctx.B = plan, vel_mode, B
-            ctx.coeffs, ctx.vstat, ctx.hist = coeffs, vstat, hist
-        return seis
-
-    @staticmethod
-    def backward(ctx, gseis):
-        gseis = gseis.contiguous()
-        plan = ctx.plan
-        gA, gk, gb = plan.adjoint(ctx.coeffs, ctx.hist, gseis, ctx.B)
-        ctx.hist = None   # release the history (largest buffer) as early as possible
-        g = plan.finalize(ctx.coeffs, ctx.vstat, gA, gk, gb, ctx.B, ctx.vel_mode)
-        return g, None, None
+        return torch.ops.red_diffeq.fwi_grad_finalize(coeffs, vstat, gA, gk, gb, self.op_id, B, vel_mode)
 
 
 class FWIForward(nn.Module):
@@ -308,7 +256,8 @@ class FWIForward(nn.Module):
             vel_mode = 1
         plan = self._plan(v.shape[2], v.shape[3], v.device)
         self._last = plan
-        s = _FWIFunction.apply(v, plan, vel_mode)
+        keep = bool(v.requires_grad and torch.is_grad_enabled())
+        s = torch.ops.red_diffeq.fwi(v, plan.op_id, vel_mode, keep)[0]   # backward: K2 + K4 (ops.py)
         return self.s_norm_func(s) if self.normalize else s
 
     def check(self):
