@@ -298,7 +298,7 @@ def main():
     info = plan.launch_info(B)
     T = info["adj_T"]
     if info["adj_persistent"]:
-        kname = f"k_adj_pt<{T}>"                 # the whole adjoint time loop is ONE launch
+        kname = f"k_adj_pr<{T}>"                 # the whole adjoint time loop is ONE launch
         launches = 1
     else:
         kname = f"k_adj_tb<{T}>"                 # one launch per T steps

@@ -24,7 +24,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
      python3 tools/pmc_calib.py > gpurun_out/pmc/calib_$c.log 2>&1
   rc=$?; echo "pmc calib $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-for k in k_fwd_pt k_adj_pt; do
+for k in k_fwd_pt k_adj_pr; do
   # file name = what bench.py looks up: profiles/pmc_traffic_<kernel><T>_ns<ns>_B<B>.json
   python3 tools/pmc_traffic.py gpurun_out/pmc/p1 gpurun_out/pmc/p2 gpurun_out/pmc/calib_FETCH_SIZE \
      gpurun_out/pmc/calib_WRITE_SIZE "$k<$ONLY," gpurun_out/pmc/pmc_traffic_${k}${ONLY}_ns8_B1.json
