@@ -179,6 +179,10 @@ def _fake_forward(coeffs, plan, B, keep_history):
 def _fwi_setup(ctx, inputs, output):
     v, plan, vel_mode, keep_history = inputs
     _, coeffs, vstat, hist = output
+    # only seis is differentiable: no zero "gradients" are materialised for the saved buffers
+    # (a zeros_like of the history would be a multi-GB fill per backward)
+    ctx.mark_non_differentiable(coeffs, vstat, hist)
+    ctx.set_materialize_grads(False)
     if not keep_history:
         ctx.plan = None
         return
