@@ -16,6 +16,7 @@ Persistent-kernel failure (a neighbour hand-off or residency timeout of the sing
 kernels, reported through the plan's status word) is handled inside the loop, without a host sync
 per iteration: see ``_FaultMonitor``.
 """
+import os
 import warnings
 from typing import Optional
 
@@ -193,6 +194,7 @@ class InversionEngine:
                 check()          # a failure before the loop (e.g. while making y) is the caller's
             monitor = _FaultMonitor(fwi_forward, ts, self.device, sharded)
         diffusion = regularization == "diffusion"
+        overlap = diffusion and mu.is_cuda and not os.environ.get("RDQ_NO_OVERLAP")
         snaps = [None] * ts
 
         pbar = tqdm(total=ts, desc="Optimizing", unit="step", disable=not self.show_progress)
@@ -214,9 +216,24 @@ class InversionEngine:
                 v_in = x0_pred[:, :, 1:-1, 1:-1]
                 if sharded:
                     v_in = grad_all_reduce(v_in, process_group, monitor)
-                predicted = fwi_forward(v_in)
-                loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
-                reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
+                if overlap:
+                    # the regulariser (U-Net forward, no dependence on the FWI operator) runs on a
+                    # side stream beside the forward / adjoint: the persistent FWI grids leave CUs
+                    # free, the U-Net's small kernels fill them.  RNG draws (t, eps) are taken here,
+                    # in the reference's order (the operator draws nothing).
+                    main = torch.cuda.current_stream(mu.device)
+                    side = self._side_stream(mu.device)
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
+                    predicted = fwi_forward(v_in)
+                    loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
+                    main.wait_stream(side)
+                    reg_loss.record_stream(main)
+                else:
+                    predicted = fwi_forward(v_in)
+                    loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
+                    reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
                 total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
 
                 optimizer.zero_grad()
@@ -253,6 +270,12 @@ class InversionEngine:
         H = hist_dev.cpu().numpy()
         results = [{k: [H[t, j, i] for t in range(ts)] for j, k in enumerate(keys)} for i in range(B)]
         return mu[:, :, 1:-1, 1:-1], results
+
+    def _side_stream(self, device):
+        streams = self.__dict__.setdefault("_streams", {})
+        if device not in streams:
+            streams[device] = torch.cuda.Stream(device=device)
+        return streams[device]
 
     @staticmethod
     def _rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar):
