@@ -5,7 +5,8 @@
  * (SimingShan/red-diffeq red_diffeq/models/diffusion.py:78-301) and the RED regulariser's
  * elementwise prologue/epilogue (diffusion.py:393-429, 516-519;
  * red_diffeq/regularization/diffusion.py:63-81).  fp32 NCHW tensors, caller-owned, stream-ordered,
- * 0 / negative error codes, deterministic (no atomics).
+ * 0 / negative error codes, deterministic (no floating-point atomics: the conv's arrival tickets
+ * only pick which workgroup sums the split-K slabs, always in slab order).
  */
 #ifndef RED_DIFFEQ_UNET_H
 #define RED_DIFFEQ_UNET_H
@@ -34,10 +35,31 @@ typedef struct rdq_conv_desc {
 /* y = conv2d(input, w, bias, stride 1, padding pad) [+ residual]   (nn.Conv2d, implicit GEMM on
  * fp32 MFMA v_mfma_f32_16x16x4_f32).  w: [cout][cin1+cin2][kh][kw]; bias/residual nullable.
  * ws (nullable) holds split-K partial slabs: rdq_conv2d_ws_bytes(d) bytes let the kernel split the
- * reduction over enough workgroups to fill the chip; a smaller (or null) ws splits less (or not). */
+ * reduction over enough workgroups to fill the chip; a smaller (or null) ws splits less (or not).
+ * tickets (nullable): rdq_conv2d_tickets(d) uint32 words that are ZERO when the call is enqueued;
+ * the launch leaves them zero again, so one zeroed pool serves every stream-ordered call (two
+ * launches must not use the same words concurrently).  With tickets the split-K slabs are combined
+ * inside the conv launch by the last-arriving workgroup of each output tile; without, by a second
+ * launch.  Both sum the slabs in slab order (deterministic, identical results). */
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d);
+size_t rdq_conv2d_tickets(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
-               const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
+               const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
+
+/* Block.forward in two launches (diffusion.py:142-149, + the identity shortcut of 168):
+ *   y = SiLU(GroupNorm_G(conv2d(input) + bias) * (scale+1) + shift) [+ post_residual]
+ * The conv (channel-chunk form) accumulates the GroupNorm statistics of its output tiles in its
+ * epilogue (fp64 per tile, group and sample; summed in tile order by the normalise pass), replacing
+ * rdq_conv2d + rdq_group_norm_silu's statistics launch (+ a residual add).  rdq_conv2d_gn_ws_bytes
+ * returns 0 where this form does not apply (filters other than 3x3 / 1x1-pad-0, channel counts
+ * not multiples of the chunk, H*W < 32, C/G outside {8,16,32,64}): use the separate calls there.
+ * ws: conv split-K slabs + the conv output + the partial statistics.  tickets as rdq_conv2d (null:
+ * no split-K). */
+size_t rdq_conv2d_gn_ws_bytes(const rdq_conv_desc *d, int32_t G);
+int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                       int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                       const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
+                       hipStream_t stream);
 
 /* Mixed-precision conv2d (same input modes and epilogue): bf16 operands, fp32 accumulation on
  * v_mfma_f32_32x32x16_bf16.  The weights are packed once by rdq_conv2d_bf16_pack into

@@ -194,6 +194,374 @@ __global__ __launch_bounds__(256) void k_conv_reduce(int S, int64_t total, int N
     y[i] = v;
 }
 
+// ------------------------------------------------------------------ conv2d, channel-chunk form
+// The same implicit GEMM for the U-Net's own shapes (3x3 or 1x1 filters, channel counts multiples
+// of the chunk): one K stage = CPS whole input channels x every filter tap (k = ci*TAPS + tap, the
+// weights' own order, so the MFMA chain visits k in the same ascending groups of 4 as k_conv_ig).
+// A thread gathers the taps of ONE (pixel, channel) per stage from tap offsets and a padding mask
+// computed once per launch: the per-element index arithmetic of k_conv_ig's gather is gone.  Loads
+// run two stages ahead (two register sets, straight-line code so the waitcnt before a stash leaves
+// the younger stage in flight) into double-buffered LDS: at B = 1 a workgroup is alone on its CU,
+// so the K loop is latency-bound unless more than one stage is in flight.
+// Split-K partial slabs are combined by the LAST-arriving workgroup of each tile (an arrival ticket
+// per tile, then the slabs summed in slab order, then bias and residual: the arithmetic of
+// k_conv_reduce, bit for bit) instead of a separate launch.  Tickets are zero before the launch and
+// returned to zero by the combining workgroup.
+template <int TAPS> struct CcCfg;
+template <> struct CcCfg<9> { static constexpr int CPS = 8, BK = 72, NA = 9, QPR = 18, NWQ = 5; };
+template <> struct CcCfg<1> { static constexpr int CPS = 64, BK = 64, NA = 8, QPR = 16, NWQ = 4; };
+constexpr int CC_BN = 64, CC_BM = 32, CC_LDA = CC_BM + 16;
+constexpr int CC_SC1 = 16;             // buffer cache policy sc1: write-through stores, L1-bypassing loads
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+struct CcArgs {
+    rdq_conv_desc d;
+    const float *x, *x2, *w, *bias, *res;
+    float *y, *part;
+    unsigned *tickets;        // S > 1: one per (m tile, n tile)
+    double *gnp;              // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
+    int K, M, HW, nstages, per_split, S, G;
+};
+
+template <int TAPS, int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
+{
+    using C = CcCfg<TAPS>;
+    constexpr int BK = C::BK, NA = C::NA, NWQ = C::NWQ, QPR = C::QPR, LDW = BK + 4;
+    __shared__ __attribute__((aligned(16))) float Ws[2][CC_BN][LDW];
+    __shared__ float As[2][BK][CC_LDA];
+    __shared__ unsigned last_s;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * CC_BM, n0 = blockIdx.y * CC_BN, split = blockIdx.z;
+    const rdq_conv_desc &d = a.d;
+    const int N = d.cout, K = a.K;
+    const int s_begin = split * a.per_split, s_end = min(a.nstages, s_begin + a.per_split);
+    // gather role: pixel gp, channel lane cl of the stage's chunk
+    const int gp = tid & (CC_BM - 1), cl = tid >> 5;
+    const int gm = m0 + gp;
+    const bool pv = gm < a.M;
+    const int gb = pv ? gm / a.HW : 0, gpix = pv ? gm - gb * a.HW : 0;
+    const int oh = gpix / d.W, ow = gpix - oh * d.W;
+    int off[TAPS];
+    unsigned vmask = 0;
+    if constexpr (TAPS == 9) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ih = oh + t / 3 - d.pad, iw = ow + t % 3 - d.pad;
+            const bool ok = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+            vmask |= (ok ? 1u : 0u) << t;
+            off[t] = !ok ? 0 : MODE == RDQ_IN_UPSAMPLE2 ? (ih >> 1) * (d.W >> 1) + (iw >> 1) : ih * d.W + iw;
+        }
+    } else {
+        vmask = pv ? 1u : 0u;
+        off[0] = MODE == RDQ_IN_UNSHUFFLE2 ? (2 * oh) * (2 * d.W) + 2 * ow : gpix;
+    }
+    const size_t plane = MODE == RDQ_IN_UPSAMPLE2 ? (size_t)(d.H >> 1) * (d.W >> 1)
+                       : MODE == RDQ_IN_UNSHUFFLE2 ? (size_t)4 * a.HW : (size_t)a.HW;
+    const int cin1 = MODE == RDQ_IN_UNSHUFFLE2 ? d.cin1 >> 2 : d.cin1;
+    const float *xb = a.x + (size_t)gb * cin1 * plane;
+    const float *x2b = a.x2 ? a.x2 + (size_t)gb * d.cin2 * a.HW : a.x;
+    // weight role: quad q of row n for idx = tid + 256 r (rows past cout clamped: their outputs are
+    // never stored; idx past the tile only loads, never stashes)
+    int woff[NWQ];
+#pragma unroll
+    for (int r = 0; r < NWQ; ++r) {
+        const int idx = min(tid + 256 * r, CC_BN * QPR - 1);
+        const int n = idx / QPR, q = idx - n * QPR;
+        woff[r] = min(n0 + n, N - 1) * K + q * 4;
+    }
+    auto load = [&](int s, float (&ra)[NA], f32x4 (&rw)[NWQ]) {
+        if constexpr (TAPS == 9) {
+            const int ci = s * C::CPS + cl;
+            const float *src = ci < d.cin1 ? xb + (size_t)ci * plane : x2b + (size_t)(ci - d.cin1) * a.HW;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float v = src[off[t]];
+                ra[t] = (vmask >> t) & 1u ? v : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ci = s * C::CPS + cl + 8 * j;
+                const float *src;
+                int o = off[0];
+                if constexpr (MODE == RDQ_IN_UNSHUFFLE2) {
+                    src = xb + (size_t)(ci >> 2) * plane;
+                    o += ((ci >> 1) & 1) * (2 * d.W) + (ci & 1);
+                } else {
+                    src = ci < d.cin1 ? xb + (size_t)ci * plane : x2b + (size_t)(ci - d.cin1) * a.HW;
+                }
+                const float v = src[o];
+                ra[j] = vmask ? v : 0.0f;
+            }
+        }
+        const float *ws = a.w + (size_t)s * BK;
+#pragma unroll
+        for (int r = 0; r < NWQ; ++r) rw[r] = *reinterpret_cast<const f32x4 *>(ws + woff[r]);
+    };
+    auto stash = [&](int buf, const float (&ra)[NA], const f32x4 (&rw)[NWQ]) {
+        if constexpr (TAPS == 9) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) As[buf][cl * 9 + t][gp] = ra[t];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) As[buf][cl + 8 * j][gp] = ra[j];
+        }
+#pragma unroll
+        for (int r = 0; r < NWQ; ++r) {
+            const int idx = tid + 256 * r;
+            if (idx < CC_BN * QPR) {
+                const int n = idx / QPR, q = idx - n * QPR;
+                *reinterpret_cast<f32x4 *>(&Ws[buf][n][q * 4]) = rw[r];
+            }
+        }
+    };
+    f32x4 acc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+    // operands of a stage read from LDS in batches of BT k-groups, the next batch's reads issued
+    // before the current batch's MFMAs (one wave per SIMD at B = 1: nothing else hides LDS latency)
+    auto mma = [&](int buf) {
+        constexpr int KS = BK / 4, BT = KS % 3 == 0 ? 3 : 4, NB = KS / BT;
+        float av[2][BT], b0[2][BT], b1[2][BT];
+        auto rd = [&](int bt, float (&a_)[BT], float (&x_)[BT], float (&y_)[BT]) {
+#pragma unroll
+            for (int u = 0; u < BT; ++u) {
+                const int kk = (bt * BT + u) * 4 + (lane >> 4);
+                a_[u] = Ws[buf][wv * 16 + (lane & 15)][kk];
+                x_[u] = As[buf][kk][lane & 15];
+                y_[u] = As[buf][kk][16 + (lane & 15)];
+            }
+        };
+        // (sched_barrier: the machine scheduler would otherwise move each read next to its MFMA
+        // and wait for it there, lgkmcnt(0) per k-group)
+        rd(0, av[0], b0[0], b1[0]);
+#pragma unroll
+        for (int bt = 0; bt < NB; ++bt) {
+            if (bt + 1 < NB) rd(bt + 1, av[(bt + 1) & 1], b0[(bt + 1) & 1], b1[(bt + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < BT; ++u) {
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bt & 1][u], b0[bt & 1][u], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bt & 1][u], b1[bt & 1][u], acc[1], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    const int ns = s_end - s_begin;
+    if (ns > 0) {
+        // four register sets: at step i LDS buffer i&1 holds stage i, stages i+1..i+3 are in flight
+        // (three steps of MFMA work cover a load's latency), stage i+1 is stashed at the step's end
+        float ra0[NA], ra1[NA], ra2[NA], ra3[NA];
+        f32x4 rw0[NWQ], rw1[NWQ], rw2[NWQ], rw3[NWQ];
+        const int sl = s_end - 1;         // loads past the split's end re-read its last stage
+        load(s_begin, ra0, rw0);
+        load(min(s_begin + 1, sl), ra1, rw1);
+        load(min(s_begin + 2, sl), ra2, rw2);
+        stash(0, ra0, rw0);
+        __syncthreads();
+        auto step = [&](int i, float (&rl)[NA], f32x4 (&wl)[NWQ], const float (&rs)[NA], const f32x4 (&wsr)[NWQ]) {
+            load(min(s_begin + i + 3, sl), rl, wl);
+            mma(i & 1);
+            stash((i + 1) & 1, rs, wsr);
+            __syncthreads();
+        };
+        for (int i = 0;; i += 4) {
+            step(i, ra3, rw3, ra1, rw1);
+            if (i + 1 >= ns) break;
+            step(i + 1, ra0, rw0, ra2, rw2);
+            if (i + 2 >= ns) break;
+            step(i + 2, ra1, rw1, ra3, rw3);
+            if (i + 3 >= ns) break;
+            step(i + 3, ra2, rw2, ra0, rw0);
+            if (i + 4 >= ns) break;
+        }
+    }
+    // outputs of this lane: (n = n0 + wv*16 + (lane>>4)*4 + r, m = m0 + j*16 + (lane&15))
+    if (a.S < 0) {                         // slabs [S][B][cout][HW] for k_conv_reduce
+        const size_t slab = (size_t)a.M * N;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int m = m0 + j * 16 + (lane & 15);
+            const int b = m / a.HW, pix = m - b * a.HW;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + wv * 16 + (lane >> 4) * 4 + r;
+                if (m < a.M && n < N) a.part[split * slab + ((size_t)b * N + n) * a.HW + pix] = acc[j][r];
+            }
+        }
+        return;
+    }
+    if (a.S > 1) {
+        // in-launch combine.  Slabs in the tile's own register order (lane tid's 8 accumulators as
+        // two 16-B words), written and read write-through (sc1) so no L2 fence is needed:
+        // every storing wave drains its stores, the workgroup barrier, one agent-scope ticket add per
+        // workgroup, and the workgroup whose add returns S-1 reads all S slabs with sc1 loads
+        // (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
+        const int ntile = gridDim.x * gridDim.y, tile = blockIdx.y * gridDim.x + blockIdx.x;
+        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, 0x7fffffff, 0x00020000);
+        const int voff = tid * 32;
+        const int tbase = tile * (CC_BM * CC_BN * 4);
+        const int sbytes = ntile * (CC_BM * CC_BN * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[0]), pr, voff, split * sbytes + tbase, CC_SC1);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[1]), pr, voff + 16, split * sbytes + tbase, CC_SC1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        unsigned *tk = a.tickets + tile;
+        if (tid == 0) last_s = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(a.S - 1);
+        __syncthreads();
+        if (!last_s) return;
+        // slabs summed in slab order, four slabs' loads in flight at a time
+        f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff, tbase, CC_SC1));
+        f32x4 v1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff + 16, tbase, CC_SC1));
+        int s = 1;
+        for (; s + 4 <= a.S; s += 4) {
+            f32x4 t0[4], t1[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                t0[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff, (s + u) * sbytes + tbase, CC_SC1));
+                t1[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff + 16, (s + u) * sbytes + tbase, CC_SC1));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { v0 += t0[u]; v1 += t1[u]; }
+        }
+        for (; s < a.S; ++s) {
+            v0 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff, s * sbytes + tbase, CC_SC1));
+            v1 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff + 16, s * sbytes + tbase, CC_SC1));
+        }
+        acc[0] = v0;
+        acc[1] = v1;
+        if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // epilogue: (sum + bias) + residual
+    float rv[2][4], bv[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = min(m0 + j * 16 + (lane & 15), a.M - 1);
+        const int b = m / a.HW, pix = m - b * a.HW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = min(n0 + wv * 16 + (lane >> 4) * 4 + r, N - 1);
+            rv[j][r] = a.res ? a.res[((size_t)b * N + n) * a.HW + pix] : 0.0f;
+            bv[j][r] = a.bias ? a.bias[n] : 0.0f;
+        }
+    }
+    float ov[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = m0 + j * 16 + (lane & 15);
+        const int b = m / a.HW, pix = m - b * a.HW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = n0 + wv * 16 + (lane >> 4) * 4 + r;
+            float v = acc[j][r];
+            if (a.bias) v = v + bv[j][r];
+            if (a.res) v = v + rv[j][r];
+            ov[j][r] = v;
+            if (m < a.M && n < N) a.y[((size_t)b * N + n) * a.HW + pix] = v;
+        }
+    }
+    if (!a.gnp) return;
+    // GroupNorm statistics of the tile's outputs, fp64 sum and sum of squares per (group, sample
+    // slot: 0 = the sample of the tile's first pixel, 1 = the next; HW >= 32 so at most two), by
+    // fixed trees: a lane's 4 channels (one group, C/G >= 8) per pixel, xor over the 16 pixel lanes,
+    // over the lanes' 4-channel blocks of the same group, then over the waves of a group in wave
+    // order; written to gnp[((m tile * G + g) * 2 + slot) * 2 + {0, 1}]
+    const int cpg = N / a.G, b0 = m0 / a.HW;
+    double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = m0 + j * 16 + (lane & 15);
+        int sl = m < a.M ? m / a.HW - b0 : -1;
+        double s1 = 0.0, q1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double xv = ov[j][r];
+            s1 += xv;
+            q1 += xv * xv;
+        }
+        if (n0 + wv * 16 + (lane >> 4) * 4 >= N) sl = -1;
+        gs[0] += sl == 0 ? s1 : 0.0;
+        gq[0] += sl == 0 ? q1 : 0.0;
+        gs[1] += sl == 1 ? s1 : 0.0;
+        gq[1] += sl == 1 ? q1 : 0.0;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            gs[k] += __shfl_xor(gs[k], o, 64);
+            gq[k] += __shfl_xor(gq[k], o, 64);
+        }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        gs[k] += __shfl_xor(gs[k], 16, 64);          // 4-channel blocks (0,1) and (2,3): 8 channels
+        gq[k] += __shfl_xor(gq[k], 16, 64);
+    }
+    if (cpg >= 16) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            gs[k] += __shfl_xor(gs[k], 32, 64);      // the wave's 16 channels
+            gq[k] += __shfl_xor(gq[k], 32, 64);
+        }
+    }
+    __shared__ double gpart[4][2][2][2];              // [wave][8-channel half][slot][s, q]
+    if ((lane & 31) == 0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            gpart[wv][lane >> 5][k][0] = gs[k];
+            gpart[wv][lane >> 5][k][1] = gq[k];
+        }
+    }
+    __syncthreads();
+    const int gt = CC_BN / cpg;
+    if (tid < 2 * gt) {
+        const int g = tid >> 1, k = tid & 1;
+        double s = 0.0, q = 0.0;
+        if (cpg == 8) {
+            s = gpart[g >> 1][g & 1][k][0];
+            q = gpart[g >> 1][g & 1][k][1];
+        } else {
+            const int wpg = cpg / 16;
+            for (int w = g * wpg; w < (g + 1) * wpg; ++w) {
+                s += gpart[w][0][k][0];
+                q += gpart[w][0][k][1];
+            }
+        }
+        if (n0 + g * cpg < N) {
+            double *o = a.gnp + (((size_t)blockIdx.x * a.G + n0 / cpg + g) * 2 + k) * 2;
+            o[0] = s;
+            o[1] = q;
+        }
+    }
+}
+
+// channel-chunk form applies: 3x3 (any pad) or 1x1 (pad 0) filters, every channel count a multiple
+// of the chunk (so a stage never straddles the concat seam), 16-B aligned weight rows
+bool cc_ok(const rdq_conv_desc *d)
+{
+    const int cin = d->cin1 + d->cin2;
+    if (d->kh != d->kw || (d->kh != 3 && d->kh != 1)) return false;
+    const int cps = d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS;
+    if (d->kh == 1 && d->pad != 0) return false;
+    if (d->in_mode == RDQ_IN_UNSHUFFLE2 && d->kh != 1) return false;
+    return d->cin1 % cps == 0 && d->cin2 % cps == 0 && cin % 4 == 0;
+}
+
+// splits: fill the chip with about one workgroup per CU (a second workgroup on a CU only shares its
+// matrix unit), >= 3 stages per split (the pipeline's fill), and at most 16 slabs to combine
+int cc_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
+{
+    const int M = d->B * d->H * d->W;
+    const int tiles = ((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN);
+    const int nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
+    int S = std::max(1, std::min(std::min(256 / tiles, nstages / 3), 16));
+    const size_t slab = (size_t)tiles * CC_BM * CC_BN * sizeof(float);      // >= M * cout floats
+    if (S > 1) S = (int)std::min<size_t>((size_t)S, ws_bytes / slab);
+    S = std::max(S, 1);
+    const int per = (nstages + S - 1) / S;
+    *per_split = per;
+    return (nstages + per - 1) / per;
+}
+
 // split count: about one workgroup per CU over the tile grid, >= 4 K stages per split, and the
 // partial slabs within the caller's workspace
 int ig_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
@@ -316,6 +684,72 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
     } else {
         const int e1 = min(HW, (ch + 1) * 1024);
         for (int i = ch * 1024 + (int)threadIdx.x; i < e1; i += 256) py[i] = gn_silu1(px[i], mean, rstd, ga, be, sso, sc1, sh);
+    }
+}
+
+// the same pass on statistics accumulated by the producing conv (k_conv_cc, a.gnp): wave 0 of each
+// workgroup sums its (sample, group)'s per-tile partials — lane l takes tiles l, l+64, ... of the
+// sample in order, then a fixed xor tree — and the pass adds an optional residual after the SiLU
+// (ResnetBlock's identity shortcut, diffusion.py:168)
+__global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const float *__restrict__ x,
+                                                    const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                    const float *__restrict__ ss, const double *__restrict__ gnp,
+                                                    float eps, const float *__restrict__ post, float *__restrict__ y)
+{
+    const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
+    const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
+    const int c = g * cpg + cl;
+    __shared__ float st2[2];
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const int mlo = (int)(((int64_t)b * HW) / CC_BM), mhi = (int)(((int64_t)(b + 1) * HW - 1) / CC_BM);
+        double s = 0.0, q = 0.0;
+        for (int mt = mlo + lane; mt <= mhi; mt += 64) {
+            const int slot = (int)(((int64_t)mt * CC_BM) / HW) == b ? 0 : 1;
+            const double *p = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
+            s += p[0];
+            q += p[1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            q += __shfl_xor(q, o, 64);
+        }
+        if (lane == 0) {
+            const double n = (double)cpg * HW, mean = s / n;
+            double var = q / n - mean * mean;
+            var = var < 0.0 ? 0.0 : var;
+            st2[0] = (float)mean;
+            st2[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+    }
+    __syncthreads();
+    const float mean = st2[0], rstd = st2[1];
+    const float ga = gamma[c], be = beta[c];
+    const bool sso = ss != nullptr;
+    const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
+    const size_t base = ((size_t)b * C + c) * HW;
+    if ((HW & 3) == 0) {
+        const int i = (ch * 256 + (int)threadIdx.x) * 4;
+        if (i < HW) {
+            float4 v = *reinterpret_cast<const float4 *>(x + base + i);
+            v.x = gn_silu1(v.x, mean, rstd, ga, be, sso, sc1, sh);
+            v.y = gn_silu1(v.y, mean, rstd, ga, be, sso, sc1, sh);
+            v.z = gn_silu1(v.z, mean, rstd, ga, be, sso, sc1, sh);
+            v.w = gn_silu1(v.w, mean, rstd, ga, be, sso, sc1, sh);
+            if (post) {
+                const float4 r = *reinterpret_cast<const float4 *>(post + base + i);
+                v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+            }
+            *reinterpret_cast<float4 *>(y + base + i) = v;
+        }
+    } else {
+        const int e1 = min(HW, (ch + 1) * 1024);
+        for (int i = ch * 1024 + (int)threadIdx.x; i < e1; i += 256) {
+            float v = gn_silu1(x[base + i], mean, rstd, ga, be, sso, sc1, sh);
+            if (post) v += post[base + i];
+            y[base + i] = v;
+        }
     }
 }
 
@@ -1191,22 +1625,69 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 
 extern "C" {
 
+size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
+{
+    if (!d || d->B < 1 || d->H < 1 || d->W < 1 || d->cout < 1) return 0;
+    const int64_t M = (int64_t)d->B * d->H * d->W;
+    return (size_t)(((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN));
+}
+
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d)
 {
     if (!d || d->B < 1 || d->H < 1 || d->W < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->cin1 < 1) return 0;
     int per = 0;
+    if (cc_ok(d)) {
+        const int S = cc_splits(d, (size_t)-1 / 2, &per);
+        return S > 1 ? (size_t)S * rdq_conv2d_tickets(d) * CC_BM * CC_BN * sizeof(float) : 0;
+    }
     const int S = ig_splits(d, (size_t)-1 / 2, &per);
     return S > 1 ? (size_t)S * d->B * d->H * d->W * d->cout * sizeof(float) : 0;
 }
 
+
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
-               const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
+               const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t st)
 {
     if (!d || !x || !w || !y || d->B < 1 || d->cin1 < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->H < 1 ||
         d->W < 1 || d->pad < 0 || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
         return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return RDQ_E_INVALID;
+    if (cc_ok(d)) {
+        CcArgs c{};
+        c.d = *d; c.x = x; c.x2 = x2; c.w = w; c.bias = bias; c.res = residual; c.y = y;
+        c.part = static_cast<float *>(ws);
+        c.tickets = tickets;
+        c.K = (d->cin1 + d->cin2) * d->kh * d->kw;
+        c.HW = d->H * d->W;
+        c.M = d->B * c.HW;
+        c.nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
+        c.S = ws ? cc_splits(d, ws_bytes, &c.per_split) : 1;
+        if (c.S == 1) c.per_split = c.nstages;
+        const bool fold = c.S > 1 && tickets;        // combine in the conv launch
+        if (c.S > 1 && !tickets) c.tickets = nullptr;
+        const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+        CcArgs cl = c;
+        if (c.S > 1 && !fold) cl.S = -c.S;            // slabs only; k_conv_reduce combines
+        if (d->kh == 3) {
+            if (d->in_mode == RDQ_IN_UPSAMPLE2)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, cl);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, cl);
+        } else {
+            if (d->in_mode == RDQ_IN_UNSHUFFLE2)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, cl);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, cl);
+        }
+        if (c.S > 1 && !fold) {
+            const int64_t total = (int64_t)c.M * d->cout;
+            hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, c.S, total,
+                               d->cout, c.HW, c.part, bias, residual, y);
+        }
+        RDQ_CHECK(hipGetLastError());
+        return 0;
+    }
     IgArgs a{};
     a.d = *d; a.x = x; a.x2 = x2; a.w = w; a.bias = bias; a.res = residual; a.y = y;
     a.part = static_cast<float *>(ws);
@@ -1227,6 +1708,61 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a.S, total, d->cout,
                            a.HW, a.part, bias, residual, y);
     }
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+size_t rdq_conv2d_gn_ws_bytes(const rdq_conv_desc *d, int32_t G)
+{
+    if (!d || !cc_ok(d) || G < 1 || d->cout % G || d->H * d->W < CC_BM) return 0;
+    const int cpg = d->cout / G;
+    if (cpg < 8 || cpg > CC_BN || CC_BN % cpg) return 0;
+    const size_t M = (size_t)d->B * d->H * d->W, mt = (M + CC_BM - 1) / CC_BM;
+    return rdq_conv2d_ws_bytes(d) + M * d->cout * sizeof(float) + mt * G * 4 * sizeof(double);
+}
+
+int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                       int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                       const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
+                       hipStream_t st)
+{
+    const size_t need = rdq_conv2d_gn_ws_bytes(d, G);
+    if (!need || !x || !w || !y || !gamma || !beta || !ws || ws_bytes < need ||
+        (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        return RDQ_E_INVALID;
+    if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return RDQ_E_INVALID;
+    if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return RDQ_E_INVALID;
+    const size_t M = (size_t)d->B * d->H * d->W;
+    const size_t slabs = rdq_conv2d_ws_bytes(d);
+    float *h = reinterpret_cast<float *>(static_cast<char *>(ws) + slabs);
+    double *gnp = reinterpret_cast<double *>(h + M * d->cout);
+    CcArgs c{};
+    c.d = *d; c.x = x; c.x2 = x2; c.w = w; c.bias = bias; c.res = nullptr; c.y = h;
+    c.part = static_cast<float *>(ws);
+    c.tickets = tickets;
+    c.gnp = gnp;
+    c.G = G;
+    c.K = (d->cin1 + d->cin2) * d->kh * d->kw;
+    c.HW = d->H * d->W;
+    c.M = (int)M;
+    c.nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
+    c.S = (slabs && tickets) ? cc_splits(d, slabs, &c.per_split) : 1;   // statistics need the in-launch combine
+    if (c.S == 1) c.per_split = c.nstages;
+    const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+    if (d->kh == 3) {
+        if (d->in_mode == RDQ_IN_UPSAMPLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+    } else {
+        if (d->in_mode == RDQ_IN_UNSHUFFLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+    }
+    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
+    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
+                       scale_shift, gnp, eps, post_residual, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

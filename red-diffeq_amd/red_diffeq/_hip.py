@@ -71,9 +71,14 @@ SIGNATURES = {
                                           c_void_p, c_void_p]),
     # include/red_diffeq_unet.h
     "rdq_conv2d_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rdq_conv2d_tickets": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p, c_size_t, c_void_p]),
-    "rdq_conv2d_bf16_wpack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+                             c_void_p, c_size_t, c_void_p, c_void_p]),
+    "rdq_conv2d_gn_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),
+    "rdq_conv2d_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                     c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                     c_void_p, c_void_p]),
+    "rdq_conv2d_bf16_wpack_bytes":(c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16_pack": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -98,9 +98,10 @@ class Block(nn.Module):
         self.norm = nn.GroupNorm(groups, dim_out)
         self.act = nn.SiLU()
 
-    def forward(self, x, scale_shift=None, skip=None):
-        x = ops.conv2d(x, self.proj, x2=skip)          # skip: the concatenated U-Net skip (293-299)
-        return ops.group_norm_affine_silu(x, self.norm, scale_shift)
+    def forward(self, x, scale_shift=None, skip=None, post=None):
+        """skip: the concatenated U-Net skip (293-299); post: added after the SiLU (the identity
+        shortcut of ResnetBlock, 168)."""
+        return ops.conv_group_norm_silu(x, self.proj, self.norm, scale_shift, skip=skip, post=post)
 
 
 class ResnetBlock(nn.Module):
@@ -117,12 +118,12 @@ class ResnetBlock(nn.Module):
         if exists(self.mlp) and exists(time_emb):
             scale_shift = ops.linear(time_emb, self.mlp[1], act_in=1)   # Linear(SiLU(t)): (B, 2C)
         h = self.block1(x, scale_shift=scale_shift, skip=skip)
-        h = self.block2(h)
         if isinstance(self.res_conv, nn.Conv2d):
+            h = self.block2(h)
             return ops.conv2d(x, self.res_conv, x2=skip, residual=h)    # h + res_conv(x), fused
         if skip is not None:
             x = torch.cat((x, skip), dim=1)
-        return h + x
+        return self.block2(h, post=x)                                    # h + x, fused
 
 
 class LinearAttention(nn.Module):

@@ -54,6 +54,18 @@ def sinusoidal(t, dim, theta=10000):
     return torch.ops.red_diffeq.sinusoidal_emb(t, dim, float(theta))
 
 
+def conv_group_norm_silu(x, conv, norm, scale_shift=None, skip=None, post=None):
+    """Block.forward: SiLU(GroupNorm(conv(cat(x, skip))) * (scale + 1) + shift) [+ post]; the fused
+    two-launch form (statistics in the conv epilogue) where it applies in fp32, else conv +
+    GroupNorm (+ add)."""
+    pad = conv.padding[0] if isinstance(conv.padding, tuple) else int(conv.padding)
+    if _PREC["mode"] == "fp32" and ops.conv_gn_fusable(x, skip, conv.weight, pad, PLAIN, norm.num_groups):
+        return torch.ops.red_diffeq.conv2d_gn_silu(x, skip, conv.weight, conv.bias, pad, PLAIN, norm.weight,
+                                                   norm.bias, scale_shift, norm.num_groups, float(norm.eps), post)
+    h = group_norm_affine_silu(conv2d(x, conv, x2=skip), norm, scale_shift)
+    return h + post if post is not None else h
+
+
 def group_norm_affine_silu(x, norm, scale_shift=None):
     """GroupNorm -> x*(scale+1)+shift -> SiLU; scale_shift: (B, 2C) (scale first, as chunk(2))."""
     return torch.ops.red_diffeq.gn_silu(x, norm.weight, norm.bias, scale_shift, norm.num_groups, float(norm.eps))
@@ -89,6 +101,6 @@ def red_epilogue(diff, xt, t, eps_hat, eps):
                                         diff.sqrt_recipm1_alphas_cumprod)
 
 
-HIP_OPS = {"conv2d", "linear", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+HIP_OPS = {"conv2d", "conv_group_norm_silu", "linear", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
            "full_attention", "red_q_sample", "red_epilogue"}
 del math

@@ -15,7 +15,8 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
-    conv2d_mfma, gn_silu, rmsnorm, linear, sinusoidal_emb, linear_attn, attn, red_q_sample, red_eps
+    conv2d_mfma, conv2d_gn_silu, gn_silu, rmsnorm, linear, sinusoidal_emb, linear_attn, attn, red_q_sample,
+    red_eps
   loop (include/red_diffeq_loop.h)
     l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
 
@@ -271,9 +272,41 @@ def conv2d_mfma(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[
         return y
     nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
     ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+    tk = _tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d)))) if nws else None
     _hip.check(L.rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(weight.contiguous()), _hip.ptr(bias),
-                            _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, st), "rdq_conv2d")
+                            _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, tk, st), "rdq_conv2d")
     return y
+
+
+# Split-K arrival tickets of rdq_conv2d (include/red_diffeq_unet.h): one zeroed pool per device,
+# every launch leaves its words zero again.  Eager calls take consecutive windows of a ring (a window
+# comes round again only thousands of launches later); calls captured into a hipGraph get windows
+# that no later call reuses, since a graph replays with the same words, possibly beside eager work
+# on another stream.  No pool yet (first call inside a capture) or the graph region used up: no
+# tickets, and the slabs are combined by a second launch instead (same result).
+_TICKET_POOL = {}
+_TICKET_EAGER, _TICKET_GRAPH = 1 << 18, 1 << 19
+
+
+def _tickets(device, n):
+    capturing = torch.cuda.is_current_stream_capturing()
+    st = _TICKET_POOL.get(device)
+    if st is None:
+        if capturing:
+            return None
+        st = _TICKET_POOL[device] = {"pool": torch.zeros(_TICKET_EAGER + _TICKET_GRAPH, dtype=torch.int32,
+                                                         device=device), "eager": 0, "graph": 0}
+    if capturing:
+        if st["graph"] + n > _TICKET_GRAPH:
+            return None
+        off = _TICKET_EAGER + st["graph"]
+        st["graph"] += n
+    else:
+        if st["eager"] + n > _TICKET_EAGER:
+            st["eager"] = 0
+        off = st["eager"]
+        st["eager"] += n
+    return st["pool"].data_ptr() + 4 * off
 
 
 @conv2d_mfma.register_fake
@@ -300,6 +333,45 @@ def gn_silu(x: Tensor, weight: Tensor, bias: Tensor, scale_shift: Optional[Tenso
 @gn_silu.register_fake
 def _(x, weight, bias, scale_shift, groups, eps):
     return torch.empty_like(x)
+
+
+def conv_gn_fusable(x, x2, weight, pad, mode, groups):
+    """rdq_conv2d_gn_silu applies to this conv + GroupNorm (fp32 channel-chunk conv, H*W >= 32,
+    C / G in {8, 16, 32, 64})."""
+    d, _ = _conv_desc(x, x2, weight, pad, mode)
+    return int(_hip.lib().rdq_conv2d_gn_ws_bytes(ctypes.byref(d), int(groups))) > 0
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_gn_silu", mutates_args=())
+def conv2d_gn_silu(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], pad: int, mode: int,
+                   gamma: Tensor, beta: Tensor, scale_shift: Optional[Tensor], groups: int, eps: float,
+                   post: Optional[Tensor]) -> Tensor:
+    """Block.forward (diffusion.py:142-149): SiLU(GroupNorm(conv(x')) * (scale + 1) + shift) [+ post],
+    the GroupNorm statistics accumulated by the conv's epilogue (two launches)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    d, shape = _conv_desc(x, x2, weight, pad, mode)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_gn_ws_bytes(ctypes.byref(d), int(groups)))
+    if nws == 0:
+        raise ValueError("conv2d_gn_silu: shape not supported by the fused form (see conv_gn_fusable)")
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    tk = _tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d))))
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_gn_silu(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(weight.contiguous()),
+                                    _hip.ptr(bias), int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta),
+                                    _hip.ptr(ss), _hip.ptr(pr), _hip.ptr(y), _hip.ptr(ws), nws, tk,
+                                    _hip.stream_of(x)), "rdq_conv2d_gn_silu")
+    return y
+
+
+@conv2d_gn_silu.register_fake
+def _(x, x2, weight, bias, pad, mode, gamma, beta, scale_shift, groups, eps, post):
+    _, shape = _conv_desc(x, x2, weight, pad, mode)
+    return x.new_empty(shape)
 
 
 @torch.library.custom_op(f"{LIB}::rmsnorm", mutates_args=())
@@ -541,7 +613,8 @@ def _forward_only(op, name):
     op.register_autograd(backward, setup_context=setup)
 
 
-for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (gn_silu, "gn_silu"), (rmsnorm, "rmsnorm"), (linear, "linear"),
+for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_gn_silu, "conv2d_gn_silu"), (gn_silu, "gn_silu"),
+                   (rmsnorm, "rmsnorm"), (linear, "linear"),
                    (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (attn, "attn"),
                    (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
     _forward_only(_op, _name)

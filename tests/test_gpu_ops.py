@@ -72,6 +72,9 @@ def test_unet_and_loop_ops_opcheck(cuda):
         opcheck(ops.conv2d_mfma, (x, x2, w, b, res, 1, 0, bf16))
     opcheck(ops.conv2d_mfma, (x, None, r(8, 16, 3, 3), None, None, 1, 1, False))      # upsample
     opcheck(ops.conv2d_mfma, (x, None, r(8, 64, 1, 1), r(8), None, 0, 2, False))       # unshuffle
+    wg = r(64, 24, 3, 3) * 0.1
+    opcheck(ops.conv2d_gn_silu, (x, x2, wg, r(64), 1, 0, r(64), r(64), r(2, 128), 8, 1e-5, r(2, 64, 12, 10)))
+    opcheck(ops.conv2d_gn_silu, (x, x2, wg, None, 1, 0, r(64), r(64), None, 8, 1e-5, None))
     opcheck(ops.gn_silu, (x, r(16), r(16), r(2, 32), 8, 1e-5))
     opcheck(ops.gn_silu, (x, r(16), r(16), None, 8, 1e-5))
     opcheck(ops.rmsnorm, (x, r(1, 16, 1, 1), x))
@@ -104,7 +107,7 @@ def test_unet_dispatches_through_ops(cuda):
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
         y = net(x, t)                 # grad enabled: the eager path (no hipGraph replay)
     names = {e.name for e in prof.events()}
-    for op in ("conv2d_mfma", "gn_silu", "rmsnorm", "linear", "sinusoidal_emb", "linear_attn", "attn"):
+    for op in ("conv2d_mfma", "conv2d_gn_silu", "gn_silu", "rmsnorm", "linear", "sinusoidal_emb", "linear_attn", "attn"):
         assert f"red_diffeq::{op}" in names, op
     with pytest.raises(RuntimeError, match="no backward"):
         y.sum().backward()

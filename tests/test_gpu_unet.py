@@ -49,6 +49,75 @@ def test_conv_concat_residual_upsample_unshuffle(cuda):
     close(ops.conv2d(a, nb), R.conv2d(a, nb))
 
 
+def _conv_abi(x, x2, conv, mode, res, tickets):
+    """rdq_conv2d through the C ABI with (pool window) or without (second launch) arrival tickets."""
+    import ctypes
+    from red_diffeq import _hip, ops as O
+    d, shape = O._conv_desc(x, x2, conv.weight, conv.padding[0], mode)
+    L = _hip.lib()
+    y = torch.empty(shape, device=x.device)
+    nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=x.device)
+    tk = O._tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d)))) if tickets else None
+    _hip.check(L.rdq_conv2d(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(conv.weight), _hip.ptr(conv.bias),
+                            _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, tk, _hip.stream_of(x)), "rdq_conv2d")
+    return y
+
+
+# the U-Net's own conv shapes at B = 1 and 2 (channel-chunk kernel k_conv_cc: 3x3 over 8-channel
+# chunks, 1x1 over 64-channel chunks, split-K combined in-launch by arrival tickets)
+@pytest.mark.parametrize("cin1,cin2,cout,k,H,B,mode", [
+    (64, 0, 64, 3, 72, 1, 0), (128, 64, 64, 3, 36, 1, 0), (512, 256, 512, 3, 9, 1, 0), (256, 0, 256, 3, 18, 2, 0),
+    (256, 0, 128, 3, 36, 1, 1), (64, 0, 384, 1, 72, 1, 0), (256, 128, 256, 1, 18, 1, 0), (256, 0, 128, 1, 18, 1, 2),
+    (512, 0, 512, 3, 9, 1, 0), (768, 0, 1536, 1, 9, 1, 0)])
+def test_conv_channel_chunk_tickets(cuda, cin1, cin2, cout, k, H, B, mode):
+    from red_diffeq import ops as O
+    torch.manual_seed(3)
+    conv = nn.Conv2d(cin1 + cin2, cout, k, padding=k // 2).to(cuda)
+    conv.weight.data *= 0.5
+    xs = H // 2 if mode == 1 else 2 * H if mode == 2 else H
+    x = torch.randn(B, cin1 // (4 if mode == 2 else 1), xs, xs, device=cuda)
+    x2 = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    res = torch.randn(B, cout, H, H, device=cuda)
+    a = _conv_abi(x, x2, conv, mode, res, True)
+    b = _conv_abi(x, x2, conv, mode, res, False)
+    assert torch.equal(a, b)                       # in-launch combine == separate combine, bit for bit
+    xin = R.upsample_nearest2(x) if mode == 1 else R.pixel_unshuffle2(x) if mode == 2 else x
+    if x2 is not None:
+        xin = torch.cat((xin, x2), 1)
+    close(a, R.conv2d(xin, conv) + res)
+    assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0     # tickets returned to zero
+
+
+# Block.forward as two launches (GroupNorm statistics in the conv epilogue, rdq_conv2d_gn_silu) vs
+# conv -> F.group_norm -> scale/shift -> SiLU (+ identity shortcut) in torch fp32
+@pytest.mark.parametrize("cin1,cin2,cout,H,B,ss,post", [
+    (64, 0, 64, 72, 1, True, True), (128, 64, 64, 36, 1, True, False), (512, 256, 512, 9, 1, True, False),
+    (256, 0, 256, 18, 2, False, True), (64, 0, 128, 9, 3, True, True), (128, 0, 256, 10, 2, True, False)])
+def test_conv_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post):
+    from red_diffeq import ops as O
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(6)
+    conv = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    norm = nn.GroupNorm(8, cout).to(cuda)
+    with torch.no_grad():
+        norm.weight.mul_(1 + 0.3 * torch.randn_like(norm.weight))
+        norm.bias.add_(0.2 * torch.randn_like(norm.bias))
+    x = torch.randn(B, cin1, H, H, device=cuda)
+    x2 = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    sc = torch.randn(B, 2 * cout, device=cuda) if ss else None
+    pr = torch.randn(B, cout, H, H, device=cuda) if post else None
+    assert O.conv_gn_fusable(x, x2, conv.weight, 1, 0, 8)
+    with torch.no_grad():
+        got = ops.conv_group_norm_silu(x, conv, norm, sc, skip=x2, post=pr)
+        xin = torch.cat((x, x2), 1) if x2 is not None else x
+        ref = R.group_norm_affine_silu(R.conv2d(xin, conv), norm, sc[:, :, None, None].chunk(2, dim=1) if ss else None)
+        if post:
+            ref = ref + pr
+    close(got, ref, rel=5e-5)
+    assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("C,H,ss", [(64, 72, True), (16, 9, False), (128, 18, True)])
 def test_group_norm_silu(cuda, C, H, ss):
     from red_diffeq.models import unet_ops as ops

@@ -27,3 +27,4 @@ if "TCC_HIT_sum" in m:
 if "GRBM_GUI_ACTIVE" in m:
     out["GRBM_GUI_ACTIVE"] = m["GRBM_GUI_ACTIVE"]
 print(out)
+print({k: v for k, v in sorted(m.items())})
