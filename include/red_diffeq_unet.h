@@ -87,13 +87,24 @@ int rdq_rmsnorm(int32_t B, int32_t C, int32_t HW, const float *x, const float *g
 int rdq_linear(int32_t B, int32_t in, int32_t out, const float *x, const float *w, const float *bias,
                int32_t act_in, int32_t act_out, float *y, hipStream_t stream);
 
+/* Unet.time_mlp in one launch (diffusion.py:255-258): y = W2 GELU(W1 SinusoidalPosEmb(t) + b1) + b2,
+ * w1 [hid][dim], w2 [out][hid]; one workgroup per sample. */
+int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid,
+                 const float *w2, const float *b2, int32_t out, float *y, hipStream_t stream);
+
+/* n <= 32 linears sharing one input, in one launch: y_j[b] = W_j . SiLU(x[b]) + b_j  (every
+ * ResnetBlock's time MLP, diffusion.py:157-165); w_j [out_j][in], y_j [B][out_j], b nullable. */
+int rdq_linear_silu_multi(int32_t B, int32_t in, const float *x, int32_t n, const float *const *w,
+                          const float *const *b, const int32_t *out, float *const *y, hipStream_t stream);
+
 /* SinusoidalPosEmb (diffusion.py:93-107): y[b] = [sin(t_b f), cos(t_b f)], f_i = exp(-i ln(theta)/(half-1)). */
 int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, float *y, hipStream_t stream);
 
 /* LinearAttention core (diffusion.py:182-194; dh <= 32), qkv = to_qkv(RMSNorm(x)) as (B, 3*heads*dh, n);
  * mem_kv (2, heads, dh, nmem); out (B, heads*dh, n) before to_out.  ws: rdq_linear_attention_ws_bytes
- * (k-softmax statistics + per-256-token context partials, combined in a fixed order, + the combined
- * context).  dh = 32 forms each partial context on v_mfma_f32_32x32x2_f32. */
+ * (per-256-token k row maxima / exp sums and partial contexts, combined in chunk order with the
+ * softmax rescaling exp(m_chunk - m), + the combined context).  dh = 32 forms each partial context
+ * on v_mfma_f32_32x32x2_f32. */
 size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem);
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
                          const float *mem_kv, float *out, void *ws, hipStream_t stream);

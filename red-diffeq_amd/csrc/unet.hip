@@ -867,46 +867,105 @@ __global__ void k_sinusoidal(int dim, float neg_emb, const int64_t *__restrict__
     y[(size_t)b * dim + half + i] = cosf(arg);
 }
 
+// Unet.time_mlp in one launch: SinusoidalPosEmb -> Linear -> GELU -> Linear, one workgroup per
+// sample, one wave per output row (the arithmetic of k_sinusoidal and k_linear, element for element)
+constexpr int TM_T = 1024;
+// the weight loads of 256 inputs are issued together (a dependent chain of loads would pay the
+// memory latency once per 64 inputs); products accumulated in input order as in k_linear
+__device__ __forceinline__ float wave_dot(const float *__restrict__ w, const float *x, int in, int lane, bool silu)
+{
+    float s = 0.0f;
+    for (int i0 = 0; i0 < in; i0 += 256) {
+        float wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wv[u] = w[min(i0 + lane + 64 * u, in - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + lane + 64 * u;
+            if (i < in) {
+                float v = x[i];
+                if (silu) v = v / (1.0f + expf(-v));
+                s += wv[u] * v;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    return s;
+}
+__global__ __launch_bounds__(TM_T) void k_time_mlp(int dim, float neg_emb, const int64_t *__restrict__ t,
+                                                   const float *__restrict__ w1, const float *__restrict__ b1, int hid,
+                                                   const float *__restrict__ w2, const float *__restrict__ b2, int out,
+                                                   float *__restrict__ y)
+{
+    extern __shared__ float tm_sm[];
+    float *e = tm_sm, *h = tm_sm + dim;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = TM_T / 64;
+    const int half = dim / 2;
+    if (tid < half) {
+        const float f = expf((float)tid * neg_emb);
+        const float arg = (float)t[b] * f;
+        e[tid] = sinf(arg);
+        e[half + tid] = cosf(arg);
+    }
+    __syncthreads();
+    // four output rows per wave at a time (their weight loads in flight together)
+    for (int o0 = wv; o0 < hid; o0 += 4 * nw) {
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = wave_dot(w1 + (size_t)min(o0 + u * nw, hid - 1) * dim, e, dim, lane, false);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int o = o0 + u * nw;
+            if (lane == 0 && o < hid) {
+                const float v = r[u] + b1[o];
+                h[o] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+            }
+        }
+    }
+    __syncthreads();
+    for (int o0 = wv; o0 < out; o0 += 4 * nw) {
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = wave_dot(w2 + (size_t)min(o0 + u * nw, out - 1) * hid, h, hid, lane, false);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int o = o0 + u * nw;
+            if (lane == 0 && o < out) y[(size_t)b * out + o] = r[u] + b2[o];
+        }
+    }
+}
+
+// every ResnetBlock's time MLP, Linear(SiLU(t)) (diffusion.py:157-165), in one launch: up to
+// LM_MAX linears sharing the input, one wave per output row
+constexpr int LM_MAX = 32;
+struct LinMulti {
+    const float *w[LM_MAX];
+    const float *b[LM_MAX];
+    float *y[LM_MAX];
+    int out[LM_MAX];
+    int start[LM_MAX + 1];
+    int n;
+};
+__global__ __launch_bounds__(256) void k_linear_silu_multi(int in, const float *__restrict__ x, LinMulti L)
+{
+    const int go = blockIdx.x * 4 + (threadIdx.x >> 6), b = blockIdx.y, lane = threadIdx.x & 63;
+    if (go >= L.start[L.n]) return;
+    int j = 0;
+    while (go >= L.start[j + 1]) ++j;
+    const int o = go - L.start[j];
+    const float s = wave_dot(L.w[j] + (size_t)o * in, x + (size_t)b * in, in, lane, true);
+    if (lane == 0) L.y[j][(size_t)b * L.out[j] + o] = s + (L.b[j] ? L.b[j][o] : 0.0f);
+}
+
 // -------------------------------------------------------------------------- linear attention
-// k softmax over the (memory + pixel) tokens per (b, h, d): ONE pass of online max / sum per row
-// (one wave per row, lanes strided over tokens, fixed-order wave reduction).
-__device__ __forceinline__ void online_merge(float &m, float &s, float m2, float s2)
-{
-    const float mn = fmaxf(m, m2);
-    if (mn == -INFINITY) return;
-    s = s * expf(m - mn) + s2 * expf(m2 - mn);
-    m = mn;
-}
-
-__global__ __launch_bounds__(256) void k_la_stats(int B, int heads, int dh, int n, int nmem,
-                                                  const float *__restrict__ qkv, const float *__restrict__ mem,
-                                                  float *__restrict__ stats)
-{
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);          // (b, h, d) flattened
-    const int C = heads * dh;
-    if (row >= B * heads * dh) return;
-    const int b = row / (heads * dh), hd = row - b * heads * dh;
-    const float *krow = qkv + ((size_t)b * 3 * C + C + hd) * n;
-    const float *mk = mem + (size_t)hd * nmem;                   // mem_kv[0][h][d][:]
-    float m = -INFINITY, sm = 0.0f;
-    for (int j = lane; j < nmem + n; j += 64) {
-        const float v = j < nmem ? mk[j] : krow[j - nmem];
-        if (v > m) { sm = sm * expf(m - v) + 1.0f; m = v; }
-        else sm += expf(v - m);
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        const float m2 = __shfl_down(m, off, 64), s2 = __shfl_down(sm, off, 64);
-        online_merge(m, sm, m2, s2);
-    }
-    if (lane == 0) { stats[2 * row] = m; stats[2 * row + 1] = sm; }
-}
-
-// partial context over a 256-token chunk: ctx_part[chunk][b][h][d][e] = sum_j exp(k[d][j] - m_d) v[e][j]
+// k softmax over the (memory + pixel) tokens per (b, h, d) folded into the context (flash style): a
+// chunk of LA_CH tokens forms exp(k - m_c) with its OWN row maxima m_c, the partial context
+// sum_j exp(k[d][j] - m_c[d]) v[e][j] and the partial sum s_c[d]; the combine rescales the chunks
+// by exp(m_c - max_c m_c) in chunk order.  No separate statistics pass over all tokens.
 constexpr int LA_CH = 256;
 __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nmem, const float *__restrict__ qkv,
-                                                const float *__restrict__ mem, const float *__restrict__ stats,
-                                                float *__restrict__ part)
+                                                const float *__restrict__ mem, float *__restrict__ part,
+                                                float *__restrict__ pstat)
 {
     __shared__ float P[32][LA_CH + 1], V[32][LA_CH + 1];
     const int ch = blockIdx.x, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
@@ -916,17 +975,39 @@ __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nm
     const float *vb = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
     const float *mk = mem + (size_t)(0 * heads + h) * dh * nmem;
     const float *mv = mem + (size_t)(1 * heads + h) * dh * nmem;
-    const float *st = stats + ((size_t)(b * heads + h) * dh) * 2;
     for (int i = tid; i < dh * LA_CH; i += 256) {
         const int d = i / LA_CH, jj = i - d * LA_CH, j = j0 + jj;
-        float pk = 0.0f, vv = 0.0f;
+        float kv = -INFINITY, vv = 0.0f;
         if (j < nk) {
-            const float kv = j < nmem ? mk[(size_t)d * nmem + j] : kb[(size_t)d * n + (j - nmem)];
-            pk = expf(kv - st[2 * d]);
+            kv = j < nmem ? mk[(size_t)d * nmem + j] : kb[(size_t)d * n + (j - nmem)];
             vv = j < nmem ? mv[(size_t)d * nmem + j] : vb[(size_t)d * n + (j - nmem)];
         }
-        P[d][jj] = pk;
+        P[d][jj] = kv;
         V[d][jj] = vv;                                           // row d of V = value channel e = d
+    }
+    __syncthreads();
+    // row maxima and exp / sums: 8 threads per row d, 32 tokens each, fixed xor trees
+    {
+        const int d = tid >> 3, q = tid & 7;
+        float m = -INFINITY;
+        if (d < dh)
+            for (int jj = q; jj < LA_CH; jj += 8) m = fmaxf(m, P[d][jj]);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 8));
+        float sm = 0.0f;
+        if (d < dh)
+            for (int jj = q; jj < LA_CH; jj += 8) {
+                const float e = P[d][jj] == -INFINITY ? 0.0f : expf(P[d][jj] - m);
+                P[d][jj] = e;
+                sm += e;
+            }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 8);
+        if (d < dh && q == 0) {
+            float *ps = pstat + (((size_t)ch * gridDim.z + b) * heads + h) * dh * 2 + 2 * d;
+            ps[0] = m;
+            ps[1] = sm;
+        }
     }
     __syncthreads();
     float *o = part + (((size_t)ch * gridDim.z + b) * heads + h) * dh * dh;
@@ -962,23 +1043,24 @@ __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nm
     for (int q = 0; q < 4; ++q) if (e0 + q < dh) o[(size_t)d * dh + e0 + q] = acc[q];
 }
 
-// ctx[b][h][d][e] = (sum of the chunk partials, in chunk order) / sum_d, once per (b, h)
-__global__ __launch_bounds__(256) void k_la_reduce(int BHDD, int dh, int nch, const float *__restrict__ stats,
+// ctx[b][h][d][e] = sum_c exp(m_c[d] - M[d]) part_c[d][e] / sum_c exp(m_c[d] - M[d]) s_c[d], chunks in
+// order (M = the maximum over the chunks)
+__global__ __launch_bounds__(256) void k_la_reduce(int BHDD, int dh, int nch, const float *__restrict__ pstat,
                                                    const float *__restrict__ part, float *__restrict__ ctx)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= BHDD) return;
-    float t = 0.0f;
-    int c = 0;
-    for (; c + 4 <= nch; c += 4) {                               // loads issued 4 at a time
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = part[(size_t)(c + u) * BHDD + i];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) t += v[u];
+    const int row = i / dh;                                      // (b, h, d)
+    const int BHD = BHDD / dh;
+    float M = -INFINITY;
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, pstat[((size_t)c * BHD + row) * 2]);
+    float num = 0.0f, den = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+        const float f = expf(pstat[((size_t)c * BHD + row) * 2] - M);
+        num += f * part[(size_t)c * BHDD + i];
+        den += f * pstat[((size_t)c * BHD + row) * 2 + 1];
     }
-    for (; c < nch; ++c) t += part[(size_t)c * BHDD + i];
-    ctx[i] = t / stats[(size_t)(i / dh) * 2 + 1];                // row (b, h, d)
+    ctx[i] = num / den;
 }
 
 // per (b, h, pixel): ctx = (sum of chunk partials in order) / sum_d; q softmax over d, scale,
@@ -1901,12 +1983,47 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
     return 0;
 }
 
+int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid,
+                 const float *w2, const float *b2, int32_t out, float *y, hipStream_t st)
+{
+    if (B < 1 || dim < 4 || dim % 2 || dim / 2 > TM_T || hid < 1 || out < 1 || (size_t)(dim + hid) * 4 > 64 * 1024 ||
+        !t || !w1 || !b1 || !w2 || !b2 || !y)
+        return RDQ_E_INVALID;
+    const int half = dim / 2;
+    const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
+    hipLaunchKernelGGL(k_time_mlp, dim3(B), dim3(TM_T), (dim + hid) * sizeof(float), st, dim, -emb, t, w1, b1, hid, w2,
+                       b2, out, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_linear_silu_multi(int32_t B, int32_t in, const float *x, int32_t n, const float *const *w,
+                          const float *const *b, const int32_t *out, float *const *y, hipStream_t st)
+{
+    if (B < 1 || in < 1 || !x || n < 1 || n > LM_MAX || !w || !out || !y) return RDQ_E_INVALID;
+    LinMulti L{};
+    L.n = n;
+    L.start[0] = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!w[j] || !y[j] || out[j] < 1) return RDQ_E_INVALID;
+        L.w[j] = w[j];
+        L.b[j] = b ? b[j] : nullptr;
+        L.y[j] = y[j];
+        L.out[j] = out[j];
+        L.start[j + 1] = L.start[j] + out[j];
+    }
+    hipLaunchKernelGGL(k_linear_silu_multi, dim3((L.start[n] + 3) / 4, B), dim3(256), 0, st, in, x, L);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
 static int la_chunks(int n, int nmem) { return (n + nmem + LA_CH - 1) / LA_CH; }
 
 size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem)
 {
     if (B < 1 || heads < 1 || dh < 1 || n < 1 || nmem < 0) return 0;
-    return ((size_t)B * heads * dh * 2 + (size_t)(la_chunks(n, nmem) + 1) * B * heads * dh * dh) * sizeof(float);
+    const size_t nch = la_chunks(n, nmem);
+    return (nch * B * heads * dh * 2 + (nch + 1) * B * heads * dh * dh) * sizeof(float);
 }
 
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
@@ -1914,15 +2031,13 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
 {
     if (B < 1 || heads < 1 || dh < 1 || dh > 32 || n < 1 || nmem < 0 || !qkv || !mem_kv || !out || !ws)
         return RDQ_E_INVALID;
-    float *stats = (float *)ws;
-    float *part = stats + (size_t)B * heads * dh * 2;
     const int nch = la_chunks(n, nmem);
+    float *pstat = (float *)ws;
+    float *part = pstat + (size_t)nch * B * heads * dh * 2;
     float *ctx = part + (size_t)nch * B * heads * dh * dh;
-    hipLaunchKernelGGL(k_la_stats, dim3((B * heads * dh + 3) / 4), dim3(256), 0, st, B, heads, dh, n, nmem, qkv,
-                       mem_kv, stats);
-    hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, stats, part);
+    hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, part, pstat);
     const int bhdd = B * heads * dh * dh;
-    hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, stats, part, ctx);
+    hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, pstat, part, ctx);
     hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx,
                        out);
     RDQ_CHECK(hipGetLastError());

@@ -78,7 +78,7 @@ SIGNATURES = {
     "rdq_conv2d_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                      c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_void_p, c_void_p]),
-    "rdq_conv2d_bf16_wpack_bytes":(c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rdq_conv2d_bf16_wpack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16_pack": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -89,6 +89,10 @@ SIGNATURES = {
     "rdq_rmsnorm": (c_int32, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rdq_linear": (c_int32, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                              c_void_p]),
+    "rdq_time_mlp": (c_int32, [c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                               c_int32, c_void_p, c_void_p]),
+    "rdq_linear_silu_multi": (c_int32, [c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
     "rdq_sinusoidal_emb": (c_int32, [c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
     "rdq_linear_attention_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "rdq_linear_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,

@@ -112,10 +112,10 @@ class ResnetBlock(nn.Module):
         self.block2 = Block(dim_out, dim_out, groups=groups)
         self.res_conv = nn.Conv2d(dim, dim_out, 1) if dim != dim_out else nn.Identity()
 
-    def forward(self, x, time_emb=None, skip=None):
-        """(reference 160-168); `skip` = the tensor the reference torch.cat's onto x first."""
-        scale_shift = None
-        if exists(self.mlp) and exists(time_emb):
+    def forward(self, x, time_emb=None, skip=None, scale_shift=None):
+        """(reference 160-168); `skip` = the tensor the reference torch.cat's onto x first;
+        `scale_shift` = this block's Linear(SiLU(time_emb)) when the caller formed it already."""
+        if scale_shift is None and exists(self.mlp) and exists(time_emb):
             scale_shift = ops.linear(time_emb, self.mlp[1], act_in=1)   # Linear(SiLU(t)): (B, 2C)
         h = self.block1(x, scale_shift=scale_shift, skip=skip)
         if isinstance(self.res_conv, nn.Conv2d):
@@ -225,9 +225,12 @@ class Unet(nn.Module):
         return 2 ** (len(self.downs) - 1)
 
     def _time(self, time):
-        t = ops.sinusoidal(time, self.time_mlp[0].dim, self.time_mlp[0].theta)
-        t = ops.linear(t, self.time_mlp[1], act_out=1)                  # Linear -> GELU
-        return ops.linear(t, self.time_mlp[3])
+        return ops.time_mlp(time, self.time_mlp)                          # one launch
+
+    def _resnet_blocks(self):
+        """The ResnetBlocks in forward order."""
+        bl = [b for b1, b2, _, _ in self.downs for b in (b1, b2)] + [self.mid_block1, self.mid_block2]
+        return bl + [b for b1, b2, _, _ in self.ups for b in (b1, b2)] + [self.final_res_block]
 
     def _resample(self, x, m):
         if isinstance(m, nn.Conv2d):
@@ -295,23 +298,24 @@ class Unet(nn.Module):
         x = ops.conv2d(x, self.init_conv)
         r = x
         t = self._time(time)
+        ss = iter(ops.resnet_scale_shifts(t, self._resnet_blocks()))    # all blocks' Linear(SiLU(t))
         h = []
         for b1, b2, attn, down in self.downs:
-            x = b1(x, t)
+            x = b1(x, t, scale_shift=next(ss))
             h.append(x)
-            x = b2(x, t)
+            x = b2(x, t, scale_shift=next(ss))
             x = attn(x)                       # attn(x) + x
             h.append(x)
             x = self._resample(x, down)
-        x = self.mid_block1(x, t)
+        x = self.mid_block1(x, t, scale_shift=next(ss))
         x = self.mid_attn(x)
-        x = self.mid_block2(x, t)
+        x = self.mid_block2(x, t, scale_shift=next(ss))
         for b1, b2, attn, up in self.ups:
-            x = b1(x, t, skip=h.pop())        # cat((x, skip)) folded into the conv gather
-            x = b2(x, t, skip=h.pop())
+            x = b1(x, t, skip=h.pop(), scale_shift=next(ss))   # cat((x, skip)) folded into the conv gather
+            x = b2(x, t, skip=h.pop(), scale_shift=next(ss))
             x = attn(x)
             x = self._resample(x, up)
-        x = self.final_res_block(x, t, skip=r)
+        x = self.final_res_block(x, t, skip=r, scale_shift=next(ss))
         return ops.conv2d(x, self.final_conv)
 
 

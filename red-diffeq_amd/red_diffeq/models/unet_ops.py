@@ -50,6 +50,22 @@ def linear(x, lin, act_in=0, act_out=0):
     return torch.ops.red_diffeq.linear(x, lin.weight, lin.bias, act_in, act_out)
 
 
+def time_mlp(t, seq):
+    """Unet.time_mlp = Sequential(SinusoidalPosEmb, Linear, GELU, Linear) in one launch."""
+    return torch.ops.red_diffeq.time_mlp(t, seq[0].dim, float(seq[0].theta), seq[1].weight, seq[1].bias,
+                                         seq[3].weight, seq[3].bias)
+
+
+def resnet_scale_shifts(t, blocks):
+    """Every ResnetBlock's Linear(SiLU(t)) (B, 2C) in one launch (at most 32 per call)."""
+    out = []
+    for i in range(0, len(blocks), 32):
+        chunk = blocks[i:i + 32]
+        out += torch.ops.red_diffeq.linear_silu_multi(t, [b.mlp[1].weight for b in chunk],
+                                                      [b.mlp[1].bias for b in chunk])
+    return out
+
+
 def sinusoidal(t, dim, theta=10000):
     return torch.ops.red_diffeq.sinusoidal_emb(t, dim, float(theta))
 
@@ -101,6 +117,6 @@ def red_epilogue(diff, xt, t, eps_hat, eps):
                                         diff.sqrt_recipm1_alphas_cumprod)
 
 
-HIP_OPS = {"conv2d", "conv_group_norm_silu", "linear", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+HIP_OPS = {"conv2d", "conv_group_norm_silu", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
            "full_attention", "red_q_sample", "red_epilogue"}
 del math

@@ -15,8 +15,8 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
-    conv2d_mfma, conv2d_gn_silu, gn_silu, rmsnorm, linear, sinusoidal_emb, linear_attn, attn, red_q_sample,
-    red_eps
+    conv2d_mfma, conv2d_gn_silu, gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb,
+    linear_attn, attn, red_q_sample, red_eps
   loop (include/red_diffeq_loop.h)
     l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
 
@@ -24,7 +24,7 @@ No CPU implementation is registered: a CPU tensor reaching an op raises (no fall
 """
 import ctypes
 import weakref
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -410,6 +410,48 @@ def _(x, weight, bias, act_in, act_out):
     return x.new_empty(x.shape[0], weight.shape[0])
 
 
+@torch.library.custom_op(f"{LIB}::time_mlp", mutates_args=())
+def time_mlp(t: Tensor, dim: int, theta: float, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor) -> Tensor:
+    """Unet.time_mlp (diffusion.py:255-258): Linear(GELU(Linear(SinusoidalPosEmb(t)))), one launch."""
+    _hip.require_device(t)
+    t = t.to(torch.int64).contiguous()
+    hid, out = w1.shape[0], w2.shape[0]
+    y = torch.empty(t.shape[0], out, device=t.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_time_mlp(t.shape[0], dim, float(theta), _hip.ptr(t), _hip.ptr(w1.contiguous()),
+                                       _hip.ptr(b1), hid, _hip.ptr(w2.contiguous()), _hip.ptr(b2), out, _hip.ptr(y),
+                                       _hip.stream_of(t)), "rdq_time_mlp")
+    return y
+
+
+@time_mlp.register_fake
+def _(t, dim, theta, w1, b1, w2, b2):
+    return t.new_empty(t.shape[0], w2.shape[0], dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::linear_silu_multi", mutates_args=())
+def linear_silu_multi(x: Tensor, weights: List[Tensor], biases: List[Tensor]) -> List[Tensor]:
+    """[Linear_j(SiLU(x)) for j]: every ResnetBlock's time MLP (diffusion.py:157-165), one launch
+    (at most 32 linears sharing x)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    n = len(weights)
+    B, fin = x.shape
+    ys = [torch.empty(B, w.shape[0], device=x.device, dtype=torch.float32) for w in weights]
+    ws = [w.contiguous() for w in weights]
+    W = (ctypes.c_void_p * n)(*[_hip.ptr(w) for w in ws])
+    Bs = (ctypes.c_void_p * n)(*[_hip.ptr(b) for b in biases])
+    O = (ctypes.c_int32 * n)(*[w.shape[0] for w in ws])
+    Y = (ctypes.c_void_p * n)(*[_hip.ptr(y) for y in ys])
+    _hip.check(_hip.lib().rdq_linear_silu_multi(B, fin, _hip.ptr(x), n, W, Bs, O, Y, _hip.stream_of(x)),
+               "rdq_linear_silu_multi")
+    return ys
+
+
+@linear_silu_multi.register_fake
+def _(x, weights, biases):
+    return [x.new_empty(x.shape[0], w.shape[0]) for w in weights]
+
+
 @torch.library.custom_op(f"{LIB}::sinusoidal_emb", mutates_args=())
 def sinusoidal_emb(t: Tensor, dim: int, theta: float) -> Tensor:
     _hip.require_device(t)
@@ -614,7 +656,8 @@ def _forward_only(op, name):
 
 
 for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_gn_silu, "conv2d_gn_silu"), (gn_silu, "gn_silu"),
-                   (rmsnorm, "rmsnorm"), (linear, "linear"),
+                   (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
+                   (linear_silu_multi, "linear_silu_multi"),
                    (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (attn, "attn"),
                    (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
     _forward_only(_op, _name)

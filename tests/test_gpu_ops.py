@@ -80,6 +80,8 @@ def test_unet_and_loop_ops_opcheck(cuda):
     opcheck(ops.rmsnorm, (x, r(1, 16, 1, 1), x))
     opcheck(ops.linear, (r(2, 32), r(64, 32), r(64), 1, 1))
     opcheck(ops.sinusoidal_emb, (torch.tensor([3, 900], device=cuda), 16, 10000.0))
+    opcheck(ops.time_mlp, (torch.tensor([3, 900], device=cuda), 16, 10000.0, r(64, 16), r(64), r(64, 64), r(64)))
+    opcheck(ops.linear_silu_multi, (r(2, 64), [r(32, 64), r(128, 64)], [r(32), r(128)]))
     opcheck(ops.linear_attn, (r(2, 3 * 4 * 8, 6, 6), r(2, 4, 8, 4), 4, 8 ** -0.5))
     opcheck(ops.attn, (r(2, 3 * 2 * 32, 3, 3), r(2, 2, 4, 32), 2))             # dim_head 32 (the U-Net)
     sa, s1 = torch.rand(1000, device=cuda) + 0.1, torch.rand(1000, device=cuda) + 0.1
@@ -107,7 +109,8 @@ def test_unet_dispatches_through_ops(cuda):
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
         y = net(x, t)                 # grad enabled: the eager path (no hipGraph replay)
     names = {e.name for e in prof.events()}
-    for op in ("conv2d_mfma", "conv2d_gn_silu", "gn_silu", "rmsnorm", "linear", "sinusoidal_emb", "linear_attn", "attn"):
+    for op in ("conv2d_mfma", "conv2d_gn_silu", "gn_silu", "rmsnorm", "time_mlp", "linear_silu_multi", "linear_attn",
+               "attn"):
         assert f"red_diffeq::{op}" in names, op
     with pytest.raises(RuntimeError, match="no backward"):
         y.sum().backward()

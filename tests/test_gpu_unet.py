@@ -6,6 +6,8 @@ Tolerances: fp32 with a different summation order (MFMA k-order vs MIOpen / CPU 
 per-op max-abs <= 2e-5 x scale; whole U-Net <= 2e-4 relative to the output range.
 The reference fixtures are "parity unpinned" at Attend (denoising-diffusion-pytorch 2.1.1 is not
 installed; its flash=False math is restated)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -152,6 +154,28 @@ def test_rmsnorm_linear_sinusoidal(cuda):
     f = torch.exp(torch.arange(half, device=cuda) * -emb)
     ref = torch.cat(((t[:, None] * f).sin(), (t[:, None] * f).cos()), -1)
     close(ops.sinusoidal(t, 64), ref, rel=1e-4)
+
+
+def test_time_mlp_and_scale_shifts(cuda):
+    """Unet.time_mlp in one launch and every ResnetBlock's Linear(SiLU(t)) in one launch vs torch."""
+    from red_diffeq.models.diffusion import Unet
+    from red_diffeq.models import unet_ops as ops
+    import torch.nn.functional as F
+    torch.manual_seed(7)
+    net = Unet(dim=16, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    t = torch.tensor([0, 17, 803, 999], device=cuda)
+    with torch.no_grad():
+        te = ops.time_mlp(t, net.time_mlp)
+        half = 8
+        f = torch.exp(torch.arange(half, device=cuda) * -(math.log(10000) / (half - 1)))
+        emb = torch.cat(((t[:, None] * f).sin(), (t[:, None] * f).cos()), -1)
+        ref = net.time_mlp[3](F.gelu(net.time_mlp[1](emb)))
+        close(te, ref, rel=1e-4)
+        blocks = net._resnet_blocks()
+        ss = ops.resnet_scale_shifts(te, blocks)
+        assert len(ss) == len(blocks) == 19
+        for b, s in zip(blocks, ss):
+            close(s, b.mlp[1](F.silu(te)))
 
 
 @pytest.mark.parametrize("C,H", [(64, 72), (128, 18)])
