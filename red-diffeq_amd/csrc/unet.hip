@@ -221,6 +221,7 @@ struct CcArgs {
     unsigned *tickets;        // S > 1: one per (m tile, n tile)
     double *gnp;              // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
     int K, M, HW, nstages, per_split, S, G;
+    int xbytes, x2bytes, wbytes;   // buffer extents (< 2^31: cc_ok)
 };
 
 template <int TAPS, int MODE>
@@ -242,62 +243,63 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
     const bool pv = gm < a.M;
     const int gb = pv ? gm / a.HW : 0, gpix = pv ? gm - gb * a.HW : 0;
     const int oh = gpix / d.W, ow = gpix - oh * d.W;
-    int off[TAPS];
-    unsigned vmask = 0;
+    // every load is a buffer load: a per-lane byte offset fixed for the launch (sample, channel
+    // lane, tap; padding taps get an offset past the buffer, which loads 0) plus a wave-uniform
+    // per-stage channel offset, so a stage issues its loads with no address arithmetic
+    constexpr int OOB_OFF = (int)0x80000000u;
+    const int plane = MODE == RDQ_IN_UPSAMPLE2 ? (d.H >> 1) * (d.W >> 1)
+                    : MODE == RDQ_IN_UNSHUFFLE2 ? 4 * a.HW : a.HW;
+    const int cin1 = MODE == RDQ_IN_UNSHUFFLE2 ? d.cin1 >> 2 : d.cin1;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.x), (short)0,
+                                                                        a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.x2 ? a.x2 : a.x),
+                                                                         (short)0, a.x2bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.w), (short)0,
+                                                                         a.wbytes, 0x00020000);
+    int vo1[NA], vo2[NA];
     if constexpr (TAPS == 9) {
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int ih = oh + t / 3 - d.pad, iw = ow + t % 3 - d.pad;
             const bool ok = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-            vmask |= (ok ? 1u : 0u) << t;
-            off[t] = !ok ? 0 : MODE == RDQ_IN_UPSAMPLE2 ? (ih >> 1) * (d.W >> 1) + (iw >> 1) : ih * d.W + iw;
+            const int o = MODE == RDQ_IN_UPSAMPLE2 ? (ih >> 1) * (d.W >> 1) + (iw >> 1) : ih * d.W + iw;
+            vo1[t] = ok ? ((gb * cin1 + cl) * plane + o) * 4 : OOB_OFF;
+            vo2[t] = ok ? ((gb * d.cin2 + cl) * a.HW + o) * 4 : OOB_OFF;
         }
     } else {
-        vmask = pv ? 1u : 0u;
-        off[0] = MODE == RDQ_IN_UNSHUFFLE2 ? (2 * oh) * (2 * d.W) + 2 * ow : gpix;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = cl + 8 * j;                 // channel within the 64-channel stage
+            if constexpr (MODE == RDQ_IN_UNSHUFFLE2) {
+                const int o = (2 * oh + ((c >> 1) & 1)) * (2 * d.W) + 2 * ow + (c & 1);
+                vo1[j] = pv ? ((gb * cin1 + (c >> 2)) * plane + o) * 4 : OOB_OFF;
+            } else {
+                vo1[j] = pv ? ((gb * cin1 + c) * plane + gpix) * 4 : OOB_OFF;
+            }
+            vo2[j] = pv ? ((gb * d.cin2 + c) * a.HW + gpix) * 4 : OOB_OFF;
+        }
     }
-    const size_t plane = MODE == RDQ_IN_UPSAMPLE2 ? (size_t)(d.H >> 1) * (d.W >> 1)
-                       : MODE == RDQ_IN_UNSHUFFLE2 ? (size_t)4 * a.HW : (size_t)a.HW;
-    const int cin1 = MODE == RDQ_IN_UNSHUFFLE2 ? d.cin1 >> 2 : d.cin1;
-    const float *xb = a.x + (size_t)gb * cin1 * plane;
-    const float *x2b = a.x2 ? a.x2 + (size_t)gb * d.cin2 * a.HW : a.x;
     // weight role: quad q of row n for idx = tid + 256 r (rows past cout clamped: their outputs are
     // never stored; idx past the tile only loads, never stashes)
-    int woff[NWQ];
+    int vw[NWQ];
 #pragma unroll
     for (int r = 0; r < NWQ; ++r) {
         const int idx = min(tid + 256 * r, CC_BN * QPR - 1);
         const int n = idx / QPR, q = idx - n * QPR;
-        woff[r] = min(n0 + n, N - 1) * K + q * 4;
+        vw[r] = (min(n0 + n, N - 1) * K + q * 4) * 4;
     }
     auto load = [&](int s, float (&ra)[NA], f32x4 (&rw)[NWQ]) {
-        if constexpr (TAPS == 9) {
-            const int ci = s * C::CPS + cl;
-            const float *src = ci < d.cin1 ? xb + (size_t)ci * plane : x2b + (size_t)(ci - d.cin1) * a.HW;
+        // stage s = channels [s*CPS, (s+1)*CPS): all in x or all in x2 (cin1 % CPS == 0)
+        const int c0 = s * C::CPS;
+        const bool first = c0 < d.cin1;
+        const int soff = first ? (MODE == RDQ_IN_UNSHUFFLE2 ? (c0 >> 2) : c0) * plane * 4 : (c0 - d.cin1) * a.HW * 4;
+        const __amdgpu_buffer_rsrc_t rs = first ? rx : rx2;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const float v = src[off[t]];
-                ra[t] = (vmask >> t) & 1u ? v : 0.0f;
-            }
-        } else {
+        for (int t = 0; t < NA; ++t)
+            ra[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, first ? vo1[t] : vo2[t], soff, 0));
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int ci = s * C::CPS + cl + 8 * j;
-                const float *src;
-                int o = off[0];
-                if constexpr (MODE == RDQ_IN_UNSHUFFLE2) {
-                    src = xb + (size_t)(ci >> 2) * plane;
-                    o += ((ci >> 1) & 1) * (2 * d.W) + (ci & 1);
-                } else {
-                    src = ci < d.cin1 ? xb + (size_t)ci * plane : x2b + (size_t)(ci - d.cin1) * a.HW;
-                }
-                const float v = src[o];
-                ra[j] = vmask ? v : 0.0f;
-            }
-        }
-        const float *ws = a.w + (size_t)s * BK;
-#pragma unroll
-        for (int r = 0; r < NWQ; ++r) rw[r] = *reinterpret_cast<const f32x4 *>(ws + woff[r]);
+        for (int r = 0; r < NWQ; ++r)
+            rw[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwt, vw[r], s * BK * 4, 0));
     };
     auto stash = [&](int buf, const float (&ra)[NA], const f32x4 (&rw)[NWQ]) {
         if constexpr (TAPS == 9) {
@@ -543,7 +545,19 @@ bool cc_ok(const rdq_conv_desc *d)
     const int cps = d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS;
     if (d->kh == 1 && d->pad != 0) return false;
     if (d->in_mode == RDQ_IN_UNSHUFFLE2 && d->kh != 1) return false;
-    return d->cin1 % cps == 0 && d->cin2 % cps == 0 && cin % 4 == 0;
+    if (d->cin1 % cps || d->cin2 % cps || cin % 4) return false;
+    const int64_t lim = INT32_MAX;                 // buffer-load extents and offsets are 32-bit
+    const int64_t xy = (int64_t)d->B * d->H * d->W * 4;
+    return xy * d->cin1 < lim && xy * d->cin2 < lim && (int64_t)d->cout * cin * d->kh * d->kw * 4 < lim &&
+           xy * d->cout < lim;
+}
+
+void cc_extents(CcArgs &c, const rdq_conv_desc *d)
+{
+    const int64_t xy = (int64_t)d->B * d->H * d->W * 4;
+    c.xbytes = (int)(d->in_mode == RDQ_IN_UPSAMPLE2 ? xy / 4 * d->cin1 : xy * d->cin1);
+    c.x2bytes = (int)(xy * d->cin2);
+    c.wbytes = (int)((int64_t)d->cout * c.K * 4);
 }
 
 // splits: fill the chip with about one workgroup per CU (a second workgroup on a CU only shares its
@@ -867,9 +881,10 @@ __global__ void k_sinusoidal(int dim, float neg_emb, const int64_t *__restrict__
     y[(size_t)b * dim + half + i] = cosf(arg);
 }
 
-// Unet.time_mlp in one launch: SinusoidalPosEmb -> Linear -> GELU -> Linear, one workgroup per
-// sample, one wave per output row (the arithmetic of k_sinusoidal and k_linear, element for element)
-constexpr int TM_T = 1024;
+// Unet.time_mlp in one launch: SinusoidalPosEmb -> Linear -> GELU -> Linear.  Workgroup (row block,
+// sample): every workgroup forms the embedding and the whole hidden layer (a thread per hidden row,
+// its weight row loaded as float4s), then four output rows (a wave each)
+constexpr int TM_ROWS = 4;
 // the weight loads of 256 inputs are issued together (a dependent chain of loads would pay the
 // memory latency once per 64 inputs); products accumulated in input order as in k_linear
 __device__ __forceinline__ float wave_dot(const float *__restrict__ w, const float *x, int in, int lane, bool silu)
@@ -892,47 +907,44 @@ __device__ __forceinline__ float wave_dot(const float *__restrict__ w, const flo
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     return s;
 }
-__global__ __launch_bounds__(TM_T) void k_time_mlp(int dim, float neg_emb, const int64_t *__restrict__ t,
-                                                   const float *__restrict__ w1, const float *__restrict__ b1, int hid,
-                                                   const float *__restrict__ w2, const float *__restrict__ b2, int out,
-                                                   float *__restrict__ y)
+__global__ __launch_bounds__(256) void k_time_mlp(int dim, float neg_emb, const int64_t *__restrict__ t,
+                                                  const float *__restrict__ w1, const float *__restrict__ b1, int hid,
+                                                  const float *__restrict__ w2, const float *__restrict__ b2, int out,
+                                                  float *__restrict__ y)
 {
     extern __shared__ float tm_sm[];
     float *e = tm_sm, *h = tm_sm + dim;
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = TM_T / 64;
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = dim / 2;
-    if (tid < half) {
-        const float f = expf((float)tid * neg_emb);
+    for (int i = tid; i < half; i += 256) {
+        const float f = expf((float)i * neg_emb);
         const float arg = (float)t[b] * f;
-        e[tid] = sinf(arg);
-        e[half + tid] = cosf(arg);
+        e[i] = sinf(arg);
+        e[half + i] = cosf(arg);
     }
     __syncthreads();
-    // four output rows per wave at a time (their weight loads in flight together)
-    for (int o0 = wv; o0 < hid; o0 += 4 * nw) {
-        float r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = wave_dot(w1 + (size_t)min(o0 + u * nw, hid - 1) * dim, e, dim, lane, false);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int o = o0 + u * nw;
-            if (lane == 0 && o < hid) {
-                const float v = r[u] + b1[o];
-                h[o] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    for (int o = tid; o < hid; o += 256) {
+        const float *wr = w1 + (size_t)o * dim;
+        float s = 0.0f;
+        if ((dim & 3) == 0) {
+            for (int i = 0; i < dim; i += 4) {
+                const float4 w4 = *reinterpret_cast<const float4 *>(wr + i);
+                s += w4.x * e[i];
+                s += w4.y * e[i + 1];
+                s += w4.z * e[i + 2];
+                s += w4.w * e[i + 3];
             }
+        } else {
+            for (int i = 0; i < dim; ++i) s += wr[i] * e[i];
         }
+        const float v = s + b1[o];
+        h[o] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
     }
     __syncthreads();
-    for (int o0 = wv; o0 < out; o0 += 4 * nw) {
-        float r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = wave_dot(w2 + (size_t)min(o0 + u * nw, out - 1) * hid, h, hid, lane, false);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int o = o0 + u * nw;
-            if (lane == 0 && o < out) y[(size_t)b * out + o] = r[u] + b2[o];
-        }
-    }
+    const int o = blockIdx.x * TM_ROWS + wv;
+    if (o >= out) return;
+    const float s = wave_dot(w2 + (size_t)o * hid, h, hid, lane, false);
+    if (lane == 0) y[(size_t)b * out + o] = s + b2[o];
 }
 
 // every ResnetBlock's time MLP, Linear(SiLU(t)) (diffusion.py:157-165), in one launch: up to
@@ -1743,6 +1755,7 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         c.K = (d->cin1 + d->cin2) * d->kh * d->kw;
         c.HW = d->H * d->W;
         c.M = d->B * c.HW;
+        cc_extents(c, d);
         c.nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
         c.S = ws ? cc_splits(d, ws_bytes, &c.per_split) : 1;
         if (c.S == 1) c.per_split = c.nstages;
@@ -1827,6 +1840,7 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     c.K = (d->cin1 + d->cin2) * d->kh * d->kw;
     c.HW = d->H * d->W;
     c.M = (int)M;
+    cc_extents(c, d);
     c.nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
     c.S = (slabs && tickets) ? cc_splits(d, slabs, &c.per_split) : 1;   // statistics need the in-launch combine
     if (c.S == 1) c.per_split = c.nstages;
@@ -1986,13 +2000,13 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
 int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid,
                  const float *w2, const float *b2, int32_t out, float *y, hipStream_t st)
 {
-    if (B < 1 || dim < 4 || dim % 2 || dim / 2 > TM_T || hid < 1 || out < 1 || (size_t)(dim + hid) * 4 > 64 * 1024 ||
+    if (B < 1 || dim < 4 || dim % 2 || hid < 1 || out < 1 || (size_t)(dim + hid) * 4 > 64 * 1024 ||
         !t || !w1 || !b1 || !w2 || !b2 || !y)
         return RDQ_E_INVALID;
     const int half = dim / 2;
     const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
-    hipLaunchKernelGGL(k_time_mlp, dim3(B), dim3(TM_T), (dim + hid) * sizeof(float), st, dim, -emb, t, w1, b1, hid, w2,
-                       b2, out, y);
+    hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float), st,
+                       dim, -emb, t, w1, b1, hid, w2, b2, out, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
