@@ -207,6 +207,16 @@ __global__ __launch_bounds__(256) void k_conv_reduce(int S, int64_t total, int N
 // per tile, then the slabs summed in slab order, then bias and residual: the arithmetic of
 // k_conv_reduce, bit for bit) instead of a separate launch.  Tickets are zero before the launch and
 // returned to zero by the combining workgroup.
+// GroupNorm-normalised value -> affine -> time scale/shift -> SiLU (Block.forward, diffusion.py:142-149)
+__device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float ga, float be, bool sso, float sc1,
+                                          float sh)
+{
+    float v = (x - mean) * rstd;
+    v = v * ga + be;
+    if (sso) v = v * sc1 + sh;
+    return v / (1.0f + expf(-v));
+}
+
 template <int TAPS> struct CcCfg;
 template <> struct CcCfg<9> { static constexpr int CPS = 8, BK = 72, NA = 9, QPR = 18, NWQ = 5; };
 template <> struct CcCfg<1> { static constexpr int CPS = 64, BK = 64, NA = 8, QPR = 16, NWQ = 4; };
@@ -650,14 +660,6 @@ __global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gs
 // y = SiLU(((x - mean) rstd gamma + beta) (scale + 1) + shift), one workgroup per (channel row,
 // 1024-element chunk; the pass is VALU-bound on the exact expf and division of SiLU): the channel's constants are wave-uniform, four elements per lane (float4
 // where the row allows it); the operation order is the per-element formula's
-__device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float ga, float be, bool sso, float sc1,
-                                          float sh)
-{
-    float v = (x - mean) * rstd;
-    v = v * ga + be;
-    if (sso) v = v * sc1 + sh;
-    return v / (1.0f + expf(-v));
-}
 // stat == nullptr (small grids, where one more launch costs more than the arithmetic): every
 // workgroup derives its group's statistics from the chunk partials itself
 __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch, const float *__restrict__ x,
@@ -803,42 +805,45 @@ __global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm(int C, int HW, const flo
     }
 }
 
-// the same with the thread's NPT = ceil(C / RMS_G) channels held in registers between the two passes
+// the same with the thread's NPT = ceil(C / G) channels held in registers between the two passes
 // (one HBM read of x), loads issued together at clamped indices (no per-element branch), the
-// residual loaded before the first store; sums in the same channel order as above
-template <int NPT>
-__global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm_r(int C, int HW, const float *__restrict__ x,
-                                                          const float *__restrict__ g, const float *__restrict__ res,
-                                                          float *__restrict__ y)
+// residual loaded before the first store.  Workgroup = PX pixels x G = 1024 / PX channel groups:
+// small images (the 9x9 / 18x18 levels) take narrow pixel blocks so that more than a couple of
+// workgroups share the work and NPT stays small
+template <int NPT, int PX>
+__global__ __launch_bounds__(1024) void k_rmsnorm_r(int C, int HW, const float *__restrict__ x,
+                                                    const float *__restrict__ g, const float *__restrict__ res,
+                                                    float *__restrict__ y)
 {
-    __shared__ float part[RMS_G][64];
-    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int pix = blockIdx.x * 64 + lane, b = blockIdx.y;
+    constexpr int G = 1024 / PX;
+    __shared__ float part[G][PX];
+    const int lane = threadIdx.x % PX, grp = threadIdx.x / PX;
+    const int pix = blockIdx.x * PX + lane, b = blockIdx.y;
     const bool ok = pix < HW;
     const size_t base = (size_t)b * C * HW + min(pix, HW - 1);
     float v[NPT];
 #pragma unroll
-    for (int i = 0; i < NPT; ++i) v[i] = x[base + (size_t)min(grp + i * RMS_G, C - 1) * HW];
+    for (int i = 0; i < NPT; ++i) v[i] = x[base + (size_t)min(grp + i * G, C - 1) * HW];
     float ssum = 0.0f;
 #pragma unroll
     for (int i = 0; i < NPT; ++i)
-        if (grp + i * RMS_G < C) ssum += v[i] * v[i];
+        if (grp + i * G < C) ssum += v[i] * v[i];
     part[grp][lane] = ssum;
     __syncthreads();
     float tot = 0.0f;
-#pragma unroll
-    for (int i = 0; i < RMS_G; ++i) tot += part[i][lane];
+#pragma unroll 8
+    for (int i = 0; i < G; ++i) tot += part[i][lane];
     float r[NPT] = {};
     if (res) {
 #pragma unroll
-        for (int i = 0; i < NPT; ++i) r[i] = res[base + (size_t)min(grp + i * RMS_G, C - 1) * HW];
+        for (int i = 0; i < NPT; ++i) r[i] = res[base + (size_t)min(grp + i * G, C - 1) * HW];
     }
     if (!ok) return;
     const float den = fmaxf(sqrtf(tot), 1e-12f);      // F.normalize: x / max(||x||, eps)
     const float sc = sqrtf((float)C);
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-        const int c = grp + i * RMS_G;
+        const int c = grp + i * G;
         if (c >= C) break;
         float o = v[i] / den;
         o = o * g[c];
@@ -846,6 +851,19 @@ __global__ __launch_bounds__(64 * RMS_G) void k_rmsnorm_r(int C, int HW, const f
         if (res) o = o + r[i];
         y[base + (size_t)c * HW] = o;
     }
+}
+
+template <int PX>
+bool launch_rmsnorm_r(int B, int C, int HW, const float *x, const float *g, const float *res, float *y, hipStream_t st)
+{
+    constexpr int G = 1024 / PX;
+    const dim3 grid((HW + PX - 1) / PX, B), blk(1024);
+    if (C <= 2 * G) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rmsnorm_r<2, PX>), grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 4 * G) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rmsnorm_r<4, PX>), grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 8 * G) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rmsnorm_r<8, PX>), grid, blk, 0, st, C, HW, x, g, res, y);
+    else if (C <= 16 * G) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rmsnorm_r<16, PX>), grid, blk, 0, st, C, HW, x, g, res, y);
+    else return false;
+    return true;
 }
 
 // ------------------------------------------------------------------------------------ linear
@@ -987,15 +1005,27 @@ __global__ __launch_bounds__(256) void k_la_ctx(int heads, int dh, int n, int nm
     const float *vb = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
     const float *mk = mem + (size_t)(0 * heads + h) * dh * nmem;
     const float *mv = mem + (size_t)(1 * heads + h) * dh * nmem;
-    for (int i = tid; i < dh * LA_CH; i += 256) {
-        const int d = i / LA_CH, jj = i - d * LA_CH, j = j0 + jj;
-        float kv = -INFINITY, vv = 0.0f;
-        if (j < nk) {
-            kv = j < nmem ? mk[(size_t)d * nmem + j] : kb[(size_t)d * n + (j - nmem)];
-            vv = j < nmem ? mv[(size_t)d * nmem + j] : vb[(size_t)d * n + (j - nmem)];
+    {
+        // thread = token j0 + tid: its dh keys and values (stride n, or nmem for memory tokens)
+        // loaded together, then staged as rows d of P and V
+        const int j = j0 + tid;
+        const bool in = j < nk, memtok = j < nmem;
+        const float *kp = memtok ? mk + j : kb + (in ? j - nmem : 0);
+        const float *vp = memtok ? mv + j : vb + (in ? j - nmem : 0);
+        const int stride = memtok ? nmem : n;
+        float kr[32], vr[32];
+#pragma unroll
+        for (int d = 0; d < 32; ++d) {
+            const int dd = min(d, dh - 1);
+            kr[d] = kp[(size_t)dd * stride];
+            vr[d] = vp[(size_t)dd * stride];
         }
-        P[d][jj] = kv;
-        V[d][jj] = vv;                                           // row d of V = value channel e = d
+#pragma unroll
+        for (int d = 0; d < 32; ++d)
+            if (d < dh) {
+                P[d][tid] = in ? kr[d] : -INFINITY;
+                V[d][tid] = in ? vr[d] : 0.0f;                   // row d of V = value channel e = d
+            }
     }
     __syncthreads();
     // row maxima and exp / sums: 8 threads per row d, 32 tokens each, fixed xor trees
@@ -1064,19 +1094,38 @@ __global__ __launch_bounds__(256) void k_la_reduce(int BHDD, int dh, int nch, co
     if (i >= BHDD) return;
     const int row = i / dh;                                      // (b, h, d)
     const int BHD = BHDD / dh;
+    // chunk statistics and partials read in groups of 8 (loads in flight together), combined in order
     float M = -INFINITY;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, pstat[((size_t)c * BHD + row) * 2]);
+    for (int c0 = 0; c0 < nch; c0 += 8) {
+        float mv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mv[u] = pstat[((size_t)min(c0 + u, nch - 1) * BHD + row) * 2];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) M = fmaxf(M, mv[u]);
+    }
     float num = 0.0f, den = 0.0f;
-    for (int c = 0; c < nch; ++c) {
-        const float f = expf(pstat[((size_t)c * BHD + row) * 2] - M);
-        num += f * part[(size_t)c * BHDD + i];
-        den += f * pstat[((size_t)c * BHD + row) * 2 + 1];
+    for (int c0 = 0; c0 < nch; c0 += 8) {
+        float mv[8], sv[8], pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int c = min(c0 + u, nch - 1);
+            mv[u] = pstat[((size_t)c * BHD + row) * 2];
+            sv[u] = pstat[((size_t)c * BHD + row) * 2 + 1];
+            pv[u] = part[(size_t)c * BHDD + i];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (c0 + u < nch) {
+                const float f = expf(mv[u] - M);
+                num += f * pv[u];
+                den += f * sv[u];
+            }
     }
     ctx[i] = num / den;
 }
 
-// per (b, h, pixel): ctx = (sum of chunk partials in order) / sum_d; q softmax over d, scale,
-// out[e] = sum_d ctx[d][e] q[d]
+// per (b, h, pixel): q softmax over d, scale, out[e] = sum_d ctx[d][e] q[d].  Workgroup = 64 pixels
+// x 4 quarters of the 32 output channels e (a thread forms the softmax of its pixel and 8 outputs)
 __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float scale,
                                                 const float *__restrict__ qkv, const float *__restrict__ ctx,
                                                 float *__restrict__ out)
@@ -1090,8 +1139,9 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
         cs[d][i - d * dh] = cb[i];
     }
     __syncthreads();
-    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pix >= n) return;
+    const int px = threadIdx.x & 63, eq = threadIdx.x >> 6;
+    const int pix = blockIdx.x * 64 + px;
+    if (pix >= n || eq * 8 >= dh) return;
     const float *q = qkv + ((size_t)b * 3 * C + h * dh) * n + pix;
     float qv[32];
     float mx = -INFINITY;
@@ -1104,15 +1154,15 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
     for (int d = 0; d < 32; ++d) if (d < dh) { qv[d] = expf(qv[d] - mx); sm += qv[d]; }
 #pragma unroll
     for (int d = 0; d < 32; ++d) if (d < dh) qv[d] = (qv[d] / sm) * scale;
-    float o[32];
+    float o[8];
 #pragma unroll
-    for (int e = 0; e < 32; ++e) o[e] = 0.0f;
+    for (int e = 0; e < 8; ++e) o[e] = 0.0f;
 #pragma unroll
     for (int d = 0; d < 32; ++d) {
         if (d < dh) {
 #pragma unroll
-            for (int e4 = 0; e4 < 8; ++e4) {
-                const f32x4 c4 = *reinterpret_cast<const f32x4 *>(&cs[d][e4 * 4]);
+            for (int e4 = 0; e4 < 2; ++e4) {
+                const f32x4 c4 = *reinterpret_cast<const f32x4 *>(&cs[d][eq * 8 + e4 * 4]);
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) o[e4 * 4 + q4] += c4[q4] * qv[d];
             }
@@ -1120,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
     }
     float *ob = out + ((size_t)b * C + h * dh) * n + pix;
 #pragma unroll
-    for (int e = 0; e < 32; ++e) if (e < dh) ob[(size_t)e * n] = o[e];
+    for (int e = 0; e < 8; ++e) if (eq * 8 + e < dh) ob[(size_t)(eq * 8 + e) * n] = o[e];
 }
 
 // ---------------------------------------------------------------------------- full attention
@@ -1968,12 +2018,10 @@ int rdq_rmsnorm(int32_t B, int32_t C, int32_t HW, const float *x, const float *g
                 hipStream_t st)
 {
     if (B < 1 || C < 1 || HW < 1 || !x || !g || !y) return RDQ_E_INVALID;
-    const dim3 grid((HW + 63) / 64, B), blk(64 * RMS_G);
-    if (C <= 4 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<4>, grid, blk, 0, st, C, HW, x, g, res, y);
-    else if (C <= 8 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<8>, grid, blk, 0, st, C, HW, x, g, res, y);
-    else if (C <= 16 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<16>, grid, blk, 0, st, C, HW, x, g, res, y);
-    else if (C <= 32 * RMS_G) hipLaunchKernelGGL(k_rmsnorm_r<32>, grid, blk, 0, st, C, HW, x, g, res, y);
-    else hipLaunchKernelGGL(k_rmsnorm, grid, blk, 0, st, C, HW, x, g, res, y);
+    const bool done = HW >= 2048 ? launch_rmsnorm_r<64>(B, C, HW, x, g, res, y, st)
+                    : HW >= 256 ? launch_rmsnorm_r<32>(B, C, HW, x, g, res, y, st)
+                                : launch_rmsnorm_r<16>(B, C, HW, x, g, res, y, st);
+    if (!done) hipLaunchKernelGGL(k_rmsnorm, dim3((HW + 63) / 64, B), dim3(64 * RMS_G), 0, st, C, HW, x, g, res, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -2052,7 +2100,7 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
     hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, part, pstat);
     const int bhdd = B * heads * dh * dh;
     hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, pstat, part, ctx);
-    hipLaunchKernelGGL(k_la_out, dim3((n + 255) / 256, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx,
+    hipLaunchKernelGGL(k_la_out, dim3((n + 63) / 64, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx,
                        out);
     RDQ_CHECK(hipGetLastError());
     return 0;
