@@ -715,6 +715,19 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
     const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
     const int c = g * cpg + cl;
+    const size_t base = ((size_t)b * C + c) * HW;
+    // this thread's elements, residual and channel constants are loaded first (independent of the
+    // statistics), so the statistics reduction below overlaps their latency
+    const bool vec = (HW & 3) == 0;
+    const int i4 = (ch * 256 + (int)threadIdx.x) * 4;
+    float4 v = {0.0f, 0.0f, 0.0f, 0.0f}, r = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (vec && i4 < HW) {
+        v = *reinterpret_cast<const float4 *>(x + base + i4);
+        if (post) r = *reinterpret_cast<const float4 *>(post + base + i4);
+    }
+    const float ga = gamma[c], be = beta[c];
+    const bool sso = ss != nullptr;
+    const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
     __shared__ float st2[2];
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -741,30 +754,21 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     }
     __syncthreads();
     const float mean = st2[0], rstd = st2[1];
-    const float ga = gamma[c], be = beta[c];
-    const bool sso = ss != nullptr;
-    const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
-    const size_t base = ((size_t)b * C + c) * HW;
-    if ((HW & 3) == 0) {
-        const int i = (ch * 256 + (int)threadIdx.x) * 4;
-        if (i < HW) {
-            float4 v = *reinterpret_cast<const float4 *>(x + base + i);
+    if (vec) {
+        if (i4 < HW) {
             v.x = gn_silu1(v.x, mean, rstd, ga, be, sso, sc1, sh);
             v.y = gn_silu1(v.y, mean, rstd, ga, be, sso, sc1, sh);
             v.z = gn_silu1(v.z, mean, rstd, ga, be, sso, sc1, sh);
             v.w = gn_silu1(v.w, mean, rstd, ga, be, sso, sc1, sh);
-            if (post) {
-                const float4 r = *reinterpret_cast<const float4 *>(post + base + i);
-                v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-            }
-            *reinterpret_cast<float4 *>(y + base + i) = v;
+            if (post) { v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w; }
+            *reinterpret_cast<float4 *>(y + base + i4) = v;
         }
     } else {
         const int e1 = min(HW, (ch + 1) * 1024);
         for (int i = ch * 1024 + (int)threadIdx.x; i < e1; i += 256) {
-            float v = gn_silu1(x[base + i], mean, rstd, ga, be, sso, sc1, sh);
-            if (post) v += post[base + i];
-            y[base + i] = v;
+            float u = gn_silu1(x[base + i], mean, rstd, ga, be, sso, sc1, sh);
+            if (post) u += post[base + i];
+            y[base + i] = u;
         }
     }
 }
@@ -1134,9 +1138,15 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
     const int C = heads * dh;
     __shared__ __attribute__((aligned(16))) float cs[32][32];
     const float *cb = ctx + (size_t)(b * heads + h) * dh * dh;
-    for (int i = threadIdx.x; i < dh * dh; i += blockDim.x) {
-        const int d = i / dh;
-        cs[d][i - d * dh] = cb[i];
+    {
+        float cv[4];                                             // dh * dh <= 1024: four loads in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cv[u] = cb[min(u * 256 + (int)threadIdx.x, dh * dh - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = u * 256 + (int)threadIdx.x;
+            if (i < dh * dh) cs[i / dh][i % dh] = cv[u];
+        }
     }
     __syncthreads();
     const int px = threadIdx.x & 63, eq = threadIdx.x >> 6;
@@ -1191,18 +1201,27 @@ __global__ __launch_bounds__(256) void k_full_attn(int heads, int n, int nmem, c
     float *Po = Vs + nk * LD;            // [256][LD + 2]: o[0..dh), m, l per (query, split)
     const float *kb = qkv + ((size_t)b * 3 * C + C + h * dh) * n;
     const float *vb = qkv + ((size_t)b * 3 * C + 2 * C + h * dh) * n;
-    for (int i = threadIdx.x; i < nk * dh; i += blockDim.x) {
-        const int j = i / dh, d = i - j * dh;
-        float kv, vv;
-        if (j < nmem) {
-            kv = mem[(((size_t)0 * heads + h) * nmem + j) * dh + d];
-            vv = mem[(((size_t)1 * heads + h) * nmem + j) * dh + d];
-        } else {
-            kv = kb[(size_t)d * n + (j - nmem)];
-            vv = vb[(size_t)d * n + (j - nmem)];
+    // K / V of the head staged 8 elements per thread at a time (loads issued together)
+    for (int i0 = 0; i0 < nk * dh; i0 += 8 * 256) {
+        float kv[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = min(i0 + u * 256 + (int)threadIdx.x, nk * dh - 1);
+            const int j = i / dh, d = i - j * dh;
+            const float *kp = j < nmem ? mem + (((size_t)0 * heads + h) * nmem + j) * dh + d : kb + (size_t)d * n + (j - nmem);
+            const float *vp = j < nmem ? mem + (((size_t)1 * heads + h) * nmem + j) * dh + d : vb + (size_t)d * n + (j - nmem);
+            kv[u] = *kp;
+            vv[u] = *vp;
         }
-        Ks[j * LD + d] = kv;
-        Vs[j * LD + d] = vv;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + (int)threadIdx.x;
+            if (i < nk * dh) {
+                const int j = i / dh, d = i - j * dh;
+                Ks[j * LD + d] = kv[u];
+                Vs[j * LD + d] = vv[u];
+            }
+        }
     }
     __syncthreads();
     const int ql = threadIdx.x % FA_QB, ks = threadIdx.x / FA_QB;
