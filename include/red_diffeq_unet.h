@@ -46,6 +46,13 @@ size_t rdq_conv2d_tickets(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
                const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
 
+/* y = conv2d(RMSNorm(x)) [+ bias] [+ residual] for a 1x1 conv (LinearAttention / Attention to_qkv,
+ * diffusion.py:184-186, 211-213): F.normalize(x, dim=1) * g * sqrt(C) formed as the conv gathers its
+ * operand (per-pixel norms from one pass over the input channels).  1x1, pad 0, no concat, C <= 2048,
+ * channel counts multiples of 64; ws / tickets as rdq_conv2d (rdq_conv2d_ws_bytes). */
+int rdq_conv2d_rms(const rdq_conv_desc *d, const float *x, const float *g, const float *w, const float *bias,
+                   const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
+
 /* Block.forward in two launches (diffusion.py:142-149, + the identity shortcut of 168):
  *   y = SiLU(GroupNorm_G(conv2d(input) + bias) * (scale+1) + shift) [+ post_residual]
  * The conv (channel-chunk form) accumulates the GroupNorm statistics of its output tiles in its

@@ -230,11 +230,12 @@ struct CcArgs {
     float *y, *part;
     unsigned *tickets;        // S > 1: one per (m tile, n tile)
     double *gnp;              // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
+    const float *rms_g;       // RMS: the input is RMSNorm'd per pixel as it is gathered (1x1, no concat)
     int K, M, HW, nstages, per_split, S, G;
     int xbytes, x2bytes, wbytes;   // buffer extents (< 2^31: cc_ok)
 };
 
-template <int TAPS, int MODE>
+template <int TAPS, int MODE, bool RMS = false>
 __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
 {
     using C = CcCfg<TAPS>;
@@ -311,10 +312,47 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
         for (int r = 0; r < NWQ; ++r)
             rw[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwt, vw[r], s * BK * 4, 0));
     };
-    auto stash = [&](int buf, const float (&ra)[NA], const f32x4 (&rw)[NWQ]) {
+    // RMS: per-pixel 1 / max(||x||, eps) from a pass over all input channels (sums of squares per
+    // channel lane in channel order, combined over the 8 lanes in order), g staged in LDS
+    __shared__ float rms_part[RMS ? 8 : 1][CC_BM];
+    __shared__ float rms_gs[RMS ? 2048 : 1];
+    float rms_den = 1.0f;
+    const float rms_sc = RMS ? sqrtf((float)d.cin1) : 1.0f;
+    if constexpr (RMS) {
+        for (int c = tid; c < d.cin1; c += 256) rms_gs[c] = a.rms_g[c];
+        // all of the thread's channels (cl + 8j + 64i, up to 512 input channels) in flight at once;
+        // channels past cin1 read 0 (offset past the buffer)
+        float ssum = 0.0f;
+        for (int c00 = 0; c00 < d.cin1; c00 += 512) {
+            float v[64];
+#pragma unroll
+            for (int k = 0; k < 64; ++k) {
+                const int c0 = c00 + (k >> 3) * 64;
+                v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    rx, vo1[k & 7], c0 < d.cin1 ? c0 * plane * 4 : a.xbytes, 0));
+            }
+#pragma unroll
+            for (int k = 0; k < 64; ++k) ssum += v[k] * v[k];
+        }
+        rms_part[cl][gp] = ssum;
+        __syncthreads();
+        float tot = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) tot += rms_part[k][gp];
+        rms_den = fmaxf(sqrtf(tot), 1e-12f);
+    }
+    auto stash = [&](int buf, int s, const float (&ra)[NA], const f32x4 (&rw)[NWQ]) {
         if constexpr (TAPS == 9) {
 #pragma unroll
             for (int t = 0; t < 9; ++t) As[buf][cl * 9 + t][gp] = ra[t];
+        } else if constexpr (RMS) {
+            // F.normalize(x, dim=1) * g * sqrt(C), the operation order of k_rmsnorm
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v = ra[j] / rms_den;
+                v = v * rms_gs[s * C::CPS + cl + 8 * j];
+                As[buf][cl + 8 * j][gp] = v * rms_sc;
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) As[buf][cl + 8 * j][gp] = ra[j];
@@ -368,12 +406,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
         load(s_begin, ra0, rw0);
         load(min(s_begin + 1, sl), ra1, rw1);
         load(min(s_begin + 2, sl), ra2, rw2);
-        stash(0, ra0, rw0);
+        stash(0, s_begin, ra0, rw0);
         __syncthreads();
         auto step = [&](int i, float (&rl)[NA], f32x4 (&wl)[NWQ], const float (&rs)[NA], const f32x4 (&wsr)[NWQ]) {
             load(min(s_begin + i + 3, sl), rl, wl);
             mma(i & 1);
-            stash((i + 1) & 1, rs, wsr);
+            stash((i + 1) & 1, min(s_begin + i + 1, sl), rs, wsr);
             __syncthreads();
         };
         for (int i = 0;; i += 4) {
@@ -1928,6 +1966,30 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
     hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, gnp, eps, post_residual, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_conv2d_rms(const rdq_conv_desc *d, const float *x, const float *g, const float *w, const float *bias,
+                   const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t st)
+{
+    if (!d || !x || !g || !w || !y || !cc_ok(d) || d->kh != 1 || d->in_mode != RDQ_IN_PLAIN || d->cin2 != 0 ||
+        d->cin1 > 2048)
+        return RDQ_E_INVALID;
+    CcArgs c{};
+    c.d = *d; c.x = x; c.x2 = nullptr; c.w = w; c.bias = bias; c.res = residual; c.y = y;
+    c.part = static_cast<float *>(ws);
+    c.tickets = tickets;
+    c.rms_g = g;
+    c.K = d->cin1;
+    c.HW = d->H * d->W;
+    c.M = d->B * c.HW;
+    cc_extents(c, d);
+    c.nstages = d->cin1 / CcCfg<1>::CPS;
+    c.S = (ws && tickets) ? cc_splits(d, ws_bytes, &c.per_split) : 1;
+    if (c.S == 1) c.per_split = c.nstages;
+    const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN, true>), grid, dim3(256), 0, st, c);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

@@ -74,6 +74,8 @@ SIGNATURES = {
     "rdq_conv2d_tickets": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p, c_void_p]),
+    "rdq_conv2d_rms": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p, c_void_p]),
     "rdq_conv2d_gn_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),
     "rdq_conv2d_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                      c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,

@@ -92,16 +92,24 @@ def rmsnorm(x, g, residual=None):
     return torch.ops.red_diffeq.rmsnorm(x, g, residual)
 
 
+def rms_conv(x, norm, conv):
+    """conv(RMSNorm(x)) for the attention blocks' to_qkv: the normalisation in the conv's operand
+    gather where that form applies (fp32), else RMSNorm then the conv."""
+    if _PREC["mode"] == "fp32" and ops.conv_rms_fusable(x, conv.weight):
+        return torch.ops.red_diffeq.conv2d_rms(x, norm.g, conv.weight, conv.bias, None)
+    return conv2d(rmsnorm(x, norm.g), conv)
+
+
 def linear_attention(x, m):
     """LinearAttention.forward(x) + x (diffusion.py:182-195 and the residual at 286/297)."""
-    qkv = conv2d(rmsnorm(x, m.norm.g), m.to_qkv)
+    qkv = rms_conv(x, m.norm, m.to_qkv)
     out = torch.ops.red_diffeq.linear_attn(qkv, m.mem_kv, m.heads, float(m.scale))
     return rmsnorm(conv2d(out, m.to_out[0]), m.to_out[1].g, residual=x)
 
 
 def full_attention(x, m):
     """Attention.forward(x) + x (diffusion.py:209-218 with Attend(flash=False), residual 290)."""
-    qkv = conv2d(rmsnorm(x, m.norm.g), m.to_qkv)
+    qkv = rms_conv(x, m.norm, m.to_qkv)
     out = torch.ops.red_diffeq.attn(qkv, m.mem_kv, m.heads)
     return conv2d(out, m.to_out, residual=x)
 

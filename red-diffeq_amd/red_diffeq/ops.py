@@ -15,7 +15,7 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
-    conv2d_mfma, conv2d_gn_silu, gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb,
+    conv2d_mfma, conv2d_rms, conv2d_gn_silu, gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb,
     linear_attn, attn, red_q_sample, red_eps
   loop (include/red_diffeq_loop.h)
     l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
@@ -333,6 +333,38 @@ def gn_silu(x: Tensor, weight: Tensor, bias: Tensor, scale_shift: Optional[Tenso
 @gn_silu.register_fake
 def _(x, weight, bias, scale_shift, groups, eps):
     return torch.empty_like(x)
+
+
+def conv_rms_fusable(x, weight):
+    """rdq_conv2d_rms applies: 1x1 conv, channel counts multiples of 64 (<= 2048), fp32 extents."""
+    cout, cin, kh, kw = weight.shape
+    return kh == 1 and kw == 1 and cin % 64 == 0 and cin <= 2048 and x.shape[1] == cin and \
+        x.numel() * 4 < 2 ** 31 and x.shape[0] * cout * x.shape[2] * x.shape[3] * 4 < 2 ** 31
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_rms", mutates_args=())
+def conv2d_rms(x: Tensor, g: Tensor, weight: Tensor, bias: Optional[Tensor], residual: Optional[Tensor]) -> Tensor:
+    """1x1 conv of RMSNorm(x) = F.normalize(x, dim=1) * g * sqrt(C) (the attention blocks' to_qkv,
+    diffusion.py:184-186, 211-213), the normalisation formed in the conv's operand gather."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    d, shape = _conv_desc(x, None, weight, 0, 0)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_ws_bytes(ctypes.byref(d)))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device) if nws else None
+    tk = _tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d)))) if nws else None
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    res = residual.contiguous() if residual is not None else None
+    _hip.check(L.rdq_conv2d_rms(ctypes.byref(d), _hip.ptr(x), _hip.ptr(g.contiguous()), _hip.ptr(weight.contiguous()),
+                                _hip.ptr(bias), _hip.ptr(res), _hip.ptr(y), _hip.ptr(ws), nws, tk,
+                                _hip.stream_of(x)), "rdq_conv2d_rms")
+    return y
+
+
+@conv2d_rms.register_fake
+def _(x, g, weight, bias, residual):
+    _, shape = _conv_desc(x, None, weight, 0, 0)
+    return x.new_empty(shape)
 
 
 def conv_gn_fusable(x, x2, weight, pad, mode, groups):
@@ -655,7 +687,8 @@ def _forward_only(op, name):
     op.register_autograd(backward, setup_context=setup)
 
 
-for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_gn_silu, "conv2d_gn_silu"), (gn_silu, "gn_silu"),
+for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"),
+                   (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
                    (linear_silu_multi, "linear_silu_multi"),
                    (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (attn, "attn"),

@@ -75,6 +75,9 @@ def test_unet_and_loop_ops_opcheck(cuda):
     wg = r(64, 24, 3, 3) * 0.1
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, r(64), 1, 0, r(64), r(64), r(2, 128), 8, 1e-5, r(2, 64, 12, 10)))
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, None, 1, 0, r(64), r(64), None, 8, 1e-5, None))
+    xr = r(2, 64, 12, 10)
+    opcheck(ops.conv2d_rms, (xr, r(1, 64, 1, 1), r(96, 64, 1, 1), None, None))
+    opcheck(ops.conv2d_rms, (xr, r(1, 64, 1, 1), r(64, 64, 1, 1), r(64), xr))
     opcheck(ops.gn_silu, (x, r(16), r(16), r(2, 32), 8, 1e-5))
     opcheck(ops.gn_silu, (x, r(16), r(16), None, 8, 1e-5))
     opcheck(ops.rmsnorm, (x, r(1, 16, 1, 1), x))

@@ -120,6 +120,25 @@ def test_conv_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post):
     assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
 
 
+# to_qkv(RMSNorm(x)) with the normalisation in the 1x1 conv's gather vs RMSNorm then conv in torch
+@pytest.mark.parametrize("C,cout,H,B", [(64, 384, 72, 1), (128, 384, 36, 2), (512, 384, 9, 1), (256, 64, 18, 3)])
+def test_conv_rms_fused(cuda, C, cout, H, B):
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(9)
+    conv = nn.Conv2d(C, cout, 1, bias=False).to(cuda)
+    g = 1 + 0.3 * torch.randn(1, C, 1, 1, device=cuda)
+    x = 2 * torch.randn(B, C, H, H, device=cuda) + 0.3
+
+    class N:
+        pass
+    nm = N()
+    nm.g = g
+    with torch.no_grad():
+        got = ops.rms_conv(x, nm, conv)
+        ref = R.conv2d(R.rmsnorm(x, g), conv)
+    close(got, ref, rel=5e-5)
+
+
 @pytest.mark.parametrize("C,H,ss", [(64, 72, True), (16, 9, False), (128, 18, True)])
 def test_group_norm_silu(cuda, C, H, ss):
     from red_diffeq.models import unet_ops as ops
