@@ -180,6 +180,42 @@ def unet_rate(dev, reps=20):
             "conv_tflops": round(tfs, 2), "peak_tflops": FP32_MFMA_PEAK_TFS, "mfma_frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
 
 
+def conv_class_rates(dev, reps=10, inner=20):
+    """fp32 conv classes of the U-Net (MFMA k_conv_cc) at B = 1 (the loop) and B = 8 (batched
+    patches): device time per launch from a hipGraph of `inner` back-to-back launches (launch gaps
+    included), TFLOP/s and the fraction of the fp32 matrix peak."""
+    shapes = {"l72_3x3_64to64": (64, 0, 64, 72), "l72_3x3_cat128to64": (64, 64, 64, 72),
+              "l9_3x3_512to512": (512, 0, 512, 9)}
+    out = {}
+    for name, (c1, c2, co, H) in shapes.items():
+        for B in (1, 8):
+            g = torch.Generator(device=dev).manual_seed(0)
+            x = torch.randn(B, c1, H, H, device=dev, generator=g)
+            x2 = torch.randn(B, c2, H, H, device=dev, generator=g) if c2 else None
+            w = torch.randn(co, c1 + c2, 3, 3, device=dev, generator=g) * 0.05
+            b = torch.randn(co, device=dev, generator=g)
+            f = lambda: torch.ops.red_diffeq.conv2d_mfma(x, x2, w, b, None, 1, 0, False)  # noqa: E731
+            for _ in range(2):
+                f()
+            torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for _ in range(inner):
+                    f()
+            gr.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                gr.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / (reps * inner)
+            tf = 2.0 * B * H * H * co * (c1 + c2) * 9 / us / 1e6
+            out[f"{name}_B{B}"] = {"us": round(us, 2), "tflops": round(tf, 1), "mfma_frac": round(tf / FP32_MFMA_PEAK_TFS, 3)}
+    return out
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -342,6 +378,7 @@ def main():
         out["per_iter_fwi_wallclock_ms"] = loop_wallclock(fwi, mu0, vt, y, a, dev, world)
     if world == 1 and not a.no_red:
         out["unet"] = unet_rate(dev)
+        out["unet"]["conv_classes"] = conv_class_rates(dev)
         out["configs2_red_loop"] = {"workload": "configs[2]: OpenFWI CurveVel-A 70x70, 32 shots, full RED-DiffEq "
                                                 "loop (fwd+adj + U-Net regulariser + Adam + metrics), random-init U-Net",
                                     "ms_per_iter": red_loop_wallclock(dev, a),

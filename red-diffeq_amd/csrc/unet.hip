@@ -608,14 +608,18 @@ void cc_extents(CcArgs &c, const rdq_conv_desc *d)
     c.wbytes = (int)((int64_t)d->cout * c.K * 4);
 }
 
-// splits: fill the chip with about one workgroup per CU (a second workgroup on a CU only shares its
-// matrix unit), >= 3 stages per split (the pipeline's fill), and at most 16 slabs to combine
+// splits: fill the chip with about one workgroup per CU, >= 3 stages per split (the pipeline's fill),
+// at most 16 slabs to combine; a grid of 128..255 tiles (half the CUs idle, or one workgroup
+// per CU with nothing to hide its waits) is split in two when each half keeps >= 6 stages (a
+// second workgroup on a CU shares the matrix unit but hides the first one's load / LDS latency:
+// level-9 512-channel convs at B = 8 measured 73 -> see DESIGN.md)
 int cc_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
 {
     const int M = d->B * d->H * d->W;
     const int tiles = ((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN);
     const int nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
     int S = std::max(1, std::min(std::min(256 / tiles, nstages / 3), 16));
+    if (tiles >= 128 && tiles < 256 && nstages >= 12) S = 2;
     const size_t slab = (size_t)tiles * CC_BM * CC_BN * sizeof(float);      // >= M * cout floats
     if (S > 1) S = (int)std::min<size_t>((size_t)S, ws_bytes / slab);
     S = std::max(S, 1);
