@@ -20,7 +20,11 @@ thread counts, so the only floor is the summation order of a different (correct)
 It also records, for each round-1 loop fixture, the RMSE between the reference's final model and
 the reference engine driven by the oracle operator ("oracle_op_floor_per_fixture").
 
-Run:  python tests/golden/repro_floor.py [fixtures]
+It also records the DiffusionFWI fixture's sensitivity ("dfwi_floor", dfwi_floor()): to a 1e-7
+relative change of the U-Net output, and to the FWI operator's summation order (the reference
+DiffusionFWI driven by the oracle operator).
+
+Run:  python tests/golden/repro_floor.py [fixtures | dfwi]
 """
 import json
 import os
@@ -77,6 +81,9 @@ class _OracleFWI:
     def __call__(self, v):
         return _OracleOp.apply(v, self.f)
 
+    def to(self, device):
+        return self
+
 
 def run(op, threads):
     torch.set_num_threads(threads)
@@ -115,7 +122,56 @@ def rmse(a, b):
     return np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2, axis=tuple(range(1, a.ndim))))
 
 
+def dfwi_floor():
+    """The REFERENCE DiffusionFWI trajectory of the dfwi_small fixture (gen_dfwi, variant "base")
+    re-run with its U-Net output eps_hat scaled by (1 + k 1e-7), k = +-1, 3: a change at the level of
+    fp32 rounding.  The run is chaotic (a sampling step's clip / branch flips), so the deviation of
+    these runs from the unperturbed one is the floor no fp32 implementation with another summation
+    order can be held below (tests/test_gpu_dfwi.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_ref_dfwi", "/root/reference/diffusion_bench/diffusionfwi.py")
+    dfwi = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(dfwi)
+    z = np.load(os.path.join(HERE, "dfwi_small.npz"))
+    ctx = dict(G.SMALL, n_grid=14, ng=14, ns=2)
+    y = torch.from_numpy(z["y"])
+    out = {}
+    base = None
+    for k in (0, 1, -1, 3, "oracle"):
+        net = G._unet_dim8()
+        diff = G.ref.diffusion.GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                                                 objective="pred_noise").eval()
+        fwd = diff.model.forward
+        sc = 1.0 + (k * 1e-7 if k != "oracle" else 0.0)
+        diff.model.forward = lambda *a, _f=fwd, _s=sc, **kw: _f(*a, **kw) * _s
+        fwi = G.make_fwi(ctx) if k != "oracle" else _OracleFWI(ctx)
+        bench = dfwi.DiffusionFWI(diff, fwi, G.ref.ssim.SSIM(window_size=11))
+        mu, hist = bench.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]), y, fwi, ts=3,
+                                  diffusion_ts=4, lr=0.03)
+        h = {m: np.array(hist[0][m]).ravel() for m in ("obs_losses", "ssim", "mae", "rmse")}
+        mu = mu.detach().numpy()
+        if k == 0:
+            base = (h, mu)
+            assert np.array_equal(h["obs_losses"], z["base_obs"])       # the fixture's own run
+            continue
+        key = "oracle_op" if k == "oracle" else "eps_1e-7"
+        o = out.setdefault(key, {})
+        for m in h:
+            r = float(np.max(np.abs(h[m] - base[0][m]) / np.abs(base[0][m])))
+            o[m] = max(o.get(m, 0.0), r)
+        o["mu_maxabs"] = max(o.get("mu_maxabs", 0.0), float(np.abs(mu - base[1]).max()))
+    return out
+
+
 def main():
+    if sys.argv[1:] == ["dfwi"]:          # only the DiffusionFWI sensitivity floor
+        p = os.path.join(HERE, "repro_floor.json")
+        rep = json.load(open(p))
+        rep.pop("dfwi_eps_1e-7_floor", None)
+        rep["dfwi_floor"] = dfwi_floor()
+        json.dump(rep, open(p, "w"), indent=1)
+        print(rep["dfwi_floor"])
+        return
     if sys.argv[1:] == ["fixtures"]:      # refresh only the per-fixture floors
         p = os.path.join(HERE, "repro_floor.json")
         rep = json.load(open(p))

@@ -1,11 +1,17 @@
 """DiffusionFWI baseline (red-diffeq_amd/diffusion_bench, reference diffusion_bench/diffusionfwi.py)
 on the HIP operators vs the reference's own trajectory (tests/golden/dfwi_small.npz, made by
 tests/golden/make_golden.py on the reference, CPU): 4 reverse-diffusion steps, 3 FWI iterations
-each, dim-8 U-Net.  fp32 with different summation orders (GPU kernels vs CPU autograd): per-step
-metrics within 2e-3 relative, final model within 2e-3 absolute (normalised units).  With
-grad_smooth the reference smooths in fp64 on the host (scipy) and Adam's m / sqrt(v) turns fp32-level
-differences of near-zero gradient cells into +-lr steps, so that variant is held to 1e-2 relative
-on the metrics and 2e-3 on the mean absolute model difference."""
+each, dim-8 U-Net.  fp32 with different summation orders (GPU kernels vs CPU autograd).
+
+The loop restarts Adam at every diffusion step, and Adam's first step is lr * g / (|g| + eps): a
+cell whose gradient is near zero moves by +-lr on the SIGN of an fp32-level quantity.  Measured
+(tools/dfwi_sensitivity.py on the GPU): scaling eps_hat by 1 +- 1e-7 moves this run's step-2
+misfit by 5.5e-3 relative and two cells of the 14 x 14 model by 2 lr (0.062, 0.064), with every
+other cell within 1e-3; the U-Net itself is within 1e-6 of the reference on its fixture.  The
+reference driven by the oracle operator happens not to sit on such a cell
+(tests/golden/repro_floor.json "dfwi_floor").  Bars: per-step metrics within 1e-2 relative; the
+final model within 2e-3 on all but at most 2 % of the cells, and those within 3 lr.  With
+grad_smooth the reference smooths in fp64 on the host (scipy): metrics 1e-2, mean |diff| 2e-3."""
 import numpy as np
 import pytest
 import torch
@@ -37,13 +43,12 @@ def test_diffusionfwi_vs_reference(cuda, tag, kw):
     mu, hist = bench.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
                               torch.from_numpy(z["y"]).to(cuda), fwi, ts=3, diffusion_ts=4, lr=0.03, **kw)
     h = hist[0]
-    rtol = 2e-3 if tag == "base" else 1e-2
     for k in ("obs", "ssim", "mae", "rmse"):
         key = "obs_losses" if k == "obs" else k
-        np.testing.assert_allclose(np.array(h[key]), z[tag + "_" + k], rtol=rtol, err_msg=k)
+        np.testing.assert_allclose(np.array(h[key]), z[tag + "_" + k], rtol=1e-2, err_msg=k)
     d = np.abs(mu.cpu().numpy() - z[tag + "_mu"])
     if tag == "base":
-        assert d.max() < 2e-3, d.max()
+        assert (d > 2e-3).mean() <= 0.02 and d.max() <= 3 * 0.03, ((d > 2e-3).sum(), d.max())
     else:
         assert d.mean() < 2e-3, (d.mean(), d.max())
 
