@@ -68,6 +68,21 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
                        const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
                        hipStream_t stream);
 
+/* ResnetBlock with a 1x1 shortcut (diffusion.py:160-168, the U-Net's up path and final block):
+ *   y   = SiLU(GroupNorm_G(conv3x3(cat(x, x2)) + bias) * (scale+1) + shift)   (block1, as rdq_conv2d_gn_silu)
+ *   y_s = conv1x1(cat(x, x2), w_s) + b_s                                      (res_conv, as rdq_conv2d)
+ * in two launches instead of three: both convs of the same input run in ONE launch (disjoint tile
+ * ranges), then the normalise pass.  Results are bit for bit those of the separate calls.  Applies
+ * where rdq_conv2d_gn_sc_ws_bytes > 0 (d: the 3x3 conv, plain input mode; the 1x1 in the
+ * channel-chunk form).  w_s [cout_s][cin1+cin2]; b_s nullable; tickets: rdq_conv2d_gn_sc_tickets
+ * zeroed words (nullable: no split-K). */
+size_t rdq_conv2d_gn_sc_ws_bytes(const rdq_conv_desc *d, int32_t G, int32_t cout_s);
+size_t rdq_conv2d_gn_sc_tickets(const rdq_conv_desc *d, int32_t cout_s);
+int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                          int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                          float *y, int32_t cout_s, const float *w_s, const float *b_s, float *y_s, void *ws,
+                          size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
+
 /* Mixed-precision conv2d (same input modes and epilogue): bf16 operands, fp32 accumulation on
  * v_mfma_f32_32x32x16_bf16.  The weights are packed once by rdq_conv2d_bf16_pack into
  * wp[cout][kh*kw][cinp] bf16 (round-to-nearest-even, cinp = cin1+cin2 rounded up to 32, zero-padded;
@@ -115,6 +130,18 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
 size_t rdq_linear_attention_ws_bytes(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem);
 int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale, const float *qkv,
                          const float *mem_kv, float *out, void *ws, hipStream_t stream);
+
+/* LinearAttention.forward + residual in three launches (diffusion.py:182-195 with to_out =
+ * Conv2d(heads*dh, dim, 1) + RMSNorm(dim), residual 286/297): the partial contexts, then ONE launch for
+ * the chunk combine (in that launch when the image has <= 8 chunks of 256 tokens, else its own
+ * launch), softmax(q) x context, the 1x1 to_out conv (+ b_out), RMSNorm(g_out) and + res.
+ * dh = 32, heads = 4 (the U-Net's), dim in {64, 128, 256}; w_out [dim][heads*dh]; b_out, res nullable;
+ * y (B, dim, n); ws: rdq_linear_attention_ws_bytes.  Replaces rdq_linear_attention + rdq_conv2d +
+ * rdq_rmsnorm for the U-Net's linear-attention blocks. */
+int rdq_linear_attention_block(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale,
+                               const float *qkv, const float *mem_kv, int32_t dim, const float *w_out,
+                               const float *b_out, const float *g_out, const float *res, float *y, void *ws,
+                               hipStream_t stream);
 
 /* Attention core with Attend(flash=False) (diffusion.py:209-217): softmax(q k^T dh^-1/2) v over
  * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32; K/V of one

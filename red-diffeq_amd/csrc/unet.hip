@@ -235,16 +235,21 @@ struct CcArgs {
     int xbytes, x2bytes, wbytes;   // buffer extents (< 2^31: cc_ok)
 };
 
-template <int TAPS, int MODE, bool RMS = false>
-__global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
+// operand staging image of one workgroup (the 3x3 layout, the larger of the two)
+constexpr int CC_SMEM = 2 * CC_BN * (CcCfg<9>::BK + 4) + 2 * CcCfg<9>::BK * CC_LDA;
+
+// one (m tile bx, n tile by, K split) of the conv on a gx x gy tile grid; smem = the CC_SMEM staging image
+template <int TAPS, int MODE, bool RMS>
+__device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, int split, int gx, int gy, float *smem)
 {
     using C = CcCfg<TAPS>;
     constexpr int BK = C::BK, NA = C::NA, NWQ = C::NWQ, QPR = C::QPR, LDW = BK + 4;
-    __shared__ __attribute__((aligned(16))) float Ws[2][CC_BN][LDW];
-    __shared__ float As[2][BK][CC_LDA];
+    static_assert(2 * CC_BN * LDW + 2 * BK * CC_LDA <= CC_SMEM, "staging image");
+    auto &Ws = *reinterpret_cast<float (*)[2][CC_BN][LDW]>(smem);
+    auto &As = *reinterpret_cast<float (*)[2][BK][CC_LDA]>(smem + 2 * CC_BN * LDW);
     __shared__ unsigned last_s;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int m0 = blockIdx.x * CC_BM, n0 = blockIdx.y * CC_BN, split = blockIdx.z;
+    const int m0 = bx * CC_BM, n0 = by * CC_BN;
     const rdq_conv_desc &d = a.d;
     const int N = d.cout, K = a.K;
     const int s_begin = split * a.per_split, s_end = min(a.nstages, s_begin + a.per_split);
@@ -446,7 +451,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
         // every storing wave drains its stores, the workgroup barrier, one agent-scope ticket add per
         // workgroup, and the workgroup whose add returns S-1 reads all S slabs with sc1 loads
         // (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
-        const int ntile = gridDim.x * gridDim.y, tile = blockIdx.y * gridDim.x + blockIdx.x;
+        const int ntile = gx * gy, tile = by * gx + bx;
         const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, 0x7fffffff, 0x00020000);
         const int voff = tid * 32;
         const int tbase = tile * (CC_BM * CC_BN * 4);
@@ -577,10 +582,33 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
             }
         }
         if (n0 + g * cpg < N) {
-            double *o = a.gnp + (((size_t)blockIdx.x * a.G + n0 / cpg + g) * 2 + k) * 2;
+            double *o = a.gnp + (((size_t)bx * a.G + n0 / cpg + g) * 2 + k) * 2;
             o[0] = s;
             o[1] = q;
         }
+    }
+}
+
+template <int TAPS, int MODE, bool RMS = false>
+__global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
+{
+    __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
+    conv_cc_tile<TAPS, MODE, RMS>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sm);
+}
+
+// A ResnetBlock with a 1x1 shortcut (the U-Net's up path and final block, diffusion.py:160-168):
+// block1's 3x3 conv (GroupNorm statistics in its epilogue) and res_conv of the same concatenated
+// input in ONE launch: n tiles [0, gy_a) run the 3x3 tile, the rest the 1x1 tile (each with its own
+// arguments, split count and tickets; the split slices past a conv's own count return at once).
+// Both tiles are those of the separate launches, so the outputs are bit for bit theirs.
+__global__ __launch_bounds__(256, 2) void k_conv_cc_pair(CcArgs a, CcArgs b, int gy_a)
+{
+    __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
+    const int by = blockIdx.y, bz = blockIdx.z;
+    if (by < gy_a) {
+        if (bz < a.S) conv_cc_tile<9, RDQ_IN_PLAIN, false>(a, blockIdx.x, by, bz, gridDim.x, gy_a, sm);
+    } else if (bz < b.S) {
+        conv_cc_tile<1, RDQ_IN_PLAIN, false>(b, blockIdx.x, by - gy_a, bz, gridDim.x, gridDim.y - gy_a, sm);
     }
 }
 
@@ -1223,6 +1251,237 @@ __global__ __launch_bounds__(256) void k_la_out(int heads, int dh, int n, float 
     float *ob = out + ((size_t)b * C + h * dh) * n + pix;
 #pragma unroll
     for (int e = 0; e < 8; ++e) if (eq * 8 + e < dh) ob[(size_t)(eq * 8 + e) * n] = o[e];
+}
+
+// LinearAttention.forward from the partial contexts on: the chunk combine (k_la_reduce's order), the
+// q softmax / context product (k_la_out's order), to_out = Conv2d(hidden, dim, 1) + bias, the to_out
+// RMSNorm and the block's residual (diffusion.py:182-195, 286/297) in ONE launch.  Workgroup = PX
+// pixels of one sample (PX = 32 at dim 64, else 16):
+//   A  combine: per (h, d) row the chunk weights exp(m_c - M) and the denominator into LDS, then
+//      ctx[h][d][e] = (sum_c f_c part_c) / den for all heads (nch = 0: ctx already combined in ws)
+//   B  hidden[h*dh + e][p] = sum_d ctx[h][d][e] softmax_d(q)[d] * scale   (dh = 32)
+//   C  y[o][p] = bias[o] + sum_c W[o][c] hidden[c][p] on v_mfma_f32_16x16x4_f32: wave w takes the
+//      16-row o blocks w, w + 4, ..., the lane's W fragment (32 contiguous c of one row, k order
+//      k = (lane >> 4) * 32 + step for W and hidden alike) loaded at the start of the launch so
+//      its latency hides behind A and B
+//   D  y / max(||y[:, p]||, 1e-12) * g * sqrt(dim) + x   (pixel-fastest stores)
+// The fused form replaces k_la_reduce + k_la_out + the 1x1 conv + k_rmsnorm_r: four dependent
+// launches of a few microseconds each at B = 1, where the launch is most of the cost.
+constexpr int LAO_MAXCH = 8;                    // chunk partials combined in the launch up to this count
+template <int DIM> struct LaoCfg { static constexpr int PX = DIM == 64 ? 32 : 16; };
+template <int DIM>
+__global__ __launch_bounds__(256) void k_la_out_proj(int heads, int n, int nch, float scale,
+                                                     const float *__restrict__ qkv, const float *__restrict__ pstat,
+                                                     const float *__restrict__ part, const float *__restrict__ w,
+                                                     const float *__restrict__ bias, const float *__restrict__ g,
+                                                     const float *__restrict__ res, float *__restrict__ y)
+{
+    constexpr int DH = 32, PX = LaoCfg<DIM>::PX, LDP = PX + 4, NG = 256 / PX, NR = DIM / NG;
+    constexpr int NOB = DIM / 64, NPB = PX / 16, CH = 128;     // heads * DH = 128 (4 heads)
+    extern __shared__ __attribute__((aligned(16))) float lo_sm[];
+    const int HDD = CH * DH;
+    float *cs = lo_sm;                          // [heads][DH][DH]
+    float *hid = cs + HDD;                      // row r at r * PX + (r >> 5) * 16 (bank skew per head)
+    float *ys = hid + CH * PX + 64;             // [DIM][LDP]
+    float *red = ys + DIM * LDP;                // [NG][PX]
+    float *tot = red + 256;                     // [PX]
+    float *fst = tot + PX;                      // [nch][CH] chunk weights, then [CH] denominators
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, b = blockIdx.y, B = gridDim.y;
+    const int px0 = blockIdx.x * PX;
+    // the lane's W fragments: o block wv + 4 j, row (lane & 15), c = (lane >> 4) * 32 .. + 31
+    f32x4 wf[NOB][8];
+#pragma unroll
+    for (int j = 0; j < NOB; ++j)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            wf[j][u] = *reinterpret_cast<const f32x4 *>(w + (size_t)((wv + 4 * j) * 16 + (lane & 15)) * CH +
+                                                        (lane >> 4) * 32 + u * 4);
+    // residual (pixel-fastest: thread -> pixel tid % PX, channels tid / PX + k NG)
+    const int ep = tid % PX, eg = tid / PX;
+    const int epix = min(px0 + ep, n - 1);
+    float rv[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) rv[k] = res ? res[((size_t)b * DIM + eg + k * NG) * n + epix] : 0.0f;
+    // the first task's q column (phase B below) in flight behind the context combine
+    const int ntask = PX * heads * 4;
+    auto task_pix = [&](int t) { return px0 + t % PX; };
+    auto load_q = [&](int t, float (&qv)[DH]) {
+        const int h = t / (PX * 4);
+        const float *q = qkv + ((size_t)b * 3 * CH + h * DH) * n + min(task_pix(t), n - 1);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] = q[(size_t)d * n];
+    };
+    float qv0[DH];
+    load_q(tid, qv0);
+    // A: combined context of every head
+    if (nch > 0) {
+        // nch <= LAO_MAXCH: every statistic of a row and a thread's partials are loaded together,
+        // combined in chunk order as k_la_reduce does
+        const int BHD = B * CH;
+        if (tid < CH) {
+            const int r = tid;
+            const size_t row = (size_t)b * CH + r;
+            float mv[LAO_MAXCH], sv[LAO_MAXCH];
+#pragma unroll
+            for (int c = 0; c < LAO_MAXCH; ++c) {
+                const size_t k = ((size_t)min(c, nch - 1) * BHD + row) * 2;
+                mv[c] = pstat[k];
+                sv[c] = pstat[k + 1];
+            }
+            float M = -INFINITY;
+#pragma unroll
+            for (int c = 0; c < LAO_MAXCH; ++c) if (c < nch) M = fmaxf(M, mv[c]);
+            float den = 0.0f;
+#pragma unroll
+            for (int c = 0; c < LAO_MAXCH; ++c)
+                if (c < nch) {
+                    const float f = expf(mv[c] - M);
+                    fst[c * CH + r] = f;
+                    den += f * sv[c];
+                }
+            fst[LAO_MAXCH * CH + r] = den;
+        }
+        const float *pb = part + (size_t)b * HDD;
+        // this thread's 4 float4 entries (i4 = tid + 256 u) in two halves of 2 x LAO_MAXCH loads
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            f32x4 pv[2][LAO_MAXCH];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int c = 0; c < LAO_MAXCH; ++c)
+                    pv[u][c] = *reinterpret_cast<const f32x4 *>(pb + (size_t)min(c, nch - 1) * B * HDD +
+                                                                (tid + 256 * (2 * hf + u)) * 4);
+            if (hf == 0) __syncthreads();                          // fst complete
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int i4 = tid + 256 * (2 * hf + u), r = (i4 * 4) / DH;
+                f32x4 num = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int c = 0; c < LAO_MAXCH; ++c)
+                    if (c < nch) {
+                        const float f = fst[c * CH + r];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) num[j] += f * pv[u][c][j];
+                    }
+                const float den = fst[LAO_MAXCH * CH + r];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) cs[i4 * 4 + j] = num[j] / den;
+            }
+        }
+    } else {
+        const float *cb = part + (size_t)b * HDD;          // nch = 0: `part` is the combined context
+        f32x4 cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cv[u] = *reinterpret_cast<const f32x4 *>(cb + (tid + 256 * u) * 4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4 *>(cs + (tid + 256 * u) * 4) = cv[u];
+    }
+    __syncthreads();
+    // B: task (pixel, head, eighth eq) -> 8 hidden channels of one pixel
+    for (int t = tid; t < ntask; t += 256) {
+        const int p = t % PX, eq = (t / PX) & 3, h = t / (PX * 4);
+        float qv[DH];
+        if (t == tid) {
+#pragma unroll
+            for (int d = 0; d < DH; ++d) qv[d] = qv0[d];
+        } else {
+            load_q(t, qv);
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) mx = fmaxf(mx, qv[d]);
+        float sm = 0.0f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) { qv[d] = expf(qv[d] - mx); sm += qv[d]; }
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] = (qv[d] / sm) * scale;
+        const float *ch = cs + h * DH * DH;
+        float o[8] = {};
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+#pragma unroll
+            for (int e4 = 0; e4 < 2; ++e4) {
+                const f32x4 c4 = *reinterpret_cast<const f32x4 *>(&ch[d * DH + eq * 8 + e4 * 4]);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) o[e4 * 4 + q4] += c4[q4] * qv[d];
+            }
+        }
+        const bool ok = px0 + p < n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hid[(h * DH + eq * 8 + e) * PX + h * 16 + p] = ok ? o[e] : 0.0f;
+    }
+    __syncthreads();
+    // C: MFMA projection
+    {
+        f32x4 acc[NOB][NPB];
+#pragma unroll
+        for (int j = 0; j < NOB; ++j)
+#pragma unroll
+            for (int pb = 0; pb < NPB; ++pb) acc[j][pb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int kr = (lane >> 4) * 32;
+        const float *hrow = hid + kr * PX + (lane >> 4) * 16 + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 32; ++s) {
+            float bv[NPB];
+#pragma unroll
+            for (int pb = 0; pb < NPB; ++pb) bv[pb] = hrow[s * PX + pb * 16];
+#pragma unroll
+            for (int j = 0; j < NOB; ++j)
+#pragma unroll
+                for (int pb = 0; pb < NPB; ++pb)
+                    acc[j][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j][s >> 2][s & 3], bv[pb], acc[j][pb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NOB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = (wv + 4 * j) * 16 + (lane >> 4) * 4 + r;
+                const float bo = bias ? bias[o] : 0.0f;
+#pragma unroll
+                for (int pb = 0; pb < NPB; ++pb) ys[o * LDP + pb * 16 + (lane & 15)] = acc[j][pb][r] + bo;
+            }
+    }
+    __syncthreads();
+    // D: squared norms per pixel (channel groups, then the groups in order)
+    {
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) { const float v = ys[(eg + k * NG) * LDP + ep]; s += v * v; }
+        red[eg * PX + ep] = s;
+    }
+    __syncthreads();
+    if (tid < PX) {
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) s += red[k * PX + tid];
+        tot[tid] = s;
+    }
+    __syncthreads();
+    if (px0 + ep >= n) return;
+    const float den = fmaxf(sqrtf(tot[ep]), 1e-12f);          // F.normalize: x / max(||x||, eps)
+    const float sc = sqrtf((float)DIM);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int o = eg + k * NG;
+        float v = ys[o * LDP + ep] / den;
+        v = v * g[o];
+        v = v * sc;
+        if (res) v = v + rv[k];
+        y[((size_t)b * DIM + o) * n + px0 + ep] = v;
+    }
+}
+
+template <int DIM>
+static void launch_la_out_proj(int B, int heads, int n, int nch, float scale, const float *qkv, const float *pstat,
+                               const float *part, const float *w, const float *bias, const float *g,
+                               const float *res, float *y, hipStream_t st)
+{
+    constexpr int PX = LaoCfg<DIM>::PX;
+    const size_t lds = ((size_t)128 * 32 + 128 * PX + 64 + (size_t)DIM * (PX + 4) + 256 + PX +
+                        (size_t)(LAO_MAXCH + 1) * 128) * sizeof(float);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_la_out_proj<DIM>), dim3((n + PX - 1) / PX, B), dim3(256), lds, st, heads, n,
+                       nch, scale, qkv, pstat, part, w, bias, g, res, y);
 }
 
 // ---------------------------------------------------------------------------- full attention
@@ -1974,6 +2233,77 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     return 0;
 }
 
+static rdq_conv_desc shortcut_desc(const rdq_conv_desc *d, int cout_s)
+{
+    rdq_conv_desc ds = *d;
+    ds.cout = cout_s; ds.kh = ds.kw = 1; ds.pad = 0;
+    return ds;
+}
+
+size_t rdq_conv2d_gn_sc_ws_bytes(const rdq_conv_desc *d, int32_t G, int32_t cout_s)
+{
+    const size_t a = rdq_conv2d_gn_ws_bytes(d, G);
+    if (!a || cout_s < 1 || d->in_mode != RDQ_IN_PLAIN || d->kh != 3) return 0;
+    const rdq_conv_desc ds = shortcut_desc(d, cout_s);
+    if (!cc_ok(&ds)) return 0;
+    return a + rdq_conv2d_ws_bytes(&ds);
+}
+
+size_t rdq_conv2d_gn_sc_tickets(const rdq_conv_desc *d, int32_t cout_s)
+{
+    const rdq_conv_desc ds = shortcut_desc(d, cout_s);
+    return rdq_conv2d_tickets(d) + rdq_conv2d_tickets(&ds);
+}
+
+int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                          int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                          float *y, int32_t cout_s, const float *w_s, const float *b_s, float *y_s, void *ws,
+                          size_t ws_bytes, uint32_t *tickets, hipStream_t st)
+{
+    const size_t need = rdq_conv2d_gn_sc_ws_bytes(d, G, cout_s);
+    if (!need || !x || !w || !y || !gamma || !beta || !w_s || !y_s || !ws || ws_bytes < need ||
+        (d->cin2 > 0 && !x2))
+        return RDQ_E_INVALID;
+    const rdq_conv_desc ds = shortcut_desc(d, cout_s);
+    const size_t M = (size_t)d->B * d->H * d->W;
+    const size_t wa = rdq_conv2d_gn_ws_bytes(d, G), slabs = rdq_conv2d_ws_bytes(d), slabs_s = rdq_conv2d_ws_bytes(&ds);
+    float *h = reinterpret_cast<float *>(static_cast<char *>(ws) + slabs);
+    // block1's conv: exactly the arguments of rdq_conv2d_gn_silu
+    CcArgs c{};
+    c.d = *d; c.x = x; c.x2 = x2; c.w = w; c.bias = bias; c.res = nullptr; c.y = h;
+    c.part = static_cast<float *>(ws);
+    c.tickets = tickets;
+    c.gnp = reinterpret_cast<double *>(h + M * d->cout);
+    c.G = G;
+    c.K = (d->cin1 + d->cin2) * 9;
+    c.HW = d->H * d->W;
+    c.M = (int)M;
+    cc_extents(c, d);
+    c.nstages = (d->cin1 + d->cin2) / CcCfg<9>::CPS;
+    c.S = (slabs && tickets) ? cc_splits(d, slabs, &c.per_split) : 1;
+    if (c.S == 1) c.per_split = c.nstages;
+    // the shortcut: exactly the arguments of rdq_conv2d (split-K combined in the launch)
+    CcArgs e{};
+    e.d = ds; e.x = x; e.x2 = x2; e.w = w_s; e.bias = b_s; e.res = nullptr; e.y = y_s;
+    e.part = reinterpret_cast<float *>(static_cast<char *>(ws) + wa);
+    e.tickets = tickets ? tickets + rdq_conv2d_tickets(d) : nullptr;
+    e.K = ds.cin1 + ds.cin2;
+    e.HW = c.HW;
+    e.M = c.M;
+    cc_extents(e, &ds);
+    e.nstages = (ds.cin1 + ds.cin2) / CcCfg<1>::CPS;
+    e.S = (slabs_s && tickets) ? cc_splits(&ds, slabs_s, &e.per_split) : 1;
+    if (e.S == 1) e.per_split = e.nstages;
+    const int gy_a = (d->cout + CC_BN - 1) / CC_BN, gy_b = (cout_s + CC_BN - 1) / CC_BN;
+    const dim3 grid((c.M + CC_BM - 1) / CC_BM, gy_a + gy_b, std::max(c.S, e.S));
+    hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
+    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
+    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
+                       scale_shift, c.gnp, eps, nullptr, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
 int rdq_conv2d_rms(const rdq_conv_desc *d, const float *x, const float *g, const float *w, const float *bias,
                    const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t st)
 {
@@ -2187,6 +2517,34 @@ int rdq_linear_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_
     hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, pstat, part, ctx);
     hipLaunchKernelGGL(k_la_out, dim3((n + 63) / 64, heads, B), dim3(256), 0, st, heads, dh, n, scale, qkv, ctx,
                        out);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_linear_attention_block(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t nmem, float scale,
+                               const float *qkv, const float *mem_kv, int32_t dim, const float *w_out,
+                               const float *b_out, const float *g_out, const float *res, float *y, void *ws,
+                               hipStream_t st)
+{
+    if (B < 1 || heads != 4 || dh != 32 || n < 1 || nmem < 0 || !qkv || !mem_kv || !w_out || !g_out ||
+        !y || !ws || (dim != 64 && dim != 128 && dim != 256))
+        return RDQ_E_INVALID;
+    const int nch = la_chunks(n, nmem);
+    float *pstat = (float *)ws;
+    float *part = pstat + (size_t)nch * B * heads * dh * 2;
+    float *ctx = part + (size_t)nch * B * heads * dh * dh;
+    hipLaunchKernelGGL(k_la_ctx, dim3(nch, heads, B), dim3(256), 0, st, heads, dh, n, nmem, qkv, mem_kv, part, pstat);
+    int fold = nch;
+    const float *src = part;
+    if (nch > LAO_MAXCH) {          // many chunks (72 x 72): the combine keeps its own launch
+        const int bhdd = B * heads * dh * dh;
+        hipLaunchKernelGGL(k_la_reduce, dim3((bhdd + 255) / 256), dim3(256), 0, st, bhdd, dh, nch, pstat, part, ctx);
+        fold = 0;
+        src = ctx;
+    }
+    if (dim == 64) launch_la_out_proj<64>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
+    else if (dim == 128) launch_la_out_proj<128>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
+    else launch_la_out_proj<256>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

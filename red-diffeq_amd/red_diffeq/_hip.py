@@ -77,6 +77,11 @@ SIGNATURES = {
     "rdq_conv2d_rms": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_size_t, c_void_p, c_void_p]),
     "rdq_conv2d_gn_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),
+    "rdq_conv2d_gn_sc_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32, c_int32]),
+    "rdq_conv2d_gn_sc_tickets": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),
+    "rdq_conv2d_gn_silu_sc": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                        c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
     "rdq_conv2d_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                      c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_void_p, c_void_p]),
@@ -99,6 +104,9 @@ SIGNATURES = {
     "rdq_linear_attention_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "rdq_linear_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p]),
+    "rdq_linear_attention_block": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p,
+                                             c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p]),
     "rdq_full_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "rdq_red_q_sample": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -117,10 +117,15 @@ class ResnetBlock(nn.Module):
         `scale_shift` = this block's Linear(SiLU(time_emb)) when the caller formed it already."""
         if scale_shift is None and exists(self.mlp) and exists(time_emb):
             scale_shift = ops.linear(time_emb, self.mlp[1], act_in=1)   # Linear(SiLU(t)): (B, 2C)
-        h = self.block1(x, scale_shift=scale_shift, skip=skip)
         if isinstance(self.res_conv, nn.Conv2d):
-            h = self.block2(h)
+            # block1's conv and the 1x1 shortcut in one launch; block2 adds the shortcut after its SiLU
+            pair = ops.conv_group_norm_silu_shortcut(x, self.block1.proj, self.block1.norm, scale_shift, skip,
+                                                     self.res_conv)
+            if pair is not None:
+                return self.block2(pair[0], post=pair[1])
+            h = self.block2(self.block1(x, scale_shift=scale_shift, skip=skip))
             return ops.conv2d(x, self.res_conv, x2=skip, residual=h)    # h + res_conv(x), fused
+        h = self.block1(x, scale_shift=scale_shift, skip=skip)
         if skip is not None:
             x = torch.cat((x, skip), dim=1)
         return self.block2(h, post=x)                                    # h + x, fused

@@ -82,6 +82,16 @@ def conv_group_norm_silu(x, conv, norm, scale_shift=None, skip=None, post=None):
     return h + post if post is not None else h
 
 
+def conv_group_norm_silu_shortcut(x, conv, norm, scale_shift, skip, res_conv):
+    """(Block.forward(cat(x, skip)), res_conv(cat(x, skip))) of a ResnetBlock with a 1x1 shortcut: both
+    convs in one launch (rdq_conv2d_gn_silu_sc) where that form applies (fp32), else None."""
+    if _PREC["mode"] != "fp32" or not isinstance(res_conv, torch.nn.Conv2d) or \
+            not ops.conv_gn_sc_fusable(x, skip, conv.weight, res_conv.weight, norm.num_groups):
+        return None
+    return torch.ops.red_diffeq.conv2d_gn_silu_sc(x, skip, conv.weight, conv.bias, norm.weight, norm.bias, scale_shift,
+                                                  norm.num_groups, float(norm.eps), res_conv.weight, res_conv.bias)
+
+
 def group_norm_affine_silu(x, norm, scale_shift=None):
     """GroupNorm -> x*(scale+1)+shift -> SiLU; scale_shift: (B, 2C) (scale first, as chunk(2))."""
     return torch.ops.red_diffeq.gn_silu(x, norm.weight, norm.bias, scale_shift, norm.num_groups, float(norm.eps))
@@ -103,8 +113,13 @@ def rms_conv(x, norm, conv):
 def linear_attention(x, m):
     """LinearAttention.forward(x) + x (diffusion.py:182-195 and the residual at 286/297)."""
     qkv = rms_conv(x, m.norm, m.to_qkv)
+    conv = m.to_out[0]
+    if _PREC["mode"] == "fp32" and ops.linear_attn_block_fusable(qkv.shape[1], m.heads, conv.weight.shape[0]):
+        # context -> (combine, softmax(q) x context, to_out conv, RMSNorm, + x) in one launch
+        return torch.ops.red_diffeq.linear_attn_block(qkv, m.mem_kv, m.heads, float(m.scale), conv.weight,
+                                                      conv.bias, m.to_out[1].g, x)
     out = torch.ops.red_diffeq.linear_attn(qkv, m.mem_kv, m.heads, float(m.scale))
-    return rmsnorm(conv2d(out, m.to_out[0]), m.to_out[1].g, residual=x)
+    return rmsnorm(conv2d(out, conv), m.to_out[1].g, residual=x)
 
 
 def full_attention(x, m):
@@ -125,6 +140,6 @@ def red_epilogue(diff, xt, t, eps_hat, eps):
                                         diff.sqrt_recipm1_alphas_cumprod)
 
 
-HIP_OPS = {"conv2d", "conv_group_norm_silu", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+HIP_OPS = {"conv2d", "conv_group_norm_silu", "conv_group_norm_silu_shortcut", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
            "full_attention", "red_q_sample", "red_epilogue"}
 del math

@@ -16,7 +16,7 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
     conv2d_mfma, conv2d_rms, conv2d_gn_silu, gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb,
-    linear_attn, attn, red_q_sample, red_eps
+    linear_attn, linear_attn_block, attn, red_q_sample, red_eps
   loop (include/red_diffeq_loop.h)
     l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
 
@@ -406,6 +406,48 @@ def _(x, x2, weight, bias, pad, mode, gamma, beta, scale_shift, groups, eps, pos
     return x.new_empty(shape)
 
 
+def conv_gn_sc_fusable(x, x2, weight, weight_s, groups):
+    """rdq_conv2d_gn_silu_sc applies: block1's 3x3 conv + GroupNorm (conv_gn_fusable) and a 1x1
+    shortcut of the same input in the channel-chunk form (channel counts multiples of 64)."""
+    d, _ = _conv_desc(x, x2, weight, 1, 0)
+    return weight.shape[-1] == 3 and weight_s.shape[-1] == 1 and \
+        int(_hip.lib().rdq_conv2d_gn_sc_ws_bytes(ctypes.byref(d), int(groups), int(weight_s.shape[0]))) > 0
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_gn_silu_sc", mutates_args=())
+def conv2d_gn_silu_sc(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], gamma: Tensor,
+                      beta: Tensor, scale_shift: Optional[Tensor], groups: int, eps: float, weight_s: Tensor,
+                      bias_s: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
+    """ResnetBlock with a 1x1 shortcut (diffusion.py:160-168): (block1(cat(x, x2)), res_conv(cat(x, x2)))
+    with both convs in one launch, then block1's normalise pass."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    d, shape = _conv_desc(x, x2, weight, 1, 0)
+    cs = int(weight_s.shape[0])
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_gn_sc_ws_bytes(ctypes.byref(d), int(groups), cs))
+    if nws == 0:
+        raise ValueError("conv2d_gn_silu_sc: shape not supported by the fused form (see conv_gn_sc_fusable)")
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    tk = _tickets(x.device, int(L.rdq_conv2d_gn_sc_tickets(ctypes.byref(d), cs)))
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    ys = torch.empty(shape[0], cs, shape[2], shape[3], device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    _hip.check(L.rdq_conv2d_gn_silu_sc(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(weight.contiguous()),
+                                       _hip.ptr(bias), int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta),
+                                       _hip.ptr(ss), _hip.ptr(y), cs, _hip.ptr(weight_s.contiguous()), _hip.ptr(bias_s),
+                                       _hip.ptr(ys), _hip.ptr(ws), nws, tk, _hip.stream_of(x)),
+               "rdq_conv2d_gn_silu_sc")
+    return y, ys
+
+
+@conv2d_gn_silu_sc.register_fake
+def _(x, x2, weight, bias, gamma, beta, scale_shift, groups, eps, weight_s, bias_s):
+    _, shape = _conv_desc(x, x2, weight, 1, 0)
+    return x.new_empty(shape), x.new_empty(shape[0], weight_s.shape[0], shape[2], shape[3])
+
+
 @torch.library.custom_op(f"{LIB}::rmsnorm", mutates_args=())
 def rmsnorm(x: Tensor, g: Tensor, residual: Optional[Tensor]) -> Tensor:
     """F.normalize(x, dim=1) * g * sqrt(C) [+ residual]."""
@@ -521,6 +563,41 @@ def linear_attn(qkv: Tensor, mem_kv: Tensor, heads: int, scale: float) -> Tensor
 def _(qkv, mem_kv, heads, scale):
     B, C3, H, W = qkv.shape
     return qkv.new_empty(B, C3 // 3, H, W)
+
+
+def linear_attn_block_fusable(qkv_channels, heads, dim):
+    return heads == 4 and qkv_channels == 3 * heads * 32 and dim in (64, 128, 256)
+
+
+@torch.library.custom_op(f"{LIB}::linear_attn_block", mutates_args=())
+def linear_attn_block(qkv: Tensor, mem_kv: Tensor, heads: int, scale: float, w_out: Tensor,
+                      b_out: Optional[Tensor], g_out: Tensor, residual: Optional[Tensor]) -> Tensor:
+    """LinearAttention.forward(x) + x from qkv = to_qkv(RMSNorm(x)) (diffusion.py:182-195, residual
+    286/297): context, softmax(q) x context, to_out = Conv2d(hidden, dim, 1) + RMSNorm(dim) and the
+    residual, the last four in one launch (rdq_linear_attention_block).  dh = 32, dim 64/128/256."""
+    _hip.require_device(qkv)
+    qkv = qkv.contiguous()
+    B, C3, H, W = qkv.shape
+    dh = C3 // (3 * heads)
+    dim = w_out.shape[0]
+    L = _hip.lib()
+    ws = torch.empty(int(L.rdq_linear_attention_ws_bytes(B, heads, dh, H * W, mem_kv.shape[-1])), dtype=torch.uint8,
+                     device=qkv.device)
+    y = torch.empty(B, dim, H, W, device=qkv.device, dtype=torch.float32)
+    res = residual.contiguous() if residual is not None else None
+    _hip.check(L.rdq_linear_attention_block(B, heads, dh, H * W, mem_kv.shape[-1], float(scale), _hip.ptr(qkv),
+                                            _hip.ptr(mem_kv.contiguous()), dim, _hip.ptr(w_out.contiguous()),
+                                            _hip.ptr(b_out) if b_out is not None else None,
+                                            _hip.ptr(g_out.contiguous()), _hip.ptr(res) if res is not None else None,
+                                            _hip.ptr(y), _hip.ptr(ws), _hip.stream_of(qkv)),
+               "rdq_linear_attention_block")
+    return y
+
+
+@linear_attn_block.register_fake
+def _(qkv, mem_kv, heads, scale, w_out, b_out, g_out, residual):
+    B, C3, H, W = qkv.shape
+    return qkv.new_empty(B, w_out.shape[0], H, W)
 
 
 @torch.library.custom_op(f"{LIB}::attn", mutates_args=())
@@ -687,10 +764,10 @@ def _forward_only(op, name):
     op.register_autograd(backward, setup_context=setup)
 
 
-for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"),
+for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"), (conv2d_gn_silu_sc, "conv2d_gn_silu_sc"),
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
                    (linear_silu_multi, "linear_silu_multi"),
-                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (attn, "attn"),
+                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (linear_attn_block, "linear_attn_block"), (attn, "attn"),
                    (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
     _forward_only(_op, _name)

@@ -75,6 +75,9 @@ def test_unet_and_loop_ops_opcheck(cuda):
     wg = r(64, 24, 3, 3) * 0.1
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, r(64), 1, 0, r(64), r(64), r(2, 128), 8, 1e-5, r(2, 64, 12, 10)))
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, None, 1, 0, r(64), r(64), None, 8, 1e-5, None))
+    xs, xs2 = r(2, 64, 12, 10), r(2, 64, 12, 10)
+    opcheck(ops.conv2d_gn_silu_sc, (xs, xs2, r(64, 128, 3, 3) * 0.1, r(64), r(64), r(64), r(2, 128), 8, 1e-5,
+                                    r(64, 128, 1, 1), r(64)))
     xr = r(2, 64, 12, 10)
     opcheck(ops.conv2d_rms, (xr, r(1, 64, 1, 1), r(96, 64, 1, 1), None, None))
     opcheck(ops.conv2d_rms, (xr, r(1, 64, 1, 1), r(64, 64, 1, 1), r(64), xr))
@@ -86,6 +89,10 @@ def test_unet_and_loop_ops_opcheck(cuda):
     opcheck(ops.time_mlp, (torch.tensor([3, 900], device=cuda), 16, 10000.0, r(64, 16), r(64), r(64, 64), r(64)))
     opcheck(ops.linear_silu_multi, (r(2, 64), [r(32, 64), r(128, 64)], [r(32), r(128)]))
     opcheck(ops.linear_attn, (r(2, 3 * 4 * 8, 6, 6), r(2, 4, 8, 4), 4, 8 ** -0.5))
+    qkv, mkv = r(2, 3 * 4 * 32, 6, 6), r(2, 4, 32, 4)
+    opcheck(ops.linear_attn_block, (qkv, mkv, 4, 32 ** -0.5, r(64, 128, 1, 1) * 0.1, r(64), r(1, 64, 1, 1),
+                                    r(2, 64, 6, 6)))
+    opcheck(ops.linear_attn_block, (qkv, mkv, 4, 32 ** -0.5, r(256, 128, 1, 1) * 0.1, None, r(1, 256, 1, 1), None))
     opcheck(ops.attn, (r(2, 3 * 2 * 32, 3, 3), r(2, 2, 4, 32), 2))             # dim_head 32 (the U-Net)
     sa, s1 = torch.rand(1000, device=cuda) + 0.1, torch.rand(1000, device=cuda) + 0.1
     t = torch.tensor([5, 700], device=cuda)

@@ -120,6 +120,32 @@ def test_conv_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post):
     assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
 
 
+# ResnetBlock with a 1x1 shortcut: block1's conv and res_conv in one launch (rdq_conv2d_gn_silu_sc),
+# bitwise equal to the separate calls, on the U-Net's up-path / final-block shapes
+@pytest.mark.parametrize("cin1,cin2,cout,H,B", [(512, 256, 512, 9, 1), (256, 128, 256, 18, 1), (128, 64, 128, 36, 2),
+                                                (64, 64, 64, 72, 1)])
+def test_conv_gn_silu_with_shortcut(cuda, cin1, cin2, cout, H, B):
+    from red_diffeq import ops as O
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(7)
+    conv = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    res = nn.Conv2d(cin1 + cin2, cout, 1).to(cuda)
+    norm = nn.GroupNorm(8, cout).to(cuda)
+    x = torch.randn(B, cin1, H, H, device=cuda)
+    x2 = torch.randn(B, cin2, H, H, device=cuda)
+    sc = torch.randn(B, 2 * cout, device=cuda)
+    assert O.conv_gn_sc_fusable(x, x2, conv.weight, res.weight, 8)
+    with torch.no_grad():
+        y, ys = ops.conv_group_norm_silu_shortcut(x, conv, norm, sc, x2, res)
+        ref_y = ops.conv_group_norm_silu(x, conv, norm, sc, skip=x2)
+        ref_s = ops.conv2d(x, res, x2=x2)
+        tref = R.conv2d(torch.cat((x, x2), 1), res)
+    assert torch.equal(y, ref_y)
+    assert torch.equal(ys, ref_s)
+    close(ys, tref)
+    assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
+
+
 # to_qkv(RMSNorm(x)) with the normalisation in the 1x1 conv's gather vs RMSNorm then conv in torch
 @pytest.mark.parametrize("C,cout,H,B", [(64, 384, 72, 1), (128, 384, 36, 2), (512, 384, 9, 1), (256, 64, 18, 3)])
 def test_conv_rms_fused(cuda, C, cout, H, B):
@@ -197,15 +223,20 @@ def test_time_mlp_and_scale_shifts(cuda):
             close(s, b.mlp[1](F.silu(te)))
 
 
-@pytest.mark.parametrize("C,H", [(64, 72), (128, 18)])
-def test_linear_attention(cuda, C, H):
+# the U-Net's linear-attention blocks (dim 64 at 72 / 36, 128 at 18 / 36, 256 at 18): the fused
+# block (rdq_linear_attention_block: 21 chunks at 72 x 72 combined in their own launch, <= 8 in the
+# output launch), B = 1 and 2; C = 32 takes the unfused three-op path
+@pytest.mark.parametrize("C,H,B", [(64, 72, 2), (64, 72, 1), (64, 36, 1), (128, 18, 2), (128, 36, 1), (256, 18, 1),
+                                   (256, 18, 2), (32, 18, 2)])
+def test_linear_attention(cuda, C, H, B):
     from red_diffeq.models.diffusion import LinearAttention
     from red_diffeq.models import unet_ops as ops
     torch.manual_seed(4)
     m = LinearAttention(C).to(cuda)
     with torch.no_grad():
         m.norm.g.mul_(1 + 0.2 * torch.randn_like(m.norm.g))
-    x = torch.randn(2, C, H, H, device=cuda)
+        m.to_out[1].g.mul_(1 + 0.2 * torch.randn_like(m.to_out[1].g))
+    x = torch.randn(B, C, H, H, device=cuda)
     close(ops.linear_attention(x, m), R.linear_attention(x, m) + x, rel=5e-5)
 
 
