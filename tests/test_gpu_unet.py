@@ -240,13 +240,14 @@ def test_linear_attention(cuda, C, H, B):
     close(ops.linear_attention(x, m), R.linear_attention(x, m) + x, rel=5e-5)
 
 
-@pytest.mark.parametrize("C", [256, 512])
-def test_full_attention(cuda, C):
+# 9 x 9 (the U-Net's level), 8 x 8 and 16 x 16, B = 1 and 2
+@pytest.mark.parametrize("C,H,B", [(256, 9, 2), (512, 9, 1), (256, 8, 1), (128, 16, 1)])
+def test_full_attention(cuda, C, H, B):
     from red_diffeq.models.diffusion import Attention
     from red_diffeq.models import unet_ops as ops
     torch.manual_seed(5)
     m = Attention(C).to(cuda)
-    x = torch.randn(2, C, 9, 9, device=cuda)
+    x = torch.randn(B, C, H, H, device=cuda)
     close(ops.full_attention(x, m), R.full_attention(x, m) + x, rel=5e-5)
 
 
