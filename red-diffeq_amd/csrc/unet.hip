@@ -323,8 +323,11 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
     __shared__ float rms_gs[RMS ? 2048 : 1];
     float rms_den = 1.0f;
     const float rms_sc = RMS ? sqrtf((float)d.cin1) : 1.0f;
-    if constexpr (RMS) {
+    if constexpr (RMS)
         for (int c = tid; c < d.cin1; c += 256) rms_gs[c] = a.rms_g[c];
+    // (run after the pipeline's first stage loads are issued: one memory round trip for both)
+    auto rms_pass = [&]() {
+    if constexpr (RMS) {
         // all of the thread's channels (cl + 8j + 64i, up to 512 input channels) in flight at once;
         // channels past cin1 read 0 (offset past the buffer)
         float ssum = 0.0f;
@@ -346,6 +349,7 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
         for (int k = 0; k < 8; ++k) tot += rms_part[k][gp];
         rms_den = fmaxf(sqrtf(tot), 1e-12f);
     }
+    };
     auto stash = [&](int buf, int s, const float (&ra)[NA], const f32x4 (&rw)[NWQ]) {
         if constexpr (TAPS == 9) {
 #pragma unroll
@@ -411,6 +415,7 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
         load(s_begin, ra0, rw0);
         load(min(s_begin + 1, sl), ra1, rw1);
         load(min(s_begin + 2, sl), ra2, rw2);
+        rms_pass();
         stash(0, s_begin, ra0, rw0);
         __syncthreads();
         auto step = [&](int i, float (&rl)[NA], f32x4 (&wl)[NWQ], const float (&rs)[NA], const f32x4 (&wsr)[NWQ]) {
