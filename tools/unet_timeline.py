@@ -25,8 +25,12 @@ def short(n):
 
 if __name__ == "__main__":
     rows = rows_of(sys.argv[1])
-    first = sys.argv[2] if len(sys.argv) > 2 else "k_conv_ig<7"
-    starts = [i for i, r in enumerate(rows) if first in r[0]]
+    marks = [sys.argv[2]] if len(sys.argv) > 2 else ["k_unet_head", "k_conv_ig<7"]   # a forward's first kernel
+    starts = []
+    for first in marks:
+        starts = [i for i, r in enumerate(rows) if first in r[0]]
+        if starts:
+            break
     fw = rows[starts[-1]:]
     t0 = fw[0][1]
     tot = collections.defaultdict(lambda: [0, 0.0])
