@@ -286,6 +286,75 @@ def gen_loop_red():
     print(f"  red marmousi loop {time.time() - t0:.1f}s")
 
 
+class _OracleOp(torch.autograd.Function):
+    @staticmethod
+    def forward(c, v, f):
+        seis, cf = f.forward(v.detach().contiguous().numpy().astype(np.float32), keep_history=True)
+        c.f, c.cf = f, cf
+        return torch.from_numpy(seis)
+
+    @staticmethod
+    def backward(c, g):
+        gA, gK, gb = c.f.adjoint(c.cf, g.contiguous().numpy())
+        out = torch.from_numpy(c.f.finalize(c.cf, gA, gK, gb))
+        c.cf = None
+        return out, None
+
+
+class _OracleFWI:
+    """The oracle (oracle/fwi_oracle.c, the kernels' summation order; forward bit-exact with the
+    reference operator, gradient within 1e-5) as a differentiable operator for the reference engine."""
+
+    def __init__(self, ctx):
+        sys.path.insert(0, os.path.join(HERE, "..", ".."))
+        from oracle import oracle as O
+        self.f = O.OracleFWI(ctx, 1)
+
+    def __call__(self, v):
+        return _OracleOp.apply(v, self.f)
+
+    def to(self, device):
+        return self
+
+
+def gen_loop_red_configs2():
+    """configs[2]'s loop at its own size: OpenFWI CurveVel-A, 32 shots, nt = 1000, the reference
+    architecture's dim-64 U-Net (weights tests/golden/ckpt_weights.py, default sigmoid schedule),
+    lambda 0.75, lr 0.03, sigma_x0 1e-4, 3 iterations, the eps_x0 / t / eps draws recorded.  The
+    reference FWIForward's autograd tape at 32 shots x 1000 steps is ~160 GB, so the reference engine,
+    regulariser and U-Net are driven by the oracle operator (pinned to the reference operator at
+    smaller sizes); y is the oracle forward (bit-exact with the reference's).  y (9 MB) is not stored:
+    the GPU test regenerates it with the HIP forward, bit-exact with the oracle's."""
+    from ckpt_weights import synth_param
+    torch.manual_seed(0)
+    net = ref.diffusion.Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1, flash_attn=False)
+    diff = ref.diffusion.GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise")
+    sd = diff.state_dict()
+    diff.load_state_dict({k: (torch.from_numpy(synth_param(k, v.shape)) if k.startswith("model.") else v)
+                          for k, v in sd.items()})
+    diff.eval()
+    ctx = dict(OPENFWI, ns=32)
+    v_true = synthetic.make_model("curvevel", 70, 70, seed=8888, batch=1)
+    op = _OracleFWI(ctx)
+    with torch.no_grad():
+        y = op.f.forward(vnorm(v_true).astype(np.float32))[0]
+    init = ref.data_trans.prepare_initial_model(torch.from_numpy(v_true), "smoothed", sigma=10.0)
+    mu0 = torch.nn.functional.pad(init, (1, 1, 1, 1), "constant", 0)
+    eng = ref.inversion.InversionEngine(diff, ref.ssim.SSIM(window_size=11), "diffusion", sigma_x0=1e-4)
+    ts = 3
+    torch.manual_seed(1234)
+    rec = record_draws()
+    with rec:
+        mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), torch.from_numpy(y), op, ts=ts, lr=0.03,
+                                reg_lambda=0.75, regularization="diffusion")
+    keys = ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")
+    save("loop_red_configs2", reg=np.array("diffusion"), v_true=v_true, mu0=mu0.numpy(), mu=mu.detach().numpy(),
+         params=np.array([ts, 0.03, 0.75, 10.0, 0, 0.0]), noise_type=np.array("gaussian"), sigma_x0=np.array(1e-4),
+         use_time_weight=np.array(False), y_checksum=np.array([float(np.abs(y).astype(np.float64).sum())]),
+         **{k: np.array(hist[0][k]) for k in keys}, **ctx_arrays(ctx), **rec.arrays())
+
+
 def gen_initial():
     """prepare_initial_model (utils/data_trans.py:65-107), all three initial_type branches."""
     out = {}
@@ -487,7 +556,8 @@ def gen_ilvr():
 
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
             loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi,
-            ilvr=gen_ilvr, loop_rng=gen_loop_rng, loop_red=gen_loop_red, initial=gen_initial, ckpt=gen_ckpt)
+            ilvr=gen_ilvr, loop_rng=gen_loop_rng, loop_red=gen_loop_red, initial=gen_initial, ckpt=gen_ckpt,
+            loop_red_configs2=gen_loop_red_configs2)
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

@@ -58,31 +58,7 @@ class _Capture:
         return self.op(v)
 
 
-class _OracleOp(torch.autograd.Function):
-    @staticmethod
-    def forward(c, v, f):
-        seis, cf = f.forward(v.detach().contiguous().numpy().astype(np.float32), keep_history=True)
-        c.f, c.cf = f, cf
-        return torch.from_numpy(seis)
-
-    @staticmethod
-    def backward(c, g):
-        gA, gK, gb = c.f.adjoint(c.cf, g.contiguous().numpy())
-        out = torch.from_numpy(c.f.finalize(c.cf, gA, gK, gb))
-        c.cf = None
-        return out, None
-
-
-class _OracleFWI:
-    def __init__(self, ctx):
-        from oracle import oracle as O
-        self.f = O.OracleFWI(ctx, 1)
-
-    def __call__(self, v):
-        return _OracleOp.apply(v, self.f)
-
-    def to(self, device):
-        return self
+_OracleFWI = G._OracleFWI          # the reference engine driven by the oracle operator
 
 
 def run(op, threads):

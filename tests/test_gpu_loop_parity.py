@@ -80,6 +80,44 @@ def test_loop_vs_reference_with_recorded_draws(cuda, name):
         np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-6, err_msg=k)
 
 
+def test_red_loop_configs2_at_its_size(cuda):
+    """configs[2]'s loop at its own size: OpenFWI CurveVel-A, 32 shots, nt = 1000, the dim-64 U-Net
+    (synthetic weights, tests/golden/ckpt_weights.py), lambda 0.75, 3 iterations, the reference's
+    eps_x0 / t / eps draws replayed.  Reference side: the reference engine, regulariser and U-Net
+    driven by the oracle operator (the reference operator's autograd tape at this size is ~160 GB;
+    make_golden.gen_loop_red_configs2).  The HIP forward regenerates y (its checksum pinned)."""
+    import sys
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    from ckpt_weights import synth_param
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.models.diffusion import GaussianDiffusion, Unet
+    from red_diffeq.utils.data_trans import v_normalize
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden("loop_red_configs2")
+    fwi = make_fwi(ctx_of(z))
+    with torch.no_grad():
+        y = fwi(v_normalize(torch.from_numpy(z["v_true"])).to(cuda))
+    ysum = float(y.abs().double().sum())
+    assert abs(ysum - float(z["y_checksum"][0])) <= 1e-9 * ysum, (ysum, z["y_checksum"])
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1)
+    diff = GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250, objective="pred_noise")
+    sd = diff.state_dict()
+    diff.load_state_dict({k: (torch.from_numpy(synth_param(k, v.shape)) if k.startswith("model.") else v)
+                          for k, v in sd.items()})
+    diff = diff.to(cuda).eval()
+    eng = InversionEngine(diff, SSIM(window_size=11), "diffusion", sigma_x0=1e-4, show_progress=False)
+    with replay_draws(z):
+        mu, hist = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]), y, fwi, ts=3, lr=0.03,
+                                reg_lambda=0.75, regularization="diffusion")
+    d = float(model_rmse(mu.detach().cpu().numpy(), z["mu"])[0])
+    print(f"loop_red_configs2: velocity-model RMSE vs the reference engine {d:.3e}")
+    assert d <= 1e-4, d                               # north_star: velocity-model RMSE within 1e-4
+    for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
+        np.testing.assert_allclose(np.array(hist[0][k], np.float64), z[k].astype(np.float64), rtol=2e-4, atol=1e-6,
+                                   err_msg=k)
+
+
 def test_tv_long_trajectory_floor(cuda):
     """30 TV iterations: the HIP engine's model vs the reference's, per iteration, against the
     reference's own drift between 1 and 8 threads (measured: 0, bitwise) and between its operator and
