@@ -1,0 +1,13 @@
+#!/bin/bash
+# U-Net forward timing only (B = 1 and 8, graph replay) + the B = 1 per-launch timeline
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/unet_t
+mkdir -p $O
+timeout -k 10 300 python -u tools/unet_prof_b1.py 1 200 > $O/time.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/unet_prof_b1.py 8 50 >> $O/time.log 2>&1 || exit $?
+cat $O/time.log
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- \
+    python3 tools/unet_prof_b1.py 1 5 > $O/prof.log 2>&1 || exit $?
+python3 tools/unet_timeline.py $(ls $O/prof/*kernel_trace.csv | head -1) > $O/timeline.txt || exit $?
+tail -24 $O/timeline.txt
