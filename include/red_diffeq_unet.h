@@ -43,6 +43,12 @@ typedef struct rdq_conv_desc {
  * launch.  Both sum the slabs in slab order (deterministic, identical results). */
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d);
 size_t rdq_conv2d_tickets(const rdq_conv_desc *d);
+/* Workgroup count of the stream-K form the channel-chunk conv takes for this shape on the current
+ * device (given tickets and rdq_conv2d_ws_bytes of ws), 0 if it uses the tile grid: grids of one to
+ * eight rounds of two workgroups per CU whose last round would be <= 80 % full get exactly one round,
+ * each workgroup an equal range of (tile, K stage) units; tiles cut by a range boundary are combined
+ * in the launch in a fixed piece order (deterministic).  RDQ_NO_STREAMK=1 disables it. */
+int rdq_conv2d_streamk(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
                const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
 
@@ -82,6 +88,34 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
                           int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
                           float *y, int32_t cout_s, const float *w_s, const float *b_s, float *y_s, void *ws,
                           size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
+
+/* The first ResnetBlock's block1 (as rdq_conv2d_gn_silu, plain input mode) with every ResnetBlock's
+ * Linear(SiLU(t)) (as rdq_linear_silu_multi: n <= 32 linears of the (B, in) time embedding temb,
+ * ly[j] (B, lout[j])) computed as a side job of the conv launch (Unet.forward, diffusion.py:280-283
+ * with 160-165).  ss_index >= 0: ly[ss_index] is this block's scale_shift (lout = 2 cout); -1: none.
+ * ws / tickets as rdq_conv2d_gn_silu. */
+int rdq_conv2d_gn_silu_lsm(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                           int32_t G, float eps, const float *gamma, const float *beta, const float *post_residual,
+                           float *y, void *ws, size_t ws_bytes, uint32_t *tickets, int32_t in, const float *temb,
+                           int32_t n, const float *const *lw, const float *const *lb, const int32_t *lout,
+                           float *const *ly, int32_t ss_index, hipStream_t stream);
+
+/* The U-Net's tail (diffusion.py:299-301): yf = conv1x1(Block(x) [+ post_residual], wf) + bf with
+ * Block = rdq_conv2d_gn_silu's SiLU(GroupNorm(conv(x)) * (scale+1) + shift) — final_res_block's block2
+ * and final_conv — in two launches, the cout-channel block output never written.  nf <= 4 output
+ * channels, wf [nf][cout], bf nullable, yf [B][nf][H][W]; cout % 4 == 0; ws / tickets as
+ * rdq_conv2d_gn_silu. */
+int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                           int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                           const float *post_residual, int32_t nf, const float *wf, const float *bf, float *yf,
+                           void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
+
+/* The U-Net's first launch (diffusion.py:276-279): y = init_conv(x) (as rdq_conv2d: a conv NOT in the
+ * channel-chunk form, 7x7 or 3x3, cout <= 64, no K split) and temb = Unet.time_mlp(t) (as
+ * rdq_time_mlp) in ONE launch.  RDQ_E_INVALID when the shapes do not allow it. */
+int rdq_unet_head(const rdq_conv_desc *d, const float *x, const float *w, const float *bias, float *y, int32_t dim,
+                  float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid, const float *w2,
+                  const float *b2, int32_t out, float *temb, hipStream_t stream);
 
 /* Mixed-precision conv2d (same input modes and epilogue): bf16 operands, fp32 accumulation on
  * v_mfma_f32_32x32x16_bf16.  The weights are packed once by rdq_conv2d_bf16_pack into
@@ -153,6 +187,10 @@ int rdq_full_attention(int32_t B, int32_t heads, int32_t dh, int32_t n, int32_t 
  * tables are the fp32 schedule buffers, t int64 [B], n elements per sample. */
 int rdq_red_q_sample(int32_t B, int64_t n, const float *sqrt_ac, const float *sqrt_1mac, const int64_t *t,
                      const float *x0, const float *eps, float *xt, hipStream_t stream);
+/* The same, also copying t to t_out [B] in the launch: x_t and t written straight into the static input
+ * buffers of a captured U-Net forward (Unet.graph_io), so the replay needs no input copies. */
+int rdq_red_q_sample_t(int32_t B, int64_t n, const float *sqrt_ac, const float *sqrt_1mac, const int64_t *t,
+                       const float *x0, const float *eps, float *xt, int64_t *t_out, hipStream_t stream);
 /* RED epilogue (pred_noise objective, clip_x_start + rederive_pred_noise, diffusion.py:393-419):
  *   x0_hat = clamp(sr[t] x_t - srm1[t] eps_hat, -1, 1);  eps' = (sr[t] x_t - x0_hat) / srm1[t];
  *   g = eps' - eps   (regularization/diffusion.py:74). */

@@ -79,13 +79,17 @@ __device__ __forceinline__ float ig_gather(const IgArgs &a, bool pv, int b, int 
     }
 }
 
+// staging image of one k_conv_ig workgroup: Ws[2][IG_BN][IG_LDW], then As[2][IG_BK][IG_LDA]
+constexpr int IG_SMEM = 2 * IG_BN * IG_LDW + 2 * IG_BK * IG_LDA;
+
+// one (m tile bx, n tile by, K split) of the conv; smem = the IG_SMEM staging image
 template <int KH, int MODE>
-__global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
+__device__ __forceinline__ void conv_ig_tile(const IgArgs &a, int bx, int by, int split, float *smem)
 {
-    __shared__ __attribute__((aligned(16))) float Ws[2][IG_BN][IG_LDW];
-    __shared__ float As[2][IG_BK][IG_LDA];
+    auto &Ws = *reinterpret_cast<float (*)[2][IG_BN][IG_LDW]>(smem);
+    auto &As = *reinterpret_cast<float (*)[2][IG_BK][IG_LDA]>(smem + 2 * IG_BN * IG_LDW);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int m0 = blockIdx.x * IG_BM, n0 = blockIdx.y * IG_BN, split = blockIdx.z;
+    const int m0 = bx * IG_BM, n0 = by * IG_BN;
     const int N = a.d.cout, K = a.K;
     const int s_begin = split * a.per_split, s_end = min(a.nsteps, s_begin + a.per_split);
     // gather role: pixel gp, k rows gk + 8j
@@ -180,6 +184,13 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
     }
 }
 
+template <int KH, int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv_ig(IgArgs a)
+{
+    __shared__ __attribute__((aligned(16))) float sm[IG_SMEM];
+    conv_ig_tile<KH, MODE>(a, blockIdx.x, blockIdx.y, blockIdx.z, sm);
+}
+
 // split-K combine: fixed slab order, then bias and residual
 __global__ __launch_bounds__(256) void k_conv_reduce(int S, int64_t total, int N, int HW, const float *__restrict__ part,
                                                      const float *__restrict__ bias, const float *__restrict__ res,
@@ -239,8 +250,12 @@ struct CcArgs {
 constexpr int CC_SMEM = 2 * CC_BN * (CcCfg<9>::BK + 4) + 2 * CcCfg<9>::BK * CC_LDA;
 
 // one (m tile bx, n tile by, K split) of the conv on a gx x gy tile grid; smem = the CC_SMEM staging image
+// stages [s_begin, s_end) of tile (bx, by) on a gx x gy tile grid, as piece `split` of S pieces whose
+// slabs the last-arriving piece sums in piece order (S == 1: the whole K range, direct epilogue;
+// S < 0: slabs only, for k_conv_reduce); smem = the CC_SMEM staging image
 template <int TAPS, int MODE, bool RMS>
-__device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, int split, int gx, int gy, float *smem)
+__device__ __forceinline__ void conv_cc_seg(const CcArgs &a, int bx, int by, int s_begin, int s_end, int S, int split,
+                                            int gx, int gy, float *smem)
 {
     using C = CcCfg<TAPS>;
     constexpr int BK = C::BK, NA = C::NA, NWQ = C::NWQ, QPR = C::QPR, LDW = BK + 4;
@@ -252,7 +267,6 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
     const int m0 = bx * CC_BM, n0 = by * CC_BN;
     const rdq_conv_desc &d = a.d;
     const int N = d.cout, K = a.K;
-    const int s_begin = split * a.per_split, s_end = min(a.nstages, s_begin + a.per_split);
     // gather role: pixel gp, channel lane cl of the stage's chunk
     const int gp = tid & (CC_BM - 1), cl = tid >> 5;
     const int gm = m0 + gp;
@@ -436,7 +450,7 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
         }
     }
     // outputs of this lane: (n = n0 + wv*16 + (lane>>4)*4 + r, m = m0 + j*16 + (lane&15))
-    if (a.S < 0) {                         // slabs [S][B][cout][HW] for k_conv_reduce
+    if (S < 0) {                         // slabs [S][B][cout][HW] for k_conv_reduce
         const size_t slab = (size_t)a.M * N;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -450,7 +464,7 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
         }
         return;
     }
-    if (a.S > 1) {
+    if (S > 1) {
         // in-launch combine.  Slabs in the tile's own register order (lane tid's 8 accumulators as
         // two 16-B words), written and read write-through (sc1) so no L2 fence is needed:
         // every storing wave drains its stores, the workgroup barrier, one agent-scope ticket add per
@@ -466,14 +480,14 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         unsigned *tk = a.tickets + tile;
-        if (tid == 0) last_s = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(a.S - 1);
+        if (tid == 0) last_s = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
         __syncthreads();
         if (!last_s) return;
         // slabs summed in slab order, four slabs' loads in flight at a time
         f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff, tbase, CC_SC1));
         f32x4 v1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff + 16, tbase, CC_SC1));
         int s = 1;
-        for (; s + 4 <= a.S; s += 4) {
+        for (; s + 4 <= S; s += 4) {
             f32x4 t0[4], t1[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -483,7 +497,7 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
 #pragma unroll
             for (int u = 0; u < 4; ++u) { v0 += t0[u]; v1 += t1[u]; }
         }
-        for (; s < a.S; ++s) {
+        for (; s < S; ++s) {
             v0 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff, s * sbytes + tbase, CC_SC1));
             v1 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, voff + 16, s * sbytes + tbase, CC_SC1));
         }
@@ -594,11 +608,49 @@ __device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, in
     }
 }
 
+template <int TAPS, int MODE, bool RMS>
+__device__ __forceinline__ void conv_cc_tile(const CcArgs &a, int bx, int by, int split, int gx, int gy, float *smem)
+{
+    const int s_begin = split * a.per_split, s_end = min(a.nstages, s_begin + a.per_split);
+    conv_cc_seg<TAPS, MODE, RMS>(a, bx, by, s_begin, s_end, a.S, split, gx, gy, smem);
+}
+
 template <int TAPS, int MODE, bool RMS = false>
 __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
 {
     __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
     conv_cc_tile<TAPS, MODE, RMS>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sm);
+}
+
+// Stream-K form of k_conv_cc for grids of a few rounds of workgroups (B = 8 at 72 x 72: 1296 tiles on
+// 512 workgroup slots = 2.53 rounds, the last one half empty).  The gx * gy * nstages (tile, K stage)
+// units are dealt in equal contiguous ranges to exactly gridDim.x workgroups (one round); a range
+// covers the tail of one tile, whole tiles and the head of another.  A tile cut by range boundaries
+// is computed in pieces whose slabs the last-arriving piece sums in piece order (conv_cc_seg's
+// in-launch combine), so the result is deterministic for a given grid.  Needs U >= gridDim.x
+// (strictly increasing boundaries: every piece is non-empty) — the host checks.
+__device__ __forceinline__ int sk_cnt(int64_t x, int64_t U, int64_t P)   // range starts <= unit x
+{
+    return (int)min(P, ((x + 1) * P + U - 1) / U);
+}
+template <int TAPS, int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv_cc_sk(CcArgs a, int gx, int gy)
+{
+    __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
+    const int nst = a.nstages;
+    const int64_t U = (int64_t)gx * gy * nst, P = gridDim.x;
+    int64_t u = (int64_t)blockIdx.x * U / P;
+    const int64_t u1 = ((int64_t)blockIdx.x + 1) * U / P;
+    while (u < u1) {
+        const int T = (int)(u / nst);
+        const int64_t t0 = (int64_t)T * nst;
+        const int s0 = (int)(u - t0), s1 = (int)min<int64_t>(nst, s0 + (u1 - u));
+        const int c0 = sk_cnt(t0, U, P);
+        const int pieces = 1 + sk_cnt(t0 + nst - 1, U, P) - c0, piece = sk_cnt(u, U, P) - c0;
+        conv_cc_seg<TAPS, MODE, false>(a, T % gx, T / gx, s0, s1, pieces, piece, gx, gy, sm);
+        __syncthreads();                          // the staging image is reused by the next piece
+        u = t0 + s1;
+    }
 }
 
 // A ResnetBlock with a 1x1 shortcut (the U-Net's up path and final block, diffusion.py:160-168):
@@ -659,6 +711,36 @@ int cc_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
     const int per = (nstages + S - 1) / S;
     *per_split = per;
     return (nstages + per - 1) / per;
+}
+
+// Stream-K plan of a channel-chunk conv (k_conv_cc_sk): the workgroup count P (two per CU, one round)
+// when the tile grid takes more than one round and its last round would be at most 80 % full, else 0;
+// *maxp = the most pieces any tile is cut into (slab slots per tile).
+static int cu_count()
+{
+    static int cus[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+int cc_streamk(const rdq_conv_desc *d, int *maxp)
+{
+    *maxp = 1;
+    if (getenv("RDQ_NO_STREAMK")) return 0;
+    const int64_t M = (int64_t)d->B * d->H * d->W;
+    const int64_t tiles = ((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN);
+    const int nst = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
+    const int64_t P = 2 * (int64_t)cu_count();
+    if (P <= 0 || tiles <= P || tiles >= 8 * P || tiles % P == 0 || (tiles % P) * 5 > P * 4) return 0;
+    const int64_t U = tiles * nst, per = U / P;              // every range >= per units
+    if (per < std::max(3, nst / 2)) return 0;
+    *maxp = (int)(1 + (nst - 1 + per - 1) / per);            // interior range starts in one tile
+    return (int)P;
 }
 
 // split count: about one workgroup per CU over the tile grid, >= 4 K stages per split, and the
@@ -848,6 +930,87 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     }
 }
 
+// The U-Net's last two steps in one pass (diffusion.py:299-301): final_res_block's block2
+// normalise pass (k_gn_apply_t's arithmetic: statistics from the conv's per-tile partials, GN ->
+// scale/shift -> SiLU, + the res_conv shortcut) feeding final_conv, a 1x1 conv to NF <= 4 channels,
+// without writing the C-channel activation.  Workgroup = 64 pixels of one sample, 16 waves; wave w takes
+// channels [w C/16, (w+1) C/16) and the 1x1 sums are combined over the waves in wave order.
+constexpr int GO_MAXF = 4, GO_NW = 16;
+__global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int G, const float *__restrict__ x,
+                                                             const float *__restrict__ gamma,
+                                                             const float *__restrict__ beta,
+                                                             const float *__restrict__ ss,
+                                                             const double *__restrict__ gnp, float eps,
+                                                             const float *__restrict__ post, int NF,
+                                                             const float *__restrict__ wf,
+                                                             const float *__restrict__ bf, float *__restrict__ yf)
+{
+    __shared__ float st[64][2];
+    __shared__ float part[GO_NW][GO_MAXF][64];
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int p = blockIdx.x * 64 + lane, cpg = C / G;
+    const int cpw = (C + GO_NW - 1) / GO_NW, c0 = wv * cpw, c1 = min(C, c0 + cpw);
+    const bool pv = p < HW;
+    const int pc = pv ? p : HW - 1;
+    // this lane's elements and shortcut values first: their loads overlap the statistics below
+    float xv[4], rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int c = min(c0 + u, C - 1);
+        const size_t o = ((size_t)b * C + c) * HW + pc;
+        xv[u] = x[o];
+        rv[u] = post ? post[o] : 0.0f;
+    }
+    // (sample, group) statistics: wave w reduces groups w, w + GO_NW, ... exactly as k_gn_apply_t's wave 0
+    for (int g = wv; g < G; g += GO_NW) {
+        const int mlo = (int)(((int64_t)b * HW) / CC_BM), mhi = (int)(((int64_t)(b + 1) * HW - 1) / CC_BM);
+        double s = 0.0, q = 0.0;
+        for (int mt = mlo + lane; mt <= mhi; mt += 64) {
+            const int slot = (int)(((int64_t)mt * CC_BM) / HW) == b ? 0 : 1;
+            const double *pp = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
+            s += pp[0];
+            q += pp[1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            q += __shfl_xor(q, o, 64);
+        }
+        if (lane == 0) {
+            const double n = (double)cpg * HW, mean = s / n;
+            double var = q / n - mean * mean;
+            var = var < 0.0 ? 0.0 : var;
+            st[g][0] = (float)mean;
+            st[g][1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+    }
+    __syncthreads();
+    float acc[GO_MAXF] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool sso = ss != nullptr;
+    for (int c = c0; c < c1; ++c) {
+        const int u = c - c0, g = c / cpg;
+        const float xe = u < 4 ? xv[u] : x[((size_t)b * C + c) * HW + pc];
+        const float re = u < 4 ? rv[u] : (post ? post[((size_t)b * C + c) * HW + pc] : 0.0f);
+        const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
+        float v = gn_silu1(xe, st[g][0], st[g][1], gamma[c], beta[c], sso, sc1, sh);
+        if (post) v += re;
+#pragma unroll
+        for (int f = 0; f < GO_MAXF; ++f)
+            if (f < NF) acc[f] += wf[(size_t)f * C + c] * v;
+    }
+#pragma unroll
+    for (int f = 0; f < GO_MAXF; ++f)
+        if (f < NF) part[wv][f][lane] = acc[f];
+    __syncthreads();
+    if (wv == 0 && pv) {
+        for (int f = 0; f < NF; ++f) {
+            float v = part[0][f][lane];
+            for (int w = 1; w < GO_NW; ++w) v += part[w][f][lane];
+            yf[((size_t)b * NF + f) * HW + p] = v + (bf ? bf[f] : 0.0f);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------- rmsnorm
 // 64 pixels (lanes, coalesced) x 16 channel groups (waves) per workgroup: the channel sum of squares
 // is split over the waves and combined in LDS in a fixed order, so small-HW stages (9x9 x 512
@@ -1004,14 +1167,23 @@ __device__ __forceinline__ float wave_dot(const float *__restrict__ w, const flo
     for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
     return s;
 }
-__global__ __launch_bounds__(256) void k_time_mlp(int dim, float neg_emb, const int64_t *__restrict__ t,
-                                                  const float *__restrict__ w1, const float *__restrict__ b1, int hid,
-                                                  const float *__restrict__ w2, const float *__restrict__ b2, int out,
-                                                  float *__restrict__ y)
+struct TmArgs {
+    int dim, hid, out;
+    float neg_emb;
+    const int64_t *t;
+    const float *w1, *b1, *w2, *b2;
+    float *y;
+};
+// row block bx of sample b; sm: dim + hid floats
+__device__ __forceinline__ void time_mlp_rows(const TmArgs &m, int bx, int b, float *sm)
 {
-    extern __shared__ float tm_sm[];
-    float *e = tm_sm, *h = tm_sm + dim;
-    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int dim = m.dim, hid = m.hid, out = m.out;
+    const float neg_emb = m.neg_emb;
+    const int64_t *__restrict__ t = m.t;
+    const float *__restrict__ w1 = m.w1, *__restrict__ b1 = m.b1, *__restrict__ w2 = m.w2, *__restrict__ b2 = m.b2;
+    float *__restrict__ y = m.y;
+    float *e = sm, *h = sm + dim;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = dim / 2;
     for (int i = tid; i < half; i += 256) {
         const float f = expf((float)i * neg_emb);
@@ -1038,10 +1210,15 @@ __global__ __launch_bounds__(256) void k_time_mlp(int dim, float neg_emb, const 
         h[o] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
     }
     __syncthreads();
-    const int o = blockIdx.x * TM_ROWS + wv;
+    const int o = bx * TM_ROWS + wv;
     if (o >= out) return;
     const float s = wave_dot(w2 + (size_t)o * hid, h, hid, lane, false);
     if (lane == 0) y[(size_t)b * out + o] = s + b2[o];
+}
+__global__ __launch_bounds__(256) void k_time_mlp(TmArgs m)
+{
+    extern __shared__ float tm_sm[];
+    time_mlp_rows(m, blockIdx.x, blockIdx.y, tm_sm);
 }
 
 // every ResnetBlock's time MLP, Linear(SiLU(t)) (diffusion.py:157-165), in one launch: up to
@@ -1055,6 +1232,59 @@ struct LinMulti {
     int start[LM_MAX + 1];
     int n;
 };
+// LSM_RPW rows of the multi-linear per wave, their weight loads issued together; each row's
+// arithmetic is wave_dot's (same order: k_linear_silu_multi's results bit for bit).  Workgroup blk
+// of sample b: rows [blk * 4 * LSM_RPW, (blk + 1) * 4 * LSM_RPW).  Used as a side job of the
+// first ResnetBlock's conv launch (k_conv_cc_lsm).
+constexpr int LSM_RPW = 8;
+template <int RPW>
+__device__ __forceinline__ void lsm_rows(int in, const float *__restrict__ x, const LinMulti &L, int blk, int b)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g0 = (blk * 4 + wv) * RPW, gend = L.start[L.n];
+    if (g0 >= gend) return;
+    const float *wr[RPW];
+    float *yo[RPW];
+    float bo[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int go = min(g0 + r, gend - 1);
+        int j = 0;
+        while (go >= L.start[j + 1]) ++j;
+        const int o = go - L.start[j];
+        wr[r] = L.w[j] + (size_t)o * in;
+        yo[r] = g0 + r < gend ? L.y[j] + (size_t)b * L.out[j] + o : nullptr;
+        bo[r] = L.b[j] ? L.b[j][o] : 0.0f;
+    }
+    const float *xb = x + (size_t)b * in;
+    float s[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) s[r] = 0.0f;
+    for (int i0 = 0; i0 < in; i0 += 256) {
+        float wv4[RPW][4];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wv4[r][u] = wr[r][min(i0 + lane + 64 * u, in - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + lane + 64 * u;
+            if (i < in) {
+                float v = xb[i];
+                v = v / (1.0f + expf(-v));
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) s[r] += wv4[r][u] * v;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        float v = s[r];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        if (lane == 0 && yo[r]) *yo[r] = v + bo[r];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_linear_silu_multi(int in, const float *__restrict__ x, LinMulti L)
 {
     const int go = blockIdx.x * 4 + (threadIdx.x >> 6), b = blockIdx.y, lane = threadIdx.x & 63;
@@ -1064,6 +1294,41 @@ __global__ __launch_bounds__(256) void k_linear_silu_multi(int in, const float *
     const int o = go - L.start[j];
     const float s = wave_dot(L.w[j] + (size_t)o * in, x + (size_t)b * in, in, lane, true);
     if (lane == 0) L.y[j][(size_t)b * L.out[j] + o] = s + (L.b[j] ? L.b[j][o] : 0.0f);
+}
+
+// The U-Net's first launch (Unet.forward, diffusion.py:276-279): init_conv (k_conv_ig tiles,
+// blockIdx.x < gxc; a single n tile, no K split) and the time MLP (the rest of the grid, as
+// k_time_mlp) are independent, so they share one launch.  Each role's arithmetic is that of its
+// own kernel, bit for bit.
+template <int KH>
+__global__ __launch_bounds__(256, 2) void k_unet_head(IgArgs a, int gxc, TmArgs m, int tm_x)
+{
+    __shared__ __attribute__((aligned(16))) float sm[IG_SMEM];
+    const int bx = blockIdx.x;
+    if (bx < gxc) {
+        conv_ig_tile<KH, RDQ_IN_PLAIN>(a, bx, 0, 0, sm);
+    } else {
+        const int r = bx - gxc;
+        time_mlp_rows(m, r % tm_x, r / tm_x, sm);
+    }
+}
+
+// The first ResnetBlock's conv (GroupNorm statistics in its epilogue) with every ResnetBlock's
+// Linear(SiLU(t)) as a side job: blockIdx.x < nlsm (y = z = 0) runs lsm_rows, the rest the conv tiles
+// of k_conv_cc.  Measured at B = 1 (tools/lsm_ab.py): 1.7 us under the two separate launches — the
+// side job's workgroups slow the conv about as much as their own launch costs, so the Python side
+// uses this form for B <= 2 only.  The GroupNorm pass that follows reads this block's scale/shift.
+template <int TAPS, int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv_cc_lsm(CcArgs a, LinMulti L, int in, const float *temb, int nlsm,
+                                                        int lsm_per_b)
+{
+    __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
+    const int bx = blockIdx.x;
+    if (bx < nlsm) {
+        if (blockIdx.y == 0 && blockIdx.z == 0) lsm_rows<LSM_RPW>(in, temb, L, bx % lsm_per_b, bx / lsm_per_b);
+        return;
+    }
+    conv_cc_tile<TAPS, MODE, false>(a, bx - nlsm, blockIdx.y, blockIdx.z, gridDim.x - nlsm, gridDim.y, sm);
 }
 
 // -------------------------------------------------------------------------- linear attention
@@ -1585,12 +1850,13 @@ __global__ __launch_bounds__(256) void k_full_attn(int heads, int n, int nmem, c
 __global__ __launch_bounds__(256) void k_red_q_sample(int64_t n, const float *__restrict__ sa,
                                                       const float *__restrict__ s1a, const int64_t *__restrict__ t,
                                                       const float *__restrict__ x0, const float *__restrict__ eps,
-                                                      float *__restrict__ xt)
+                                                      float *__restrict__ xt, int64_t *__restrict__ t_out)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (i >= n) return;
     const int64_t tb = t[b];
+    if (t_out && i == 0) t_out[b] = tb;
     const size_t o = (size_t)b * n + i;
     const float a1 = sa[tb] * x0[o];
     const float a2 = s1a[tb] * eps[o];
@@ -2092,6 +2358,29 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 }
 }  // namespace
 
+// k_conv_cc_sk in place of k_conv_cc when cc_streamk plans it, tickets are given and ws holds the
+// pieces' slabs; false: not taken (the caller launches k_conv_cc)
+static bool launch_streamk(const CcArgs &c0, const rdq_conv_desc *d, size_t ws_bytes, int gx, int gy, hipStream_t st)
+{
+    int maxp = 1;
+    const int P = cc_streamk(d, &maxp);
+    if (!P || !c0.tickets || !c0.part || (size_t)maxp * gx * gy * CC_BM * CC_BN * sizeof(float) > ws_bytes ||
+        d->in_mode == RDQ_IN_UNSHUFFLE2)
+        return false;
+    CcArgs c = c0;
+    c.S = 1;
+    c.per_split = c.nstages;
+    if (d->kh == 3) {
+        if (d->in_mode == RDQ_IN_UPSAMPLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<9, RDQ_IN_UPSAMPLE2>), dim3(P), dim3(256), 0, st, c, gx, gy);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<9, RDQ_IN_PLAIN>), dim3(P), dim3(256), 0, st, c, gx, gy);
+    } else {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<1, RDQ_IN_PLAIN>), dim3(P), dim3(256), 0, st, c, gx, gy);
+    }
+    return true;
+}
+
 extern "C" {
 
 size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
@@ -2101,12 +2390,19 @@ size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
     return (size_t)(((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN));
 }
 
+int rdq_conv2d_streamk(const rdq_conv_desc *d)
+{
+    int maxp = 1;
+    return d && cc_ok(d) && d->in_mode != RDQ_IN_UNSHUFFLE2 ? cc_streamk(d, &maxp) : 0;
+}
+
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d)
 {
     if (!d || d->B < 1 || d->H < 1 || d->W < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->cin1 < 1) return 0;
     int per = 0;
     if (cc_ok(d)) {
-        const int S = cc_splits(d, (size_t)-1 / 2, &per);
+        int maxp = 1;
+        const int S = std::max(cc_splits(d, (size_t)-1 / 2, &per), cc_streamk(d, &maxp) ? maxp : 1);
         return S > 1 ? (size_t)S * rdq_conv2d_tickets(d) * CC_BM * CC_BN * sizeof(float) : 0;
     }
     const int S = ig_splits(d, (size_t)-1 / 2, &per);
@@ -2137,6 +2433,10 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         const bool fold = c.S > 1 && tickets;        // combine in the conv launch
         if (c.S > 1 && !tickets) c.tickets = nullptr;
         const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+        if (launch_streamk(c, d, ws_bytes, grid.x, grid.y, st)) {
+            RDQ_CHECK(hipGetLastError());
+            return 0;
+        }
         CcArgs cl = c;
         if (c.S > 1 && !fold) cl.S = -c.S;            // slabs only; k_conv_reduce combines
         if (d->kh == 3) {
@@ -2191,26 +2491,23 @@ size_t rdq_conv2d_gn_ws_bytes(const rdq_conv_desc *d, int32_t G)
     return rdq_conv2d_ws_bytes(d) + M * d->cout * sizeof(float) + mt * G * 4 * sizeof(double);
 }
 
-int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
-                       int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
-                       const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
-                       hipStream_t st)
+// arguments of the conv of rdq_conv2d_gn_silu (output and statistics in ws); false: not applicable
+static bool gn_conv_args(CcArgs &c, const rdq_conv_desc *d, const float *x, const float *x2, const float *w,
+                         const float *bias, int32_t G, void *ws, size_t ws_bytes, uint32_t *tickets)
 {
     const size_t need = rdq_conv2d_gn_ws_bytes(d, G);
-    if (!need || !x || !w || !y || !gamma || !beta || !ws || ws_bytes < need ||
-        (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
-        return RDQ_E_INVALID;
-    if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return RDQ_E_INVALID;
-    if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return RDQ_E_INVALID;
+    if (!need || !x || !w || !ws || ws_bytes < need || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        return false;
+    if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return false;
+    if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return false;
     const size_t M = (size_t)d->B * d->H * d->W;
     const size_t slabs = rdq_conv2d_ws_bytes(d);
     float *h = reinterpret_cast<float *>(static_cast<char *>(ws) + slabs);
-    double *gnp = reinterpret_cast<double *>(h + M * d->cout);
-    CcArgs c{};
+    c = CcArgs{};
     c.d = *d; c.x = x; c.x2 = x2; c.w = w; c.bias = bias; c.res = nullptr; c.y = h;
     c.part = static_cast<float *>(ws);
     c.tickets = tickets;
-    c.gnp = gnp;
+    c.gnp = reinterpret_cast<double *>(h + M * d->cout);
     c.G = G;
     c.K = (d->cin1 + d->cin2) * d->kh * d->kw;
     c.HW = d->H * d->W;
@@ -2219,8 +2516,21 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     c.nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
     c.S = (slabs && tickets) ? cc_splits(d, slabs, &c.per_split) : 1;   // statistics need the in-launch combine
     if (c.S == 1) c.per_split = c.nstages;
+    return true;
+}
+
+int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                       int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                       const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
+                       hipStream_t st)
+{
+    CcArgs c;
+    if (!y || !gamma || !beta || !gn_conv_args(c, d, x, x2, w, bias, G, ws, ws_bytes, tickets)) return RDQ_E_INVALID;
+    float *h = c.y;
+    double *gnp = c.gnp;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-    if (d->kh == 3) {
+    if (launch_streamk(c, d, rdq_conv2d_ws_bytes(d), grid.x, grid.y, st)) {
+    } else if (d->kh == 3) {
         if (d->in_mode == RDQ_IN_UPSAMPLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
         else
@@ -2305,6 +2615,102 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
     const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
     hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, c.gnp, eps, nullptr, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_conv2d_gn_silu_lsm(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                           int32_t G, float eps, const float *gamma, const float *beta, const float *post_residual,
+                           float *y, void *ws, size_t ws_bytes, uint32_t *tickets, int32_t in, const float *temb,
+                           int32_t n, const float *const *lw, const float *const *lb, const int32_t *lout,
+                           float *const *ly, int32_t ss_index, hipStream_t st)
+{
+    CcArgs c;
+    if (!y || !gamma || !beta || !temb || in < 1 || n < 1 || n > LM_MAX || !lw || !lout || !ly ||
+        ss_index >= n || d->in_mode != RDQ_IN_PLAIN || !gn_conv_args(c, d, x, x2, w, bias, G, ws, ws_bytes, tickets))
+        return RDQ_E_INVALID;
+    LinMulti L{};
+    L.n = n;
+    L.start[0] = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!lw[j] || !ly[j] || lout[j] < 1) return RDQ_E_INVALID;
+        L.w[j] = lw[j];
+        L.b[j] = lb ? lb[j] : nullptr;
+        L.y[j] = ly[j];
+        L.out[j] = lout[j];
+        L.start[j + 1] = L.start[j] + lout[j];
+    }
+    if (ss_index >= 0 && lout[ss_index] != 2 * d->cout) return RDQ_E_INVALID;
+    const int per_b = (L.start[n] + 4 * LSM_RPW - 1) / (4 * LSM_RPW), nlsm = per_b * d->B;
+    const dim3 grid(nlsm + (c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+    if (d->kh == 3)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_lsm<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c, L, in, temb,
+                           nlsm, per_b);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_lsm<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c, L, in, temb,
+                           nlsm, per_b);
+    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
+    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, c.y, gamma, beta,
+                       ss_index >= 0 ? ly[ss_index] : nullptr, c.gnp, eps, post_residual, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                           int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                           const float *post_residual, int32_t nf, const float *wf, const float *bf, float *yf,
+                           void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t st)
+{
+    CcArgs c;
+    if (!yf || !wf || !gamma || !beta || nf < 1 || nf > GO_MAXF || d->cout % 4 || G > 64 ||
+        !gn_conv_args(c, d, x, x2, w, bias, G, ws, ws_bytes, tickets))
+        return RDQ_E_INVALID;
+    const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
+    if (launch_streamk(c, d, rdq_conv2d_ws_bytes(d), grid.x, grid.y, st)) {
+    } else if (d->kh == 3) {
+        if (d->in_mode == RDQ_IN_UPSAMPLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+    } else {
+        if (d->in_mode == RDQ_IN_UNSHUFFLE2)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+    }
+    const int HW = c.HW;
+    hipLaunchKernelGGL(k_gn_apply_out, dim3((HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, HW, G, c.y, gamma, beta,
+                       scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_unet_head(const rdq_conv_desc *d, const float *x, const float *w, const float *bias, float *y, int32_t dim,
+                  float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid, const float *w2,
+                  const float *b2, int32_t out, float *temb, hipStream_t st)
+{
+    if (!d || !x || !w || !y || !t || !w1 || !b1 || !w2 || !b2 || !temb || d->B < 1 || d->cin1 < 1 ||
+        d->cin2 != 0 || d->in_mode != RDQ_IN_PLAIN || d->cout < 1 || d->cout > IG_BN || d->kh != d->kw ||
+        (d->kh != 7 && d->kh != 3) || d->pad < 0 || d->H < 1 || d->W < 1 || cc_ok(d))
+        return RDQ_E_INVALID;
+    if (dim < 4 || dim % 2 || hid < 1 || out < 1 || dim + hid > IG_SMEM) return RDQ_E_INVALID;
+    IgArgs a{};
+    a.d = *d; a.x = x; a.x2 = nullptr; a.w = w; a.bias = bias; a.res = nullptr; a.y = y;
+    a.K = d->cin1 * d->kh * d->kw;
+    a.HW = d->H * d->W;
+    a.M = d->B * a.HW;
+    a.nsteps = (a.K + IG_BK - 1) / IG_BK;
+    int per = 0;
+    if (ig_splits(d, (size_t)-1 / 2, &per) != 1) return RDQ_E_INVALID;    // rdq_conv2d would split K
+    a.S = 1;
+    a.per_split = a.nsteps;
+    const int half = dim / 2;
+    const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
+    const TmArgs m{dim, hid, out, -emb, t, w1, b1, w2, b2, temb};
+    const int gxc = (a.M + IG_BM - 1) / IG_BM, tm_x = (out + TM_ROWS - 1) / TM_ROWS;
+    const dim3 grid(gxc + tm_x * d->B);
+    if (d->kh == 7) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_unet_head<7>), grid, dim3(256), 0, st, a, gxc, m, tm_x);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_unet_head<3>), grid, dim3(256), 0, st, a, gxc, m, tm_x);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -2473,8 +2879,8 @@ int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const fl
         return RDQ_E_INVALID;
     const int half = dim / 2;
     const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
-    hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float), st,
-                       dim, -emb, t, w1, b1, hid, w2, b2, out, y);
+    const TmArgs m{dim, hid, out, -emb, t, w1, b1, w2, b2, y};
+    hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float), st, m);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -2570,7 +2976,18 @@ int rdq_red_q_sample(int32_t B, int64_t n, const float *sa, const float *s1a, co
                      const float *eps, float *xt, hipStream_t st)
 {
     if (B < 1 || n < 1 || !sa || !s1a || !t || !x0 || !eps || !xt) return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_red_q_sample, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, st, n, sa, s1a, t, x0, eps, xt);
+    hipLaunchKernelGGL(k_red_q_sample, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, st, n, sa, s1a, t, x0, eps, xt,
+                       (int64_t *)nullptr);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_red_q_sample_t(int32_t B, int64_t n, const float *sa, const float *s1a, const int64_t *t, const float *x0,
+                       const float *eps, float *xt, int64_t *t_out, hipStream_t st)
+{
+    if (B < 1 || n < 1 || !sa || !s1a || !t || !x0 || !eps || !xt || !t_out) return RDQ_E_INVALID;
+    hipLaunchKernelGGL(k_red_q_sample, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, st, n, sa, s1a, t, x0, eps, xt,
+                       t_out);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

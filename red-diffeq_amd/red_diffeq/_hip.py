@@ -72,6 +72,7 @@ SIGNATURES = {
     # include/red_diffeq_unet.h
     "rdq_conv2d_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_tickets": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rdq_conv2d_streamk": (c_int32, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p, c_void_p]),
     "rdq_conv2d_rms": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -85,6 +86,15 @@ SIGNATURES = {
     "rdq_conv2d_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                      c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_void_p, c_void_p]),
+    "rdq_conv2d_gn_silu_lsm": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                         c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                         c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_int32, c_void_p]),
+    "rdq_conv2d_gn_silu_out": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                         c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "rdq_unet_head": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_float,
+                                c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_wpack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16_pack": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
@@ -111,6 +121,8 @@ SIGNATURES = {
                                      c_void_p]),
     "rdq_red_q_sample": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
+    "rdq_red_q_sample_t": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
     "rdq_red_epilogue": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     # include/red_diffeq_loop.h

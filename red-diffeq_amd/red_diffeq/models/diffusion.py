@@ -275,6 +275,37 @@ class Unet(nn.Module):
         return getattr(self, "_wgen", 0)
 
     def _graphed(self, x, time):
+        ent = self._graph_entry(x, time)
+        ent["x"].copy_(x)
+        ent["t"].copy_(time)
+        ent["graph"].replay()
+        return ent["y"].clone()
+
+    def graph_io(self, shape, device, time_dtype=torch.int64):
+        """The static (x, t) input buffers of the captured no-grad forward for inputs of `shape` (None
+        where forward() would not replay a graph).  A caller that writes its inputs straight into them
+        (ops.red_q_sample_into, the RED regulariser) and calls replay_static() pays neither the input
+        copies nor the output clone of forward()."""
+        B, _, H, W = shape
+        if (torch.device(device).type != "cuda" or torch.is_grad_enabled() or self.self_condition
+                or B * H * W > self.GRAPH_MAX_PIXELS or os.environ.get("RDQ_NO_UNET_GRAPH")
+                or torch.cuda.is_current_stream_capturing()):
+            return None
+        x = torch.zeros(shape, device=device, dtype=torch.float32)
+        ent = self._graph_entry(x, torch.zeros(B, device=device, dtype=time_dtype))
+        return ent["x"], ent["t"]
+
+    def replay_static(self, xs, ts):
+        """Replay the forward captured for the static buffers (xs, ts) of graph_io; returns the static
+        output (overwritten by the next replay of the same shape)."""
+        ent = self._graph_entry(xs, ts)
+        assert ent["x"] is xs and ent["t"] is ts, "replay_static: not this graph's static inputs"
+        ent["graph"].replay()
+        return ent["y"]
+
+    def _graph_entry(self, x, time):
+        """The captured forward for x's shape and time's dtype (captured now, on copies of x / time as its
+        static inputs, if missing or stale)."""
         key = (tuple(x.shape), x.dtype, x.device, self.precision, time.dtype)
         cache = self.__dict__.setdefault("_graphs", {})
         ver = self._weights_version()
@@ -291,22 +322,27 @@ class Unet(nn.Module):
                 ys = self._forward(xs, ts, None)
             ent = {"ver": ver, "graph": graph, "x": xs, "t": ts, "y": ys}
             cache[key] = ent
-        ent["x"].copy_(x)
-        ent["t"].copy_(time)
-        ent["graph"].replay()
-        return ent["y"].clone()
+        return ent
 
     def _forward(self, x, time, x_self_cond):
         if self.self_condition:
             x_self_cond = default(x_self_cond, lambda: torch.zeros_like(x))
             x = torch.cat((x_self_cond, x), dim=1)
-        x = ops.conv2d(x, self.init_conv)
+        x, t = ops.head(x, self.init_conv, time, self.time_mlp)          # init_conv + time_mlp: one launch
         r = x
-        t = self._time(time)
-        ss = iter(ops.resnet_scale_shifts(t, self._resnet_blocks()))    # all blocks' Linear(SiLU(t))
+        blocks = self._resnet_blocks()
+        first = ops.first_block_and_scale_shifts(x, self.downs[0][0], t, blocks)
+        if first is None:
+            ss = iter(ops.resnet_scale_shifts(t, blocks))                 # all blocks' Linear(SiLU(t))
+        else:
+            ss = iter(first[1])                 # formed in the first block's conv launch
         h = []
-        for b1, b2, attn, down in self.downs:
-            x = b1(x, t, scale_shift=next(ss))
+        for i, (b1, b2, attn, down) in enumerate(self.downs):
+            if i == 0 and first is not None:
+                x = first[0]
+                next(ss)
+            else:
+                x = b1(x, t, scale_shift=next(ss))
             h.append(x)
             x = b2(x, t, scale_shift=next(ss))
             x = attn(x)                       # attn(x) + x
@@ -320,7 +356,11 @@ class Unet(nn.Module):
             x = b2(x, t, skip=h.pop(), scale_shift=next(ss))
             x = attn(x)
             x = self._resample(x, up)
-        x = self.final_res_block(x, t, skip=r, scale_shift=next(ss))
+        ss_last = next(ss)
+        out = ops.last_block_and_out(x, self.final_res_block, ss_last, r, self.final_conv)
+        if out is not None:
+            return out                          # final_res_block's last pass feeds final_conv
+        x = self.final_res_block(x, t, skip=r, scale_shift=ss_last)
         return ops.conv2d(x, self.final_conv)
 
 

@@ -66,6 +66,62 @@ def resnet_scale_shifts(t, blocks):
     return out
 
 
+# The fused first / last launches of Unet.forward (head, first_block_and_scale_shifts,
+# last_block_and_out); False: the separate-launch sequence (tests compare the two)
+FUSED_EDGES = True
+
+
+def head(x, init_conv, time, seq):
+    """(init_conv(x), Unet.time_mlp(time)) in ONE launch (rdq_unet_head) where that form applies, else
+    the two separate launches.  The stem conv runs in fp32 under either precision (bf16_eligible)."""
+    pad = init_conv.padding[0] if isinstance(init_conv.padding, tuple) else int(init_conv.padding)
+    if FUSED_EDGES and ops.unet_head_fusable(x, init_conv.weight, seq):
+        return torch.ops.red_diffeq.unet_head(x, init_conv.weight, init_conv.bias, pad, time, seq[0].dim,
+                                              float(seq[0].theta), seq[1].weight, seq[1].bias, seq[3].weight,
+                                              seq[3].bias)
+    return conv2d(x, init_conv), time_mlp(time, seq)
+
+
+def first_block_and_scale_shifts(x, block, t, blocks):
+    """(block(x, scale_shift = its Linear(SiLU(t))), [Linear(SiLU(t)) of every block in `blocks`]) for a
+    ResnetBlock with an identity shortcut that is blocks[0]: all the time projections are formed as a
+    side job of block1's conv launch (rdq_conv2d_gn_silu_lsm).  None where that form does not apply."""
+    b1 = block.block1
+    # B <= 2: beyond, the side job costs more than its own launch (tools/lsm_ab.py)
+    if not FUSED_EDGES or _PREC["mode"] != "fp32" or x.shape[0] > 2 or not blocks or blocks[0] is not block or \
+            len(blocks) > 32 or \
+            isinstance(block.res_conv, torch.nn.Conv2d) or any(b.mlp is None for b in blocks):
+        return None
+    pad = b1.proj.padding[0] if isinstance(b1.proj.padding, tuple) else int(b1.proj.padding)
+    if not ops.conv_gn_fusable(x, None, b1.proj.weight, pad, PLAIN, b1.norm.num_groups):
+        return None
+    h, ss = torch.ops.red_diffeq.conv2d_gn_silu_lsm(
+        x, b1.proj.weight, b1.proj.bias, pad, b1.norm.weight, b1.norm.bias, b1.norm.num_groups, float(b1.norm.eps),
+        None, t, [b.mlp[1].weight for b in blocks], [b.mlp[1].bias for b in blocks], 0)
+    return block.block2(h, post=x), ss
+
+
+def last_block_and_out(x, block, scale_shift, skip, out_conv):
+    """out_conv(block(x, skip, scale_shift)) for a ResnetBlock with a 1x1 shortcut followed by a 1x1
+    conv to <= 4 channels (final_res_block + final_conv): block2's normalise pass feeds out_conv
+    directly (rdq_conv2d_gn_silu_out).  None where that form does not apply."""
+    b2 = block.block2
+    if not FUSED_EDGES or _PREC["mode"] != "fp32" or out_conv.weight.shape[-1] != 1 or out_conv.weight.shape[0] > 4 or \
+            b2.proj.weight.shape[0] % 4:
+        return None
+    pad = b2.proj.padding[0] if isinstance(b2.proj.padding, tuple) else int(b2.proj.padding)
+    hshape = (x.shape[0], b2.proj.weight.shape[1], x.shape[2], x.shape[3])
+    if not ops.conv_gn_fusable(torch.empty(hshape, device="meta"), None, b2.proj.weight, pad, PLAIN,
+                               b2.norm.num_groups):
+        return None
+    pair = conv_group_norm_silu_shortcut(x, block.block1.proj, block.block1.norm, scale_shift, skip, block.res_conv)
+    if pair is None:
+        return None
+    return torch.ops.red_diffeq.conv2d_gn_silu_out(pair[0], b2.proj.weight, b2.proj.bias, pad, b2.norm.weight,
+                                                   b2.norm.bias, None, b2.norm.num_groups, float(b2.norm.eps), pair[1],
+                                                   out_conv.weight, out_conv.bias)
+
+
 def sinusoidal(t, dim, theta=10000):
     return torch.ops.red_diffeq.sinusoidal_emb(t, dim, float(theta))
 
@@ -134,12 +190,18 @@ def red_q_sample(diff, x0, t, eps):
     return torch.ops.red_diffeq.red_q_sample(x0, t, eps, diff.sqrt_alphas_cumprod, diff.sqrt_one_minus_alphas_cumprod)
 
 
+def red_q_sample_into(diff, x0, t, eps, xt, t_out):
+    """red_q_sample written into xt, with t copied to t_out in the same launch (Unet.graph_io)."""
+    torch.ops.red_diffeq.red_q_sample_into(x0, t, eps, diff.sqrt_alphas_cumprod, diff.sqrt_one_minus_alphas_cumprod,
+                                           xt, t_out)
+
+
 def red_epilogue(diff, xt, t, eps_hat, eps):
     """(eps' - eps) with eps' re-derived from the clipped x0 (diffusion.py:393-419)."""
     return torch.ops.red_diffeq.red_eps(xt, t, eps_hat, eps, diff.sqrt_recip_alphas_cumprod,
                                         diff.sqrt_recipm1_alphas_cumprod)
 
 
-HIP_OPS = {"conv2d", "conv_group_norm_silu", "conv_group_norm_silu_shortcut", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
-           "full_attention", "red_q_sample", "red_epilogue"}
+HIP_OPS = {"head", "first_block_and_scale_shifts", "last_block_and_out", "conv2d", "conv_group_norm_silu", "conv_group_norm_silu_shortcut", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+           "full_attention", "red_q_sample", "red_q_sample_into", "red_epilogue"}
 del math

@@ -15,8 +15,9 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
-    conv2d_mfma, conv2d_rms, conv2d_gn_silu, gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb,
-    linear_attn, linear_attn_block, attn, red_q_sample, red_eps
+    conv2d_mfma, conv2d_rms, conv2d_gn_silu, conv2d_gn_silu_sc, conv2d_gn_silu_lsm, conv2d_gn_silu_out, unet_head,
+    gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb, linear_attn, linear_attn_block, attn,
+    red_q_sample, red_q_sample_into, red_eps
   loop (include/red_diffeq_loop.h)
     l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
 
@@ -448,6 +449,112 @@ def _(x, x2, weight, bias, gamma, beta, scale_shift, groups, eps, weight_s, bias
     return x.new_empty(shape), x.new_empty(shape[0], weight_s.shape[0], shape[2], shape[3])
 
 
+def _ptr_array(ts):
+    return (ctypes.c_void_p * len(ts))(*[_hip.ptr(t) for t in ts])
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_gn_silu_lsm", mutates_args=())
+def conv2d_gn_silu_lsm(x: Tensor, weight: Tensor, bias: Optional[Tensor], pad: int, gamma: Tensor, beta: Tensor,
+                       groups: int, eps: float, post: Optional[Tensor], temb: Tensor, weights: List[Tensor],
+                       biases: List[Tensor], ss_index: int) -> Tuple[Tensor, List[Tensor]]:
+    """(conv2d_gn_silu(x, ..., scale_shift = ys[ss_index], post), ys = linear_silu_multi(temb, weights,
+    biases)): the first ResnetBlock's block1 with every block's Linear(SiLU(t)) computed as a side job of
+    its conv launch (diffusion.py:280-283, 160-165)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    temb = temb.contiguous()
+    d, shape = _conv_desc(x, None, weight, pad, 0)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_gn_ws_bytes(ctypes.byref(d), int(groups)))
+    if nws == 0 or len(weights) > 32:
+        raise ValueError("conv2d_gn_silu_lsm: shape not supported by the fused form")
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    tk = _tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d))))
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    B, fin = temb.shape
+    wl = [w.contiguous() for w in weights]
+    ys = [torch.empty(B, w.shape[0], device=x.device, dtype=torch.float32) for w in wl]
+    O = (ctypes.c_int32 * len(wl))(*[w.shape[0] for w in wl])
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_gn_silu_lsm(ctypes.byref(d), _hip.ptr(x), None, _hip.ptr(weight.contiguous()),
+                                        _hip.ptr(bias), int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta),
+                                        _hip.ptr(pr), _hip.ptr(y), _hip.ptr(ws), nws, tk, fin, _hip.ptr(temb), len(wl),
+                                        _ptr_array(wl), _ptr_array(biases), O, _ptr_array(ys), int(ss_index),
+                                        _hip.stream_of(x)), "rdq_conv2d_gn_silu_lsm")
+    return y, ys
+
+
+@conv2d_gn_silu_lsm.register_fake
+def _(x, weight, bias, pad, gamma, beta, groups, eps, post, temb, weights, biases, ss_index):
+    _, shape = _conv_desc(x, None, weight, pad, 0)
+    return x.new_empty(shape), [temb.new_empty(temb.shape[0], w.shape[0]) for w in weights]
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_gn_silu_out", mutates_args=())
+def conv2d_gn_silu_out(x: Tensor, weight: Tensor, bias: Optional[Tensor], pad: int, gamma: Tensor, beta: Tensor,
+                       scale_shift: Optional[Tensor], groups: int, eps: float, post: Optional[Tensor],
+                       w_out: Tensor, b_out: Optional[Tensor]) -> Tensor:
+    """conv1x1(conv2d_gn_silu(x, ..., post), w_out) + b_out: final_res_block's block2 and final_conv
+    (diffusion.py:299-301), the block output never written (w_out: (nf <= 4, cout, 1, 1))."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    d, shape = _conv_desc(x, None, weight, pad, 0)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_gn_ws_bytes(ctypes.byref(d), int(groups)))
+    if nws == 0:
+        raise ValueError("conv2d_gn_silu_out: shape not supported by the fused form")
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    tk = _tickets(x.device, int(L.rdq_conv2d_tickets(ctypes.byref(d))))
+    nf = int(w_out.shape[0])
+    yf = torch.empty(shape[0], nf, shape[2], shape[3], device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_gn_silu_out(ctypes.byref(d), _hip.ptr(x), None, _hip.ptr(weight.contiguous()),
+                                        _hip.ptr(bias), int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta),
+                                        _hip.ptr(ss), _hip.ptr(pr), nf, _hip.ptr(w_out.contiguous()), _hip.ptr(b_out),
+                                        _hip.ptr(yf), _hip.ptr(ws), nws, tk, _hip.stream_of(x)),
+               "rdq_conv2d_gn_silu_out")
+    return yf
+
+
+@conv2d_gn_silu_out.register_fake
+def _(x, weight, bias, pad, gamma, beta, scale_shift, groups, eps, post, w_out, b_out):
+    _, shape = _conv_desc(x, None, weight, pad, 0)
+    return x.new_empty(shape[0], w_out.shape[0], shape[2], shape[3])
+
+
+def unet_head_fusable(x, weight, time_mlp):
+    """rdq_unet_head applies: init_conv outside the channel-chunk form (7x7 / 3x3, cout <= 64, no K split)."""
+    cout, cin, kh, kw = weight.shape
+    dim, hid = time_mlp[1].weight.shape[1], time_mlp[1].weight.shape[0]
+    return kh == kw and kh in (3, 7) and cout <= 64 and cin * kh * kw <= 224 and x.shape[1] == cin and \
+        (kh == 7 or cin % 8 != 0) and dim + hid <= 7680
+
+
+@torch.library.custom_op(f"{LIB}::unet_head", mutates_args=())
+def unet_head(x: Tensor, weight: Tensor, bias: Optional[Tensor], pad: int, t: Tensor, dim: int, theta: float,
+              w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor) -> Tuple[Tensor, Tensor]:
+    """(init_conv(x), time_mlp(t)) in one launch (diffusion.py:276-279)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    t = t.to(torch.int64).contiguous()
+    d, shape = _conv_desc(x, None, weight, pad, 0)
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    hid, out = w1.shape[0], w2.shape[0]
+    temb = torch.empty(t.shape[0], out, device=x.device, dtype=torch.float32)
+    _hip.check(_hip.lib().rdq_unet_head(ctypes.byref(d), _hip.ptr(x), _hip.ptr(weight.contiguous()), _hip.ptr(bias),
+                                        _hip.ptr(y), dim, float(theta), _hip.ptr(t), _hip.ptr(w1.contiguous()),
+                                        _hip.ptr(b1), hid, _hip.ptr(w2.contiguous()), _hip.ptr(b2), out,
+                                        _hip.ptr(temb), _hip.stream_of(x)), "rdq_unet_head")
+    return y, temb
+
+
+@unet_head.register_fake
+def _(x, weight, bias, pad, t, dim, theta, w1, b1, w2, b2):
+    _, shape = _conv_desc(x, None, weight, pad, 0)
+    return x.new_empty(shape), x.new_empty(t.shape[0], w2.shape[0])
+
+
 @torch.library.custom_op(f"{LIB}::rmsnorm", mutates_args=())
 def rmsnorm(x: Tensor, g: Tensor, residual: Optional[Tensor]) -> Tensor:
     """F.normalize(x, dim=1) * g * sqrt(C) [+ residual]."""
@@ -633,6 +740,25 @@ def red_q_sample(x0: Tensor, t: Tensor, eps: Tensor, sqrt_ac: Tensor, sqrt_1mac:
     return xt
 
 
+@torch.library.custom_op(f"{LIB}::red_q_sample_into", mutates_args=("xt", "t_out"))
+def red_q_sample_into(x0: Tensor, t: Tensor, eps: Tensor, sqrt_ac: Tensor, sqrt_1mac: Tensor, xt: Tensor,
+                      t_out: Tensor) -> None:
+    """red_q_sample written into xt (contiguous, x0's shape), t copied into t_out (int64 [B]) by the same
+    launch: the static inputs of a captured U-Net forward (Unet.graph_io)."""
+    _hip.require_device(x0)
+    x0, eps = x0.contiguous(), eps.contiguous()
+    if xt.shape != x0.shape or not xt.is_contiguous() or t_out.dtype != torch.int64 or t_out.numel() != x0.shape[0]:
+        raise ValueError("red_q_sample_into: xt / t_out do not match x0")
+    _hip.check(_hip.lib().rdq_red_q_sample_t(x0.shape[0], x0[0].numel(), _hip.ptr(sqrt_ac), _hip.ptr(sqrt_1mac),
+                                             _hip.ptr(t.to(torch.int64).contiguous()), _hip.ptr(x0), _hip.ptr(eps),
+                                             _hip.ptr(xt), _hip.ptr(t_out), _hip.stream_of(x0)), "rdq_red_q_sample_t")
+
+
+@red_q_sample_into.register_fake
+def _(x0, t, eps, sqrt_ac, sqrt_1mac, xt, t_out):
+    return None
+
+
 @red_q_sample.register_fake
 def _(x0, t, eps, sqrt_ac, sqrt_1mac):
     return torch.empty_like(x0)
@@ -765,6 +891,7 @@ def _forward_only(op, name):
 
 
 for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"), (conv2d_gn_silu_sc, "conv2d_gn_silu_sc"),
+                   (conv2d_gn_silu_lsm, "conv2d_gn_silu_lsm"), (conv2d_gn_silu_out, "conv2d_gn_silu_out"), (unet_head, "unet_head"),
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
                    (linear_silu_multi, "linear_silu_multi"),

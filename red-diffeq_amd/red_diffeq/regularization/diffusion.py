@@ -51,6 +51,14 @@ class RED_DiffEq:
         with torch.no_grad():
             if getattr(dm, "objective", None) == "pred_noise" and x0.is_cuda and not dm.self_condition:
                 from ..models import unet_ops
+                io = dm.model.graph_io(x0.shape, x0.device) if t.dtype == torch.int64 and \
+                    hasattr(dm.model, "graph_io") else None
+                if io is not None:
+                    # x_t and t written straight into the captured forward's static inputs
+                    xs, ts = io
+                    unet_ops.red_q_sample_into(dm, x0, t, noise, xs, ts)
+                    eps_hat = dm.model.replay_static(xs, ts)
+                    return unet_ops.red_epilogue(dm, xs, t, eps_hat, noise)
                 x_t = unet_ops.red_q_sample(dm, x0, t, noise)
                 eps_hat = dm.model(x_t, t, None)
                 return unet_ops.red_epilogue(dm, x_t, t, eps_hat, noise)

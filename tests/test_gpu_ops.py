@@ -88,6 +88,13 @@ def test_unet_and_loop_ops_opcheck(cuda):
     opcheck(ops.sinusoidal_emb, (torch.tensor([3, 900], device=cuda), 16, 10000.0))
     opcheck(ops.time_mlp, (torch.tensor([3, 900], device=cuda), 16, 10000.0, r(64, 16), r(64), r(64, 64), r(64)))
     opcheck(ops.linear_silu_multi, (r(2, 64), [r(32, 64), r(128, 64)], [r(32), r(128)]))
+    tt = torch.tensor([3, 900], device=cuda)
+    opcheck(ops.unet_head, (r(2, 1, 12, 10), r(64, 1, 7, 7), r(64), 3, tt, 16, 10000.0, r(64, 16), r(64), r(64, 64),
+                            r(64)))
+    opcheck(ops.conv2d_gn_silu_lsm, (xs, r(64, 64, 3, 3) * 0.1, r(64), 1, r(64), r(64), 8, 1e-5, xs, r(2, 64),
+                                     [r(128, 64), r(40, 64)], [r(128), r(40)], 0))
+    opcheck(ops.conv2d_gn_silu_out, (xs, r(64, 64, 3, 3) * 0.1, r(64), 1, r(64), r(64), r(2, 128), 8, 1e-5, xs2,
+                                     r(3, 64, 1, 1), r(3)))
     opcheck(ops.linear_attn, (r(2, 3 * 4 * 8, 6, 6), r(2, 4, 8, 4), 4, 8 ** -0.5))
     qkv, mkv = r(2, 3 * 4 * 32, 6, 6), r(2, 4, 32, 4)
     opcheck(ops.linear_attn_block, (qkv, mkv, 4, 32 ** -0.5, r(64, 128, 1, 1) * 0.1, r(64), r(1, 64, 1, 1),
@@ -98,6 +105,11 @@ def test_unet_and_loop_ops_opcheck(cuda):
     t = torch.tensor([5, 700], device=cuda)
     opcheck(ops.red_q_sample, (r(2, 1, 8, 8), t, r(2, 1, 8, 8), sa, s1))
     opcheck(ops.red_eps, (r(2, 1, 8, 8), t, r(2, 1, 8, 8), r(2, 1, 8, 8), sa, s1))
+    xt, tq = torch.empty(2, 1, 8, 8, device=cuda), torch.zeros(2, dtype=torch.int64, device=cuda)
+    x0q, eq = r(2, 1, 8, 8), r(2, 1, 8, 8)
+    opcheck(ops.red_q_sample_into, (x0q, t, eq, sa, s1, xt, tq))
+    ops.red_q_sample_into(x0q, t, eq, sa, s1, xt, tq)
+    assert torch.equal(xt, ops.red_q_sample(x0q, t, eq, sa, s1)) and torch.equal(tq, t)
     pred, y = r(2, 3, 20, 7), r(2, 3, 20, 7)
     mask = (torch.rand(2, 3, 20, 7, generator=g) > 0.3).float().to(cuda)
     opcheck(ops.l1_misfit, (pred, y, mask))
@@ -119,7 +131,7 @@ def test_unet_dispatches_through_ops(cuda):
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
         y = net(x, t)                 # grad enabled: the eager path (no hipGraph replay)
     names = {e.name for e in prof.events()}
-    for op in ("conv2d_mfma", "conv2d_gn_silu", "gn_silu", "rmsnorm", "time_mlp", "linear_silu_multi", "linear_attn",
+    for op in ("unet_head", "conv2d_mfma", "conv2d_gn_silu", "gn_silu", "rmsnorm", "linear_silu_multi", "linear_attn",
                "attn"):
         assert f"red_diffeq::{op}" in names, op
     with pytest.raises(RuntimeError, match="no backward"):
@@ -127,3 +139,61 @@ def test_unet_dispatches_through_ops(cuda):
     with torch.no_grad():
         assert torch.equal(net(x, t), y.detach())      # graph replay == eager
     assert np.isfinite(y.detach().cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_unet_fused_edges_match_separate_launches(cuda, B):
+    """The U-Net's fused first / last launches (unet_head: init_conv + time MLP; the first block's conv
+    with every block's Linear(SiLU(t)); final_res_block's last pass + final_conv) against the
+    separate-launch sequence: head and time projections bit for bit, the output within fp32 rounding
+    of the 1x1 conv's summation order."""
+    from red_diffeq.models import unet_ops
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(0)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    x = torch.randn(B, 1, 72, 72, device=cuda)
+    t = torch.randint(0, 1000, (B,), device=cuda)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        y = net(x, t).detach()
+    names = {e.name for e in prof.events()}
+    for op in ("unet_head", "conv2d_gn_silu_out") + (("conv2d_gn_silu_lsm",) if B <= 2 else ()):
+        assert f"red_diffeq::{op}" in names, op
+    x0, te = torch.ops.red_diffeq.unet_head(x, net.init_conv.weight, net.init_conv.bias, 3, t, 64, 10000.0,
+                                            net.time_mlp[1].weight, net.time_mlp[1].bias, net.time_mlp[3].weight,
+                                            net.time_mlp[3].bias)
+    assert torch.equal(x0, unet_ops.conv2d(x, net.init_conv))
+    assert torch.equal(te, unet_ops.time_mlp(t, net.time_mlp))
+    blocks = net._resnet_blocks()
+    h, ss = unet_ops.first_block_and_scale_shifts(x0[:2], blocks[0], te[:2], blocks)
+    x0, te = x0[:2], te[:2]
+    for a, b in zip(ss, unet_ops.resnet_scale_shifts(te, blocks)):
+        assert torch.equal(a, b)
+    assert torch.equal(h, blocks[0](x0, te, scale_shift=ss[0]))
+    unet_ops.FUSED_EDGES = False
+    try:
+        with torch.no_grad():
+            ysep = net._forward(x, t, None)
+    finally:
+        unet_ops.FUSED_EDGES = True
+    err = (y - ysep).abs().max().item() / ysep.abs().max().item()
+    assert err < 2e-6, err
+    with torch.no_grad():
+        assert torch.equal(net(x, t), y)          # graph replay == eager
+
+
+def test_unet_static_graph_io(cuda):
+    """graph_io / replay_static (the RED regulariser's path: x_t and t written into the captured
+    forward's static inputs, output read in place) == forward()."""
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(0)
+    net = Unet(dim=16, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    x = torch.randn(2, 1, 72, 72, device=cuda)
+    t = torch.tensor([7, 901], device=cuda)
+    with torch.no_grad():
+        y = net(x, t)
+        xs, ts = net.graph_io(x.shape, x.device)
+        xs.copy_(x)
+        ts.copy_(t)
+        assert torch.equal(net.replay_static(xs, ts), y)
+        assert net.graph_io(x.shape, x.device)[0] is xs            # one graph per shape
+    assert net.graph_io(x.shape, x.device) is None                   # grad enabled: eager, no graph

@@ -13,14 +13,24 @@ torch.manual_seed(0)
 net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).cuda().eval()
 x = torch.randn(B, 1, 72, 72, device="cuda")
 t = torch.randint(0, 1000, (B,), device="cuda")
-with torch.no_grad():
+def timed(f):
     for _ in range(3):
-        net(x, t)
+        f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        net(x, t)
+        f()
     e1.record()
     torch.cuda.synchronize()
-print(f"B={B}: {e0.elapsed_time(e1) / reps:.3f} ms per forward", flush=True)
+    return e0.elapsed_time(e1) / reps
+
+
+with torch.no_grad():
+    ms_call = timed(lambda: net(x, t))
+    xs, ts = net.graph_io(x.shape, x.device)
+    xs.copy_(x)
+    ts.copy_(t)
+    ms = timed(lambda: net.replay_static(xs, ts))
+print(f"B={B}: {ms:.3f} ms per forward (static graph I/O, the RED loop's path); module call {ms_call:.3f} ms",
+      flush=True)
