@@ -43,12 +43,6 @@ typedef struct rdq_conv_desc {
  * launch.  Both sum the slabs in slab order (deterministic, identical results). */
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d);
 size_t rdq_conv2d_tickets(const rdq_conv_desc *d);
-/* Workgroup count of the stream-K form the channel-chunk conv takes for this shape on the current
- * device (given tickets and rdq_conv2d_ws_bytes of ws), 0 if it uses the tile grid: grids of one to
- * eight rounds of two workgroups per CU whose last round would be <= 80 % full get exactly one round,
- * each workgroup an equal range of (tile, K stage) units; tiles cut by a range boundary are combined
- * in the launch in a fixed piece order (deterministic).  RDQ_NO_STREAMK=1 disables it. */
-int rdq_conv2d_streamk(const rdq_conv_desc *d);
 int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
                const float *residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets, hipStream_t stream);
 

@@ -622,37 +622,6 @@ __global__ __launch_bounds__(256, 2) void k_conv_cc(CcArgs a)
     conv_cc_tile<TAPS, MODE, RMS>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sm);
 }
 
-// Stream-K form of k_conv_cc for grids of a few rounds of workgroups (B = 8 at 72 x 72: 1296 tiles on
-// 512 workgroup slots = 2.53 rounds, the last one half empty).  The gx * gy * nstages (tile, K stage)
-// units are dealt in equal contiguous ranges to exactly gridDim.x workgroups (one round); a range
-// covers the tail of one tile, whole tiles and the head of another.  A tile cut by range boundaries
-// is computed in pieces whose slabs the last-arriving piece sums in piece order (conv_cc_seg's
-// in-launch combine), so the result is deterministic for a given grid.  Needs U >= gridDim.x
-// (strictly increasing boundaries: every piece is non-empty) — the host checks.
-__device__ __forceinline__ int sk_cnt(int64_t x, int64_t U, int64_t P)   // range starts <= unit x
-{
-    return (int)min(P, ((x + 1) * P + U - 1) / U);
-}
-template <int TAPS, int MODE>
-__global__ __launch_bounds__(256, 2) void k_conv_cc_sk(CcArgs a, int gx, int gy)
-{
-    __shared__ __attribute__((aligned(16))) float sm[CC_SMEM];
-    const int nst = a.nstages;
-    const int64_t U = (int64_t)gx * gy * nst, P = gridDim.x;
-    int64_t u = (int64_t)blockIdx.x * U / P;
-    const int64_t u1 = ((int64_t)blockIdx.x + 1) * U / P;
-    while (u < u1) {
-        const int T = (int)(u / nst);
-        const int64_t t0 = (int64_t)T * nst;
-        const int s0 = (int)(u - t0), s1 = (int)min<int64_t>(nst, s0 + (u1 - u));
-        const int c0 = sk_cnt(t0, U, P);
-        const int pieces = 1 + sk_cnt(t0 + nst - 1, U, P) - c0, piece = sk_cnt(u, U, P) - c0;
-        conv_cc_seg<TAPS, MODE, false>(a, T % gx, T / gx, s0, s1, pieces, piece, gx, gy, sm);
-        __syncthreads();                          // the staging image is reused by the next piece
-        u = t0 + s1;
-    }
-}
-
 // A ResnetBlock with a 1x1 shortcut (the U-Net's up path and final block, diffusion.py:160-168):
 // block1's 3x3 conv (GroupNorm statistics in its epilogue) and res_conv of the same concatenated
 // input in ONE launch: n tiles [0, gy_a) run the 3x3 tile, the rest the 1x1 tile (each with its own
@@ -711,36 +680,6 @@ int cc_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
     const int per = (nstages + S - 1) / S;
     *per_split = per;
     return (nstages + per - 1) / per;
-}
-
-// Stream-K plan of a channel-chunk conv (k_conv_cc_sk): the workgroup count P (two per CU, one round)
-// when the tile grid takes more than one round and its last round would be at most 80 % full, else 0;
-// *maxp = the most pieces any tile is cut into (slab slots per tile).
-static int cu_count()
-{
-    static int cus[16] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
-int cc_streamk(const rdq_conv_desc *d, int *maxp)
-{
-    *maxp = 1;
-    if (getenv("RDQ_NO_STREAMK")) return 0;
-    const int64_t M = (int64_t)d->B * d->H * d->W;
-    const int64_t tiles = ((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN);
-    const int nst = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
-    const int64_t P = 2 * (int64_t)cu_count();
-    if (P <= 0 || tiles <= P || tiles >= 8 * P || tiles % P == 0 || (tiles % P) * 5 > P * 4) return 0;
-    const int64_t U = tiles * nst, per = U / P;              // every range >= per units
-    if (per < std::max(3, nst / 2)) return 0;
-    *maxp = (int)(1 + (nst - 1 + per - 1) / per);            // interior range starts in one tile
-    return (int)P;
 }
 
 // split count: about one workgroup per CU over the tile grid, >= 4 K stages per split, and the
@@ -2358,29 +2297,6 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 }
 }  // namespace
 
-// k_conv_cc_sk in place of k_conv_cc when cc_streamk plans it, tickets are given and ws holds the
-// pieces' slabs; false: not taken (the caller launches k_conv_cc)
-static bool launch_streamk(const CcArgs &c0, const rdq_conv_desc *d, size_t ws_bytes, int gx, int gy, hipStream_t st)
-{
-    int maxp = 1;
-    const int P = cc_streamk(d, &maxp);
-    if (!P || !c0.tickets || !c0.part || (size_t)maxp * gx * gy * CC_BM * CC_BN * sizeof(float) > ws_bytes ||
-        d->in_mode == RDQ_IN_UNSHUFFLE2)
-        return false;
-    CcArgs c = c0;
-    c.S = 1;
-    c.per_split = c.nstages;
-    if (d->kh == 3) {
-        if (d->in_mode == RDQ_IN_UPSAMPLE2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<9, RDQ_IN_UPSAMPLE2>), dim3(P), dim3(256), 0, st, c, gx, gy);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<9, RDQ_IN_PLAIN>), dim3(P), dim3(256), 0, st, c, gx, gy);
-    } else {
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_sk<1, RDQ_IN_PLAIN>), dim3(P), dim3(256), 0, st, c, gx, gy);
-    }
-    return true;
-}
-
 extern "C" {
 
 size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
@@ -2390,19 +2306,12 @@ size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
     return (size_t)(((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN));
 }
 
-int rdq_conv2d_streamk(const rdq_conv_desc *d)
-{
-    int maxp = 1;
-    return d && cc_ok(d) && d->in_mode != RDQ_IN_UNSHUFFLE2 ? cc_streamk(d, &maxp) : 0;
-}
-
 size_t rdq_conv2d_ws_bytes(const rdq_conv_desc *d)
 {
     if (!d || d->B < 1 || d->H < 1 || d->W < 1 || d->cout < 1 || d->kh < 1 || d->kw < 1 || d->cin1 < 1) return 0;
     int per = 0;
     if (cc_ok(d)) {
-        int maxp = 1;
-        const int S = std::max(cc_splits(d, (size_t)-1 / 2, &per), cc_streamk(d, &maxp) ? maxp : 1);
+        const int S = cc_splits(d, (size_t)-1 / 2, &per);
         return S > 1 ? (size_t)S * rdq_conv2d_tickets(d) * CC_BM * CC_BN * sizeof(float) : 0;
     }
     const int S = ig_splits(d, (size_t)-1 / 2, &per);
@@ -2433,10 +2342,6 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         const bool fold = c.S > 1 && tickets;        // combine in the conv launch
         if (c.S > 1 && !tickets) c.tickets = nullptr;
         const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-        if (launch_streamk(c, d, ws_bytes, grid.x, grid.y, st)) {
-            RDQ_CHECK(hipGetLastError());
-            return 0;
-        }
         CcArgs cl = c;
         if (c.S > 1 && !fold) cl.S = -c.S;            // slabs only; k_conv_reduce combines
         if (d->kh == 3) {
@@ -2529,8 +2434,7 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     float *h = c.y;
     double *gnp = c.gnp;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-    if (launch_streamk(c, d, rdq_conv2d_ws_bytes(d), grid.x, grid.y, st)) {
-    } else if (d->kh == 3) {
+    if (d->kh == 3) {
         if (d->in_mode == RDQ_IN_UPSAMPLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
         else
@@ -2666,8 +2570,7 @@ int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *
         !gn_conv_args(c, d, x, x2, w, bias, G, ws, ws_bytes, tickets))
         return RDQ_E_INVALID;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-    if (launch_streamk(c, d, rdq_conv2d_ws_bytes(d), grid.x, grid.y, st)) {
-    } else if (d->kh == 3) {
+    if (d->kh == 3) {
         if (d->in_mode == RDQ_IN_UPSAMPLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
         else

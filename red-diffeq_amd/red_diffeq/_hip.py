@@ -72,7 +72,6 @@ SIGNATURES = {
     # include/red_diffeq_unet.h
     "rdq_conv2d_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_tickets": (c_size_t, [ctypes.POINTER(ConvDesc)]),
-    "rdq_conv2d_streamk": (c_int32, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p, c_void_p]),
     "rdq_conv2d_rms": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -91,42 +91,12 @@ def test_conv_channel_chunk_tickets(cuda, cin1, cin2, cout, k, H, B, mode):
     assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0     # tickets returned to zero
 
 
-# stream-K form (grids of a few rounds: B = 8 / 16 at the U-Net's large levels): every shape here takes
-# it (rdq_conv2d_streamk), matches torch, is deterministic, returns its tickets, and stays within fp32
-# rounding of the tile-grid form (RDQ_NO_STREAMK)
-@pytest.mark.parametrize("cin1,cin2,cout,k,H,B,mode", [
-    (64, 0, 64, 3, 72, 8, 0), (64, 64, 64, 3, 72, 8, 0), (128, 0, 128, 3, 36, 8, 0), (128, 0, 64, 3, 72, 8, 1),
-    (64, 0, 384, 1, 72, 3, 0), (256, 0, 256, 3, 18, 16, 0)])
-def test_conv_streamk(cuda, cin1, cin2, cout, k, H, B, mode, monkeypatch):
-    import ctypes
-    from red_diffeq import _hip, ops as O
-    torch.manual_seed(4)
-    conv = nn.Conv2d(cin1 + cin2, cout, k, padding=k // 2).to(cuda)
-    conv.weight.data *= 0.5
-    xs = H // 2 if mode == 1 else H
-    x = torch.randn(B, cin1, xs, xs, device=cuda)
-    x2 = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
-    res = torch.randn(B, cout, H, H, device=cuda)
-    d, _ = O._conv_desc(x, x2, conv.weight, k // 2, mode)
-    assert _hip.lib().rdq_conv2d_streamk(ctypes.byref(d)) > 0
-    a = _conv_abi(x, x2, conv, mode, res, True)
-    assert torch.equal(a, _conv_abi(x, x2, conv, mode, res, True))          # deterministic
-    assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
-    xin = R.upsample_nearest2(x) if mode == 1 else x
-    if x2 is not None:
-        xin = torch.cat((xin, x2), 1)
-    close(a, R.conv2d(xin, conv) + res)
-    monkeypatch.setenv("RDQ_NO_STREAMK", "1")
-    assert _hip.lib().rdq_conv2d_streamk(ctypes.byref(d)) == 0
-    close(a, _conv_abi(x, x2, conv, mode, res, True), rel=2e-6)
-
-
 # Block.forward as two launches (GroupNorm statistics in the conv epilogue, rdq_conv2d_gn_silu) vs
 # conv -> F.group_norm -> scale/shift -> SiLU (+ identity shortcut) in torch fp32
 @pytest.mark.parametrize("cin1,cin2,cout,H,B,ss,post", [
     (64, 0, 64, 72, 1, True, True), (128, 64, 64, 36, 1, True, False), (512, 256, 512, 9, 1, True, False),
     (256, 0, 256, 18, 2, False, True), (64, 0, 128, 9, 3, True, True), (128, 0, 256, 10, 2, True, False),
-    (64, 0, 64, 72, 8, True, True), (64, 64, 64, 72, 8, True, False)])          # B = 8: stream-K conv
+    (64, 0, 64, 72, 8, True, True), (64, 64, 64, 72, 8, True, False)])
 def test_conv_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post):
     from red_diffeq import ops as O
     from red_diffeq.models import unet_ops as ops
