@@ -122,6 +122,24 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
+/* Block.forward in two launches on the bf16 halo-staged conv (the batched, mixed-precision U-Net of
+ * configs[4]): y = SiLU(GroupNorm_G(conv3x3_bf16(input) + bias) * (scale+1) + shift) [+ post_residual],
+ * the GroupNorm statistics reduced in the conv's epilogue (fp64, fixed trees) instead of a separate
+ * statistics pass over the conv output.  rdq_conv2d_bf16_gn_ws_bytes returns 0 where this form does not
+ * apply (not the halo-staged conv: see rdq_conv2d_bf16; H*W < 256; C/G outside {8,16,32,64}).
+ * wp: rdq_conv2d_bf16_pack's weights; ws: the conv output + the partial statistics. */
+size_t rdq_conv2d_bf16_gn_ws_bytes(const rdq_conv_desc *d, int32_t G);
+int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                            int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                            const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
+
+/* rdq_conv2d_gn_silu_out's tail (final_res_block's block2 + final_conv, diffusion.py:299-301) on the bf16
+ * halo-staged conv: yf = conv1x1(Block_bf16(x) [+ post_residual], wf) + bf; ws: rdq_conv2d_bf16_gn_ws_bytes. */
+int rdq_conv2d_bf16_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp,
+                                const float *bias, int32_t G, float eps, const float *gamma, const float *beta,
+                                const float *scale_shift, const float *post_residual, int32_t nf, const float *wf,
+                                const float *bf, float *yf, void *ws, size_t ws_bytes, hipStream_t stream);
+
 /* GroupNorm(G) -> [x*(scale+1)+shift] -> SiLU  (Block.forward, diffusion.py:142-149).
  * scale_shift: nullable [B][2C] (first C = scale, next C = shift); ws: rdq_group_norm_ws_bytes (fp64
  * chunk partials of sum / sum of squares, then the per-(sample, group) mean and 1/std). */

@@ -806,7 +806,8 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
 __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const float *__restrict__ x,
                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
                                                     const float *__restrict__ ss, const double *__restrict__ gnp,
-                                                    float eps, const float *__restrict__ post, float *__restrict__ y)
+                                                    float eps, const float *__restrict__ post, float *__restrict__ y,
+                                                    int bm = CC_BM)
 {
     const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
     const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
@@ -827,10 +828,10 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     __shared__ float st2[2];
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const int mlo = (int)(((int64_t)b * HW) / CC_BM), mhi = (int)(((int64_t)(b + 1) * HW - 1) / CC_BM);
+        const int mlo = (int)(((int64_t)b * HW) / bm), mhi = (int)(((int64_t)(b + 1) * HW - 1) / bm);
         double s = 0.0, q = 0.0;
         for (int mt = mlo + lane; mt <= mhi; mt += 64) {
-            const int slot = (int)(((int64_t)mt * CC_BM) / HW) == b ? 0 : 1;
+            const int slot = (int)(((int64_t)mt * bm) / HW) == b ? 0 : 1;
             const double *p = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
             s += p[0];
             q += p[1];
@@ -882,7 +883,8 @@ __global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int 
                                                              const double *__restrict__ gnp, float eps,
                                                              const float *__restrict__ post, int NF,
                                                              const float *__restrict__ wf,
-                                                             const float *__restrict__ bf, float *__restrict__ yf)
+                                                             const float *__restrict__ bf, float *__restrict__ yf,
+                                                             int bm = CC_BM)
 {
     __shared__ float st[64][2];
     __shared__ float part[GO_NW][GO_MAXF][64];
@@ -902,10 +904,10 @@ __global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int 
     }
     // (sample, group) statistics: wave w reduces groups w, w + GO_NW, ... exactly as k_gn_apply_t's wave 0
     for (int g = wv; g < G; g += GO_NW) {
-        const int mlo = (int)(((int64_t)b * HW) / CC_BM), mhi = (int)(((int64_t)(b + 1) * HW - 1) / CC_BM);
+        const int mlo = (int)(((int64_t)b * HW) / bm), mhi = (int)(((int64_t)(b + 1) * HW - 1) / bm);
         double s = 0.0, q = 0.0;
         for (int mt = mlo + lane; mt <= mhi; mt += 64) {
-            const int slot = (int)(((int64_t)mt * CC_BM) / HW) == b ? 0 : 1;
+            const int slot = (int)(((int64_t)mt * bm) / HW) == b ? 0 : 1;
             const double *pp = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
             s += pp[0];
             q += pp[1];
@@ -1160,6 +1162,53 @@ __global__ __launch_bounds__(256) void k_time_mlp(TmArgs m)
     time_mlp_rows(m, blockIdx.x, blockIdx.y, tm_sm);
 }
 
+// Large batches (the configs[4] tile batch, hundreds of samples): the time MLP for TMB samples per
+// workgroup, so the hidden layer's weights are read once per sample block instead of once per
+// (row block, sample); per sample the arithmetic is time_mlp_rows' (bit for bit k_time_mlp's).
+constexpr int TMB = 8;
+__global__ __launch_bounds__(256) void k_time_mlp_b(TmArgs m, int B)
+{
+    extern __shared__ float tmb_sm[];                 // [TMB][dim + hid]
+    const int dim = m.dim, hid = m.hid, out = m.out, ld = dim + hid;
+    const int b0 = blockIdx.y * TMB, nb = min(TMB, B - b0);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, half = dim / 2;
+    for (int idx = tid; idx < nb * half; idx += 256) {
+        const int bb = idx / half, i = idx - bb * half;
+        const float f = expf((float)i * m.neg_emb);
+        const float arg = (float)m.t[b0 + bb] * f;
+        tmb_sm[bb * ld + i] = sinf(arg);
+        tmb_sm[bb * ld + half + i] = cosf(arg);
+    }
+    __syncthreads();
+    for (int o = tid; o < hid; o += 256) {
+        const float *wr = m.w1 + (size_t)o * dim;
+        for (int bb = 0; bb < nb; ++bb) {
+            const float *e = tmb_sm + bb * ld;
+            float s = 0.0f;
+            if ((dim & 3) == 0) {
+                for (int i = 0; i < dim; i += 4) {
+                    const float4 w4 = *reinterpret_cast<const float4 *>(wr + i);
+                    s += w4.x * e[i];
+                    s += w4.y * e[i + 1];
+                    s += w4.z * e[i + 2];
+                    s += w4.w * e[i + 3];
+                }
+            } else {
+                for (int i = 0; i < dim; ++i) s += wr[i] * e[i];
+            }
+            const float v = s + m.b1[o];
+            tmb_sm[bb * ld + dim + o] = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+        }
+    }
+    __syncthreads();
+    const int o = blockIdx.x * TM_ROWS + wv;
+    if (o >= out) return;
+    for (int bb = 0; bb < nb; ++bb) {
+        const float s = wave_dot(m.w2 + (size_t)o * hid, tmb_sm + bb * ld + dim, hid, lane, false);
+        if (lane == 0) m.y[(size_t)(b0 + bb) * out + o] = s + m.b2[o];
+    }
+}
+
 // every ResnetBlock's time MLP, Linear(SiLU(t)) (diffusion.py:157-165), in one launch: up to
 // LM_MAX linears sharing the input, one wave per output row
 constexpr int LM_MAX = 32;
@@ -1221,6 +1270,55 @@ __device__ __forceinline__ void lsm_rows(int in, const float *__restrict__ x, co
         float v = s[r];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
         if (lane == 0 && yo[r]) *yo[r] = v + bo[r];
+    }
+}
+
+// Large batches: SiLU(x) of LSB samples formed once per workgroup into LDS, then each wave runs
+// wave_dot's arithmetic (bit for bit k_linear_silu_multi's) for LSR rows x the LSB samples, its row's
+// weights re-read from the cache instead of once per sample from the whole weight set.
+constexpr int LSB = 32, LSR = 16;
+__global__ __launch_bounds__(256) void k_linear_silu_multi_b(int in, int B, const float *__restrict__ x, LinMulti L)
+{
+    extern __shared__ float lsb_sm[];                 // [LSB][in], SiLU'd
+    const int b0 = blockIdx.y * LSB, nb = min(LSB, B - b0);
+    for (int idx = threadIdx.x; idx < nb * in; idx += 256) {
+        float v = x[(size_t)b0 * in + idx];
+        lsb_sm[idx] = v / (1.0f + expf(-v));
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gend = L.start[L.n];
+    for (int rr = 0; rr < LSR; ++rr) {
+        const int go = (blockIdx.x * 4 + wv) * LSR + rr;
+        if (go >= gend) return;
+        int j = 0;
+        while (go >= L.start[j + 1]) ++j;
+        const int o = go - L.start[j];
+        const float *w = L.w[j] + (size_t)o * in;
+        const float bo = L.b[j] ? L.b[j][o] : 0.0f;
+        float wv4[4];                                 // in <= 256 (host check): one chunk, loaded once
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wv4[u] = w[min(lane + 64 * u, in - 1)];
+        // four samples at a time: independent chains, their reductions interleaved
+        for (int bb0 = 0; bb0 < nb; bb0 += 4) {
+            float s[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float *xs = lsb_sm + min(bb0 + q, nb - 1) * in;
+                s[q] = 0.0f;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = lane + 64 * u;
+                    if (i < in) s[q] += wv4[u] * xs[i];
+                }
+            }
+            for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) s[q] += __shfl_down(s[q], off, 64);
+            if (lane == 0)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (bb0 + q < nb) L.y[j][(size_t)(b0 + bb0 + q) * L.out[j] + o] = s[q] + bo;
+        }
     }
 }
 
@@ -2048,7 +2146,8 @@ struct C3Args {
     const float *x, *x2, *bias, *res;
     const __bf16 *w;                 // [cout][9][cinp]
     float *y;
-    int cinp, K, M, HW, R, cch, plane;
+    double *gnp;                     // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
+    int cinp, K, M, HW, R, cch, plane, G;
 };
 
 template <int MODE>
@@ -2243,6 +2342,70 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
                 const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
             }
+    }
+    if (!a.gnp) return;
+    // GroupNorm statistics of the tile's outputs (for k_gn_apply_t with bm = C3_BM; HW >= C3_BM so a
+    // tile spans at most two samples): fp64 sum and sum of squares per 8-channel block e = c*4 + (r >> 2)
+    // (a lane's 4 channels r & 3; the other half-wave holds the block's other 4) and sample slot.  Each
+    // thread's partials go through the halo buffer (free after the last chunk's barrier), four blocks
+    // at a time, and 16 threads per (block, slot, sum) add 16 of them each in thread order, then a
+    // fixed xor tree: deterministic, no long shuffle chains of fp64 per lane.
+    __shared__ double c3g[8][2][2];                     // [8-channel block][slot][s, q]
+    double *red = reinterpret_cast<double *>(&Hs[0][0][0]);   // [16][256] per round (32 KiB)
+    const int b0 = m0 / a.HW;
+    int sl[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int m = m0 + pl[mb];
+        sl[mb] = m < a.M ? m / a.HW - b0 : -1;
+    }
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+#pragma unroll
+        for (int el = 0; el < 4; ++el) {
+            const int e = rd * 4 + el;
+            double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                double s1 = 0.0, q1 = 0.0;
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const double xv = acc[e >> 2][mb][(e & 3) * 4 + r4];
+                    s1 += xv;
+                    q1 += xv * xv;
+                }
+                gs[0] += sl[mb] == 0 ? s1 : 0.0;
+                gq[0] += sl[mb] == 0 ? q1 : 0.0;
+                gs[1] += sl[mb] == 1 ? s1 : 0.0;
+                gq[1] += sl[mb] == 1 ? q1 : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                red[((el * 2 + k) * 2 + 0) * 256 + tid] = gs[k];
+                red[((el * 2 + k) * 2 + 1) * 256 + tid] = gq[k];
+            }
+        }
+        __syncthreads();
+        const int combo = tid >> 4, part = tid & 15;
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v += red[combo * 256 + part + 16 * j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (part == 0) c3g[rd * 4 + (combo >> 2)][(combo >> 1) & 1][combo & 1] = v;
+        __syncthreads();
+    }
+    const int cpg = d.cout / a.G, gt = C3_BN / cpg, epg = cpg / 8;
+    if (tid < 2 * gt) {
+        const int g = tid >> 1, k = tid & 1;
+        double s = 0.0, q = 0.0;
+        for (int e = g * epg; e < (g + 1) * epg; ++e) {
+            s += c3g[e][k][0];
+            q += c3g[e][k][1];
+        }
+        double *o = a.gnp + (((size_t)blockIdx.x * a.G + n0 / cpg + g) * 2 + k) * 2;
+        o[0] = s;
+        o[1] = q;
     }
 }
 
@@ -2715,6 +2878,75 @@ int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, con
     return 0;
 }
 
+size_t rdq_conv2d_bf16_gn_ws_bytes(const rdq_conv_desc *d, int32_t G)
+{
+    if (!d || !conv_desc_ok(d) || !conv3_ok(d) || G < 1 || d->cout % G || d->H * d->W < C3_BM) return 0;
+    const int cpg = d->cout / G;
+    if (cpg < 8 || cpg > C3_BN || C3_BN % cpg) return 0;
+    const size_t M = (size_t)d->B * d->H * d->W, mt = (M + C3_BM - 1) / C3_BM;
+    return M * d->cout * sizeof(float) + mt * G * 4 * sizeof(double);
+}
+
+int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                            int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                            const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t st);
+
+// conv3x3_bf16 + GroupNorm statistics in its epilogue (as rdq_conv2d_bf16_gn_silu), conv output in ws
+static bool bf16_gn_conv(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                         int32_t G, void *ws, size_t ws_bytes, C3Args &c, hipStream_t st)
+{
+    const size_t need = rdq_conv2d_bf16_gn_ws_bytes(d, G);
+    if (!need || !x || !wp || !ws || ws_bytes < need || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        return false;
+    const size_t M = (size_t)d->B * d->H * d->W;
+    float *h = static_cast<float *>(ws);
+    c = C3Args{};
+    c.d = *d; c.x = x; c.x2 = x2; c.w = static_cast<const __bf16 *>(wp); c.bias = bias; c.res = nullptr; c.y = h;
+    c.gnp = reinterpret_cast<double *>(h + M * d->cout);
+    c.G = G;
+    c.cinp = bf_cinp(d);
+    c.K = 9 * c.cinp;
+    c.HW = d->H * d->W;
+    c.M = (int)M;
+    c.R = C3_BM + 2 * d->W + 2;
+    c.cch = c.cinp / BF_BK;
+    c.plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? c.HW / 4 : c.HW;
+    const dim3 grid((c.M + C3_BM - 1) / C3_BM, d->cout / C3_BN);
+    if (d->in_mode == RDQ_IN_UPSAMPLE2)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
+    return true;
+}
+
+int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
+                            int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
+                            const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    C3Args c;
+    if (!y || !gamma || !beta || !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st)) return RDQ_E_INVALID;
+    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
+    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, c.y, gamma, beta,
+                       scale_shift, c.gnp, eps, post_residual, y, C3_BM);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_conv2d_bf16_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp,
+                                const float *bias, int32_t G, float eps, const float *gamma, const float *beta,
+                                const float *scale_shift, const float *post_residual, int32_t nf, const float *wf,
+                                const float *bf, float *yf, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    C3Args c;
+    if (!yf || !wf || !gamma || !beta || nf < 1 || nf > GO_MAXF || G > 64 ||
+        !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st))
+        return RDQ_E_INVALID;
+    hipLaunchKernelGGL(k_gn_apply_out, dim3((c.HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, c.HW, G, c.y,
+                       gamma, beta, scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf, C3_BM);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
 size_t rdq_group_norm_ws_bytes(int32_t B, int32_t C, int32_t HW, int32_t G)
 {
     if (B < 1 || C < 1 || HW < 1 || G < 1) return 0;
@@ -2777,13 +3009,18 @@ int rdq_sinusoidal_emb(int32_t B, int32_t dim, float theta, const int64_t *t, fl
 int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid,
                  const float *w2, const float *b2, int32_t out, float *y, hipStream_t st)
 {
-    if (B < 1 || dim < 4 || dim % 2 || hid < 1 || out < 1 || (size_t)(dim + hid) * 4 > 64 * 1024 ||
+    if (B < 1 || dim < 4 || dim % 2 || hid < 1 || out < 1 || (size_t)(dim + hid) * 4 * TMB > 64 * 1024 ||
         !t || !w1 || !b1 || !w2 || !b2 || !y)
         return RDQ_E_INVALID;
     const int half = dim / 2;
     const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
     const TmArgs m{dim, hid, out, -emb, t, w1, b1, w2, b2, y};
-    hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float), st, m);
+    if (B > 2 * TMB)
+        hipLaunchKernelGGL(k_time_mlp_b, dim3((out + TM_ROWS - 1) / TM_ROWS, (B + TMB - 1) / TMB), dim3(256),
+                           TMB * (dim + hid) * sizeof(float), st, m, B);
+    else
+        hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float),
+                           st, m);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -2803,7 +3040,11 @@ int rdq_linear_silu_multi(int32_t B, int32_t in, const float *x, int32_t n, cons
         L.out[j] = out[j];
         L.start[j + 1] = L.start[j] + out[j];
     }
-    hipLaunchKernelGGL(k_linear_silu_multi, dim3((L.start[n] + 3) / 4, B), dim3(256), 0, st, in, x, L);
+    if (B > LSB / 2 && in <= 256)
+        hipLaunchKernelGGL(k_linear_silu_multi_b, dim3((L.start[n] + 4 * LSR - 1) / (4 * LSR), (B + LSB - 1) / LSB),
+                           dim3(256), LSB * in * sizeof(float), st, in, B, x, L);
+    else
+        hipLaunchKernelGGL(k_linear_silu_multi, dim3((L.start[n] + 3) / 4, B), dim3(256), 0, st, in, x, L);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

@@ -99,6 +99,13 @@ SIGNATURES = {
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_conv2d_bf16": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rdq_conv2d_bf16_gn_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),
+    "rdq_conv2d_bf16_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                          c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_size_t, c_void_p]),
+    "rdq_conv2d_bf16_gn_silu_out": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "rdq_group_norm_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
     "rdq_group_norm_silu": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -15,7 +15,7 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     red_diffeq::fwi(v, plan, vel_mode, keep_history) -> (seis, coeffs, vstat, history)
         differentiable in v (register_autograd: adjoint + finalize), what FWIForward calls
   U-Net (include/red_diffeq_unet.h)
-    conv2d_mfma, conv2d_rms, conv2d_gn_silu, conv2d_gn_silu_sc, conv2d_gn_silu_lsm, conv2d_gn_silu_out, unet_head,
+    conv2d_mfma, conv2d_rms, conv2d_gn_silu, conv2d_bf16_gn_silu, conv2d_bf16_gn_silu_out, conv2d_gn_silu_sc, conv2d_gn_silu_lsm, conv2d_gn_silu_out, unet_head,
     gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb, linear_attn, linear_attn_block, attn,
     red_q_sample, red_q_sample_into, red_eps
   loop (include/red_diffeq_loop.h)
@@ -407,6 +407,76 @@ def _(x, x2, weight, bias, pad, mode, gamma, beta, scale_shift, groups, eps, pos
     return x.new_empty(shape)
 
 
+def conv_gn_bf16_fusable(x, x2, weight, pad, mode, groups):
+    """rdq_conv2d_bf16_gn_silu applies (the bf16 halo-staged conv, H*W >= 256, C / G in {8, 16, 32, 64})."""
+    d, _ = _conv_desc(x, x2, weight, pad, mode)
+    return bf16_eligible(weight) and int(_hip.lib().rdq_conv2d_bf16_gn_ws_bytes(ctypes.byref(d), int(groups))) > 0
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_bf16_gn_silu", mutates_args=())
+def conv2d_bf16_gn_silu(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], pad: int, mode: int,
+                        gamma: Tensor, beta: Tensor, scale_shift: Optional[Tensor], groups: int, eps: float,
+                        post: Optional[Tensor]) -> Tensor:
+    """conv2d_gn_silu with bf16 conv operands (fp32 accumulation): the configs[4] batched U-Net's Block, the
+    GroupNorm statistics reduced in the halo-staged conv's epilogue (two launches)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    d, shape = _conv_desc(x, x2, weight, pad, mode)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_bf16_gn_ws_bytes(ctypes.byref(d), int(groups)))
+    if nws == 0 or not bf16_eligible(weight):
+        raise ValueError("conv2d_bf16_gn_silu: shape not supported by the fused form (see conv_gn_bf16_fusable)")
+    st = _hip.stream_of(x)
+    wp = _bf16_pack(weight, d, st)
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    y = torch.empty(shape, device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_bf16_gn_silu(ctypes.byref(d), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(wp), _hip.ptr(bias),
+                                         int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta), _hip.ptr(ss),
+                                         _hip.ptr(pr), _hip.ptr(y), _hip.ptr(ws), nws, st), "rdq_conv2d_bf16_gn_silu")
+    return y
+
+
+@conv2d_bf16_gn_silu.register_fake
+def _(x, x2, weight, bias, pad, mode, gamma, beta, scale_shift, groups, eps, post):
+    _, shape = _conv_desc(x, x2, weight, pad, mode)
+    return x.new_empty(shape)
+
+
+@torch.library.custom_op(f"{LIB}::conv2d_bf16_gn_silu_out", mutates_args=())
+def conv2d_bf16_gn_silu_out(x: Tensor, weight: Tensor, bias: Optional[Tensor], pad: int, gamma: Tensor, beta: Tensor,
+                            scale_shift: Optional[Tensor], groups: int, eps: float, post: Optional[Tensor],
+                            w_out: Tensor, b_out: Optional[Tensor]) -> Tensor:
+    """conv2d_gn_silu_out on the bf16 halo-staged conv (the configs[4] batched U-Net's tail)."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    d, shape = _conv_desc(x, None, weight, pad, 0)
+    L = _hip.lib()
+    nws = int(L.rdq_conv2d_bf16_gn_ws_bytes(ctypes.byref(d), int(groups)))
+    if nws == 0 or not bf16_eligible(weight):
+        raise ValueError("conv2d_bf16_gn_silu_out: shape not supported by the fused form (see conv_gn_bf16_fusable)")
+    st = _hip.stream_of(x)
+    wp = _bf16_pack(weight, d, st)
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    nf = int(w_out.shape[0])
+    yf = torch.empty(shape[0], nf, shape[2], shape[3], device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_bf16_gn_silu_out(ctypes.byref(d), _hip.ptr(x), None, _hip.ptr(wp), _hip.ptr(bias),
+                                             int(groups), float(eps), _hip.ptr(gamma), _hip.ptr(beta), _hip.ptr(ss),
+                                             _hip.ptr(pr), nf, _hip.ptr(w_out.contiguous()), _hip.ptr(b_out),
+                                             _hip.ptr(yf), _hip.ptr(ws), nws, st), "rdq_conv2d_bf16_gn_silu_out")
+    return yf
+
+
+@conv2d_bf16_gn_silu_out.register_fake
+def _(x, weight, bias, pad, gamma, beta, scale_shift, groups, eps, post, w_out, b_out):
+    _, shape = _conv_desc(x, None, weight, pad, 0)
+    return x.new_empty(shape[0], w_out.shape[0], shape[2], shape[3])
+
+
 def conv_gn_sc_fusable(x, x2, weight, weight_s, groups):
     """rdq_conv2d_gn_silu_sc applies: block1's 3x3 conv + GroupNorm (conv_gn_fusable) and a 1x1
     shortcut of the same input in the channel-chunk form (channel counts multiples of 64)."""
@@ -524,10 +594,12 @@ def _(x, weight, bias, pad, gamma, beta, scale_shift, groups, eps, post, w_out, 
 
 
 def unet_head_fusable(x, weight, time_mlp):
-    """rdq_unet_head applies: init_conv outside the channel-chunk form (7x7 / 3x3, cout <= 64, no K split)."""
+    """rdq_unet_head applies: init_conv outside the channel-chunk form (7x7 / 3x3, cout <= 64, no K split), B <= 16
+    (beyond, the time MLP's batched kernel reads its weights once per sample block instead)."""
     cout, cin, kh, kw = weight.shape
     dim, hid = time_mlp[1].weight.shape[1], time_mlp[1].weight.shape[0]
-    return kh == kw and kh in (3, 7) and cout <= 64 and cin * kh * kw <= 224 and x.shape[1] == cin and \
+    return x.shape[0] <= 16 and kh == kw and kh in (3, 7) and cout <= 64 and cin * kh * kw <= 224 and \
+        x.shape[1] == cin and \
         (kh == 7 or cin % 8 != 0) and dim + hid <= 7680
 
 
@@ -891,6 +963,7 @@ def _forward_only(op, name):
 
 
 for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"), (conv2d_gn_silu_sc, "conv2d_gn_silu_sc"),
+                   (conv2d_bf16_gn_silu, "conv2d_bf16_gn_silu"), (conv2d_bf16_gn_silu_out, "conv2d_bf16_gn_silu_out"),
                    (conv2d_gn_silu_lsm, "conv2d_gn_silu_lsm"), (conv2d_gn_silu_out, "conv2d_gn_silu_out"), (unet_head, "unet_head"),
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),

@@ -75,6 +75,12 @@ def test_unet_and_loop_ops_opcheck(cuda):
     wg = r(64, 24, 3, 3) * 0.1
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, r(64), 1, 0, r(64), r(64), r(2, 128), 8, 1e-5, r(2, 64, 12, 10)))
     opcheck(ops.conv2d_gn_silu, (x, x2, wg, None, 1, 0, r(64), r(64), None, 8, 1e-5, None))
+    xb = r(64, 64, 36, 36)                               # 648 halo tiles: the bf16 halo-staged conv
+    opcheck(ops.conv2d_bf16_gn_silu, (xb, None, r(128, 64, 3, 3) * 0.1, r(128), 1, 0, r(128), r(128), r(64, 256), 8,
+                                      1e-5, None))
+    xo = r(128, 64, 36, 36)                              # 648 halo tiles at cout 64
+    opcheck(ops.conv2d_bf16_gn_silu_out, (xo, r(64, 64, 3, 3) * 0.1, r(64), 1, r(64), r(64), None, 8, 1e-5, xo,
+                                          r(1, 64, 1, 1), r(1)))
     xs, xs2 = r(2, 64, 12, 10), r(2, 64, 12, 10)
     opcheck(ops.conv2d_gn_silu_sc, (xs, xs2, r(64, 128, 3, 3) * 0.1, r(64), r(64), r(64), r(2, 128), 8, 1e-5,
                                     r(64, 128, 1, 1), r(64)))
@@ -197,3 +203,28 @@ def test_unet_static_graph_io(cuda):
         assert torch.equal(net.replay_static(xs, ts), y)
         assert net.graph_io(x.shape, x.device)[0] is xs            # one graph per shape
     assert net.graph_io(x.shape, x.device) is None                   # grad enabled: eager, no graph
+
+
+def test_unet_bf16_batched_fused_tail(cuda):
+    """bf16 U-Net at a batch that takes the halo-staged conv everywhere at 72 x 72 (the configs[4] tile
+    batch form): the fused tail (block2's normalise pass feeding final_conv) and the bf16 Blocks with
+    their statistics in the conv epilogue vs the separate-launch tail, within fp32 rounding."""
+    from red_diffeq.models import unet_ops
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(5)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval().set_precision("bf16")
+    x = torch.randn(27, 1, 72, 72, device=cuda).clamp(-1, 1)
+    t = torch.randint(0, 1000, (27,), device=cuda)
+    with torch.no_grad(), torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        y = net(x, t)
+    names = {e.name for e in prof.events()}
+    for op in ("conv2d_bf16_gn_silu", "conv2d_bf16_gn_silu_out"):
+        assert f"red_diffeq::{op}" in names, op
+    unet_ops.FUSED_EDGES = False
+    try:
+        with torch.no_grad():
+            ysep = net(x, t)
+    finally:
+        unet_ops.FUSED_EDGES = True
+    err = (y - ysep).abs().max().item() / ysep.abs().max().item()
+    assert err < 1e-5, err

@@ -224,6 +224,24 @@ def test_time_mlp_and_scale_shifts(cuda):
             close(s, b.mlp[1](F.silu(te)))
 
 
+def test_time_mlp_and_scale_shifts_batched(cuda):
+    """The large-batch kernels (B > 16: the configs[4] tile batch) give every sample exactly what the
+    per-sample launch gives it."""
+    from red_diffeq.models.diffusion import Unet
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(8)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    t = torch.randint(0, 1000, (45,), device=cuda)
+    blocks = net._resnet_blocks()
+    with torch.no_grad():
+        te = ops.time_mlp(t, net.time_mlp)
+        ss = ops.resnet_scale_shifts(te, blocks)
+        for i in (0, 7, 8, 31, 32, 44):
+            assert torch.equal(te[i:i + 1], ops.time_mlp(t[i:i + 1], net.time_mlp))
+            for a, b in zip(ss, ops.resnet_scale_shifts(te[i:i + 1], blocks)):
+                assert torch.equal(a[i:i + 1], b)
+
+
 # the U-Net's linear-attention blocks (dim 64 at 72 / 36, 128 at 18 / 36, 256 at 18): the fused
 # block (rdq_linear_attention_block: 21 chunks at 72 x 72 combined in their own launch, <= 8 in the
 # output launch), B = 1 and 2; C = 32 takes the unfused three-op path
@@ -364,6 +382,38 @@ def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
     ref = F.conv2d(_bf(xin), _bf(conv.weight), conv.bias, padding=1) + (r if res else 0)
     close(got, ref, rel=2e-5)
     close(got, per_tap, rel=2e-5)
+
+
+# Block.forward on the bf16 halo-staged conv with the GroupNorm statistics in its epilogue
+# (rdq_conv2d_bf16_gn_silu, the configs[4] batched U-Net) vs the same conv followed by the separate
+# GroupNorm pass: the conv output is the same kernel's; the statistics differ in fp64 summation order
+@pytest.mark.parametrize("cin1,cin2,cout,H,B,ss,post,mode", [
+    (64, 0, 64, 72, 32, True, True, "plain"), (64, 64, 64, 72, 32, True, False, "plain"),
+    (128, 0, 128, 36, 128, False, True, "plain"), (256, 0, 256, 18, 128, True, False, "plain"),
+    (128, 0, 128, 72, 16, True, False, "up")])
+def test_conv_bf16_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post, mode):
+    from red_diffeq import ops as O
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(21)
+    conv = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    norm = nn.GroupNorm(8, cout).to(cuda)
+    with torch.no_grad():
+        norm.weight.mul_(1 + 0.3 * torch.randn_like(norm.weight))
+        norm.bias.add_(0.2 * torch.randn_like(norm.bias))
+    Hin = H // 2 if mode == "up" else H
+    md = ops.UPSAMPLE2 if mode == "up" else ops.PLAIN
+    x = torch.randn(B, cin1, Hin, Hin, device=cuda)
+    x2 = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    sc = torch.randn(B, 2 * cout, device=cuda) if ss else None
+    pr = torch.randn(B, cout, H, H, device=cuda) if post else None
+    assert O.conv_gn_bf16_fusable(x, x2, conv.weight, 1, md, 8)
+    with torch.no_grad(), ops.precision("bf16"):
+        got = torch.ops.red_diffeq.conv2d_bf16_gn_silu(x, x2, conv.weight, conv.bias, 1, md, norm.weight, norm.bias,
+                                                       sc, 8, float(norm.eps), pr)
+        ref = ops.group_norm_affine_silu(ops.conv2d(x, conv, x2=x2, mode=md), norm, sc)
+        if post:
+            ref = ref + pr
+    close(got, ref, rel=1e-5)
 
 
 def test_unet_bf16_close_to_fp32(cuda):
