@@ -758,6 +758,7 @@ __global__ __launch_bounds__(256) void k_gn_stats(int BG, int nchunk, int64_t gs
 // where the row allows it); the operation order is the per-element formula's
 // stat == nullptr (small grids, where one more launch costs more than the arithmetic): every
 // workgroup derives its group's statistics from the chunk partials itself
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
                                                   const float *__restrict__ ss, const float *__restrict__ stat,
@@ -765,7 +766,7 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
                                                   float *__restrict__ y)
 {
     const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
-    const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
+    const int cl = SMALL ? 0 : blockIdx.x / nch, ch = SMALL ? 0 : blockIdx.x - cl * nch;
     const int c = g * cpg + cl;
     float mean, rstd;
     if (stat) {
@@ -778,8 +779,18 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
         mean = st2[0];
         rstd = st2[1];
     }
-    const float ga = gamma[c], be = beta[c];
     const bool sso = ss != nullptr;
+    if constexpr (SMALL) {        // small images: -nch whole channels of the group per workgroup
+        const int cpb = -nch, cl0 = blockIdx.x * cpb, n = min(cpb, cpg - cl0) * HW;
+        const size_t base = ((size_t)b * C + g * cpg + cl0) * HW;
+        for (int e = threadIdx.x; e < n; e += 256) {
+            const int cc = g * cpg + cl0 + e / HW;
+            const float s1 = sso ? ss[(size_t)b * 2 * C + cc] + 1.0f : 0.0f, sh1 = sso ? ss[(size_t)b * 2 * C + C + cc] : 0.0f;
+            y[base + e] = gn_silu1(x[base + e], mean, rstd, gamma[cc], beta[cc], sso, s1, sh1);
+        }
+        return;
+    }
+    const float ga = gamma[c], be = beta[c];
     const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
     const float *px = x + ((size_t)b * C + c) * HW;
     float *py = y + ((size_t)b * C + c) * HW;
@@ -803,6 +814,7 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
 // workgroup sums its (sample, group)'s per-tile partials — lane l takes tiles l, l+64, ... of the
 // sample in order, then a fixed xor tree — and the pass adds an optional residual after the SiLU
 // (ResnetBlock's identity shortcut, diffusion.py:168)
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const float *__restrict__ x,
                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
                                                     const float *__restrict__ ss, const double *__restrict__ gnp,
@@ -810,7 +822,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
                                                     int bm = CC_BM)
 {
     const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
-    const int cl = blockIdx.x / nch, ch = blockIdx.x - cl * nch;
+    const int cl = SMALL ? 0 : blockIdx.x / nch, ch = SMALL ? 0 : blockIdx.x - cl * nch;
     const int c = g * cpg + cl;
     const size_t base = ((size_t)b * C + c) * HW;
     // this thread's elements, residual and channel constants are loaded first (independent of the
@@ -818,7 +830,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     const bool vec = (HW & 3) == 0;
     const int i4 = (ch * 256 + (int)threadIdx.x) * 4;
     float4 v = {0.0f, 0.0f, 0.0f, 0.0f}, r = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (vec && i4 < HW) {
+    if (!SMALL && vec && i4 < HW) {
         v = *reinterpret_cast<const float4 *>(x + base + i4);
         if (post) r = *reinterpret_cast<const float4 *>(post + base + i4);
     }
@@ -851,6 +863,18 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     }
     __syncthreads();
     const float mean = st2[0], rstd = st2[1];
+    if constexpr (SMALL) {        // small images: -nch whole channels of the group per workgroup
+        const int cpb = -nch, cl0 = blockIdx.x * cpb, n = min(cpb, cpg - cl0) * HW;
+        const size_t base0 = ((size_t)b * C + g * cpg + cl0) * HW;
+        for (int e = threadIdx.x; e < n; e += 256) {
+            const int cc = g * cpg + cl0 + e / HW;
+            const float s1 = sso ? ss[(size_t)b * 2 * C + cc] + 1.0f : 0.0f, sh1 = sso ? ss[(size_t)b * 2 * C + C + cc] : 0.0f;
+            float u = gn_silu1(x[base0 + e], mean, rstd, gamma[cc], beta[cc], sso, s1, sh1);
+            if (post) u += post[base0 + e];
+            y[base0 + e] = u;
+        }
+        return;
+    }
     if (vec) {
         if (i4 < HW) {
             v.x = gn_silu1(v.x, mean, rstd, ga, be, sso, sc1, sh);
@@ -2460,6 +2484,34 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 }
 }  // namespace
 
+// the small-image form is its own instantiation (the per-channel form's code is unchanged by it)
+#define LAUNCH_GN_T(GRID, ST, ...)                                                                     \
+    do {                                                                                               \
+        if (nch < 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<true>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false>), GRID, dim3(256), 0, ST, __VA_ARGS__);      \
+    } while (0)
+#define LAUNCH_GN(GRID, ST, ...)                                                                       \
+    do {                                                                                               \
+        if (nch < 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply<true>), GRID, dim3(256), 0, ST, __VA_ARGS__);   \
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply<false>), GRID, dim3(256), 0, ST, __VA_ARGS__);        \
+    } while (0)
+
+// GroupNorm pass grid: one workgroup per (channel, 1024-element chunk) of a group, or for images of
+// <= 512 pixels in grids of more than 8192 workgroups -nch = 1024 / HW whole channels per workgroup
+// (9 x 9 at B = 344 had 176 K workgroups of 81 elements each: 138 -> 10 us per pass; at B = 1 the
+// per-channel form is faster); returns the x extent, *nch the kernels' chunk argument
+static int gn_grid(int B, int C, int G, int HW, int *nch)
+{
+    const int cpg = C / G;
+    if (HW <= 512 && (int64_t)C * B > 8192) {
+        const int cpb = 1024 / HW;
+        *nch = -cpb;
+        return (cpg + cpb - 1) / cpb;
+    }
+    *nch = (HW + 1023) / 1024;
+    return cpg * *nch;
+}
+
 extern "C" {
 
 size_t rdq_conv2d_tickets(const rdq_conv_desc *d)
@@ -2608,8 +2660,10 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
     }
-    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
-    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
+    const int C = d->cout, HW = c.HW;
+    int nch = 0;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, gnp, eps, post_residual, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
@@ -2679,8 +2733,10 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
     const int gy_a = (d->cout + CC_BN - 1) / CC_BN, gy_b = (cout_s + CC_BN - 1) / CC_BN;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, gy_a + gy_b, std::max(c.S, e.S));
     hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
-    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
-    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, h, gamma, beta,
+    const int C = d->cout, HW = c.HW;
+    int nch = 0;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, c.gnp, eps, nullptr, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
@@ -2716,8 +2772,10 @@ int rdq_conv2d_gn_silu_lsm(const rdq_conv_desc *d, const float *x, const float *
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc_lsm<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c, L, in, temb,
                            nlsm, per_b);
-    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
-    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, c.y, gamma, beta,
+    const int C = d->cout, HW = c.HW;
+    int nch = 0;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
                        ss_index >= 0 ? ly[ss_index] : nullptr, c.gnp, eps, post_residual, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
@@ -2925,8 +2983,10 @@ int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float 
 {
     C3Args c;
     if (!y || !gamma || !beta || !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st)) return RDQ_E_INVALID;
-    const int C = d->cout, HW = c.HW, nch = (HW + 1023) / 1024;
-    hipLaunchKernelGGL(k_gn_apply_t, dim3((C / G) * nch, d->B * G), dim3(256), 0, st, C, HW, G, nch, c.y, gamma, beta,
+    const int C = d->cout, HW = c.HW;
+    int nch = 0;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
                        scale_shift, c.gnp, eps, post_residual, y, C3_BM);
     RDQ_CHECK(hipGetLastError());
     return 0;
@@ -2964,12 +3024,13 @@ int rdq_group_norm_silu(int32_t B, int32_t C, int32_t HW, int32_t G, float eps, 
     double *part = (double *)ws;
     float *stat = (float *)(part + (size_t)B * G * nchunk * 2);
     hipLaunchKernelGGL(k_gn_partial, dim3(nchunk, B * G), dim3(256), 0, st, x, gsize, nchunk, part);
-    const int nch = (HW + 1023) / 1024;               // 1024 elements of one channel row per workgroup
-    const int64_t blocks = (int64_t)(C / G) * nch * B * G;
+    int nch = 0;
+    const int gxa = gn_grid(B, C, G, HW, &nch);
+    const int64_t blocks = (int64_t)gxa * B * G;
     const bool sep = blocks > 4096;                    // a separate statistics pass pays off
     if (sep)
         hipLaunchKernelGGL(k_gn_stats, dim3((B * G + 255) / 256), dim3(256), 0, st, B * G, nchunk, gsize, eps, part, stat);
-    hipLaunchKernelGGL(k_gn_apply, dim3((C / G) * nch, B * G), dim3(256), 0, st, C, HW, G, nch, x, gamma, beta, ss,
+    LAUNCH_GN(dim3(gxa, B * G), st, C, HW, G, nch, x, gamma, beta, ss,
                        sep ? stat : nullptr, part, nchunk, eps, y);
     RDQ_CHECK(hipGetLastError());
     return 0;

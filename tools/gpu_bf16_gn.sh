@@ -13,3 +13,6 @@ cat $O/unet.jsonl
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
     python3 tools/bench_configs4.py --unet-only --precision bf16 > $O/prof.log 2>&1 || exit $?
 ls $O/prof
+timeout -k 10 300 python -u tools/unet_prof_b1.py 1 200 > $O/time.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/unet_prof_b1.py 8 50 >> $O/time.log 2>&1 || exit $?
+grep -v amdgpu.ids $O/time.log
