@@ -146,7 +146,10 @@ class FwiPlan:
                    "rdq_fwi_set_tuning")
 
     def __del__(self):
-        _ops.unregister_plan(getattr(self, "op_id", -1))
+        try:
+            _ops.unregister_plan(getattr(self, "op_id", -1))
+        except Exception:          # interpreter shutdown: module globals already torn down
+            pass
         h = getattr(self, "handle", None)
         if h is not None and h.value:
             try:
