@@ -228,16 +228,22 @@ class InversionEngine:
                         reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
                     predicted = fwi_forward(v_in)
                     loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
+                    # the data term's backward (the FWI adjoint) does not need the regulariser: it
+                    # is run first, so the side stream's U-Net overlaps the adjoint too, and only the
+                    # regulariser's (elementwise) backward waits for it.  d(obs + lambda reg) / d mu
+                    # is accumulated as the same two-tensor sum as in one backward (bit for bit).
+                    optimizer.zero_grad()
+                    loss_obs.sum().backward()
                     main.wait_stream(side)
                     reg_loss.record_stream(main)
+                    (reg_lambda * reg_loss).sum().backward()
                 else:
                     predicted = fwi_forward(v_in)
                     loss_obs = loss_calc.observation_loss(predicted, y, mask=mask)
                     reg_loss, time_tensor = loss_calc.regularization_loss(x0_pred, generator=None)
-                total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
-
-                optimizer.zero_grad()
-                total_loss.sum().backward()
+                    total_loss = loss_calc.total_loss(loss_obs, reg_loss, reg_lambda)
+                    optimizer.zero_grad()
+                    total_loss.sum().backward()
                 optimizer.step(guard=None if monitor is None else monitor.guard())   # + clamp_(-1, 1)
                 optimizer.lr = scheduler.step()
                 if monitor is not None:
