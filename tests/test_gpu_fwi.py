@@ -287,17 +287,20 @@ def test_batch_and_dot_product_openfwi_ns8(cuda):
     from red_diffeq.utils.synthetic import make_model
     ctx = dict(n_grid=70, nt=1000, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=8)
     fwi = make_fwi(ctx)
+    # draws from a generator of the test's own: with the global one they depended on the tests run
+    # before this one, and some directions put the central difference's truncation error near the bar
+    gen = torch.Generator(device=cuda).manual_seed(2024)
     v = torch.from_numpy(vnorm(make_model("curvevel", 70, 70, seed=5, batch=2))).to(cuda).double()
-    v = v + 0.02 * torch.rand_like(v)
+    v = v + 0.02 * torch.rand(v.shape, generator=gen, device=cuda, dtype=v.dtype)
     v[:, 0, 30, 40] = v.amin(dim=(1, 2, 3)) - 0.05          # unique minimum
     v = v.float()
     vv = v.clone().requires_grad_(True)
     seis = fwi(vv)
-    w = torch.randn_like(seis)
+    w = torch.randn(seis.shape, generator=gen, device=cuda, dtype=seis.dtype)
     (seis * w).sum().backward()
     fwi.check()
     g = vv.grad.double()
-    dv = 5e-3 * torch.randn_like(v)
+    dv = 5e-3 * torch.randn(v.shape, generator=gen, device=cuda, dtype=v.dtype)
     with torch.no_grad():
         lhs = (((fwi(v + dv).double() - fwi(v - dv).double()) / 2) * w.double()).sum()
     fwi.check()
