@@ -8,9 +8,11 @@ history) -> L1 misfit -> TV -> hand-written adjoint (1000 steps) -> gradient fin
 Inputs (velocity model, observed data) are synthetic and resident in HBM before timing.
 
 value = shot-timesteps/s over the whole job = N * ns_per_gpu * nt * B / (step time, max over
-ranks).  Weak scaling: every rank owns 8 shots of an 8N-shot survey.
+ranks).  Weak scaling.  N = 1: configs[1] (FlatVel-A, 8 shots).  N > 1: configs[3]'s shape
+(CurveFault-B, 32 shots per GPU: 256 over 8 GPUs); the N = 1 line also reports that per-rank
+workload on one GPU ("configs3_rank_workload") as the base of the scaling curve.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--ns 8] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--ns S] [--family F] [--no-cpu-baseline]
 
 --gpus N > 1 outside a torch.distributed launcher starts the N ranks itself (torch.distributed.run,
 one process per GPU, RCCL) as child processes; this parent never touches the GPU.
@@ -42,7 +44,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--ns", type=int, default=8, help="shots per GPU")
+    p.add_argument("--ns", type=int, default=None,
+                   help="shots per GPU (default: 8 at N=1, configs[1]; 32 at N>1, configs[3]: 256 shots over 8 GPUs)")
+    p.add_argument("--family", default=None, help="synthetic model family (default flatvel at N=1, curvefault at N>1)")
     p.add_argument("--nt", type=int, default=1000)
     p.add_argument("--batch", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -141,6 +145,49 @@ def red_loop_wallclock(dev, a, ns=32, family="curvevel"):
     t_w = run(a.warmup)
     t_all = run(a.warmup + a.steps)
     return round((t_all - t_w) / a.steps * 1e3, 3)
+
+
+def rank_workload_rate(dev, a, nsl, family):
+    """One rank's share of configs[3] (CurveFault-B, 32 of the 256 shots) on this GPU: the same
+    gradient step as the N > 1 bench minus its all-reduce, shot-timesteps/s over `a.steps` steps.
+    The N-GPU scaling efficiency on configs[3]'s shape is value(N) / (N x this)."""
+    from red_diffeq.core.fused import CosineLR, FusedAdamClamp
+    from red_diffeq.core.losses import l1_misfit
+    from red_diffeq.regularization.benchmark import total_variation_loss
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import prepare_initial_model, s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.synthetic import make_model
+    nt = a.nt
+    ctx = dict(n_grid=70, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=nsl * 8)
+    fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none,
+                     shots=(0, nsl))
+    vt = torch.from_numpy(make_model(family, 70, 70, seed=8888, batch=1))
+    with torch.no_grad():
+        y = fwi(v_normalize(vt).to(dev))
+    mu = torch.nn.functional.pad(prepare_initial_model(vt, "smoothed", sigma=10.0), (1, 1, 1, 1)).to(dev)
+    mu.requires_grad_(True)
+    opt = FusedAdamClamp(mu, lr=0.03, clamp=(-1.0, 1.0))
+    sched = CosineLR(0.03, T_max=300, eta_min=0.0)
+    nobs = torch.full((1,), float(nsl * 8 * nt * 70), device=dev)
+
+    def step():
+        loss = l1_misfit(fwi(mu[:, :, 1:-1, 1:-1]), y, None, nobs) + 0.01 * total_variation_loss(mu)
+        opt.zero_grad()
+        loss.sum().backward()
+        opt.step()
+        opt.lr = sched.step()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    fwi.check()
+    return {"workload": f"configs[3] per-rank share: CurveFault-B, {nsl} of {nsl * 8} shots, nt={nt}, one GPU, "
+                        "no all-reduce", "ms_per_step": round(dt * 1e3, 4),
+            "shot_timesteps_per_s": round(nsl * nt / dt, 1), "kernels": fwi._plan(70, 70, dev).launch_info(1)}
 
 
 def launch_ranks(a):
@@ -253,7 +300,12 @@ def main():
     from red_diffeq.utils.data_trans import prepare_initial_model, s_normalize_none, v_denormalize, v_normalize
     from red_diffeq.utils.synthetic import make_model
 
-    B, nsl, nt = a.batch, a.ns, a.nt
+    # N = 1: configs[1] (FlatVel-A, 8 shots).  N > 1: configs[3]'s shape (CurveFault-B, 32 shots per GPU,
+    # 256 shots at N = 8), weak scaling; its one-GPU rank workload is reported by the N = 1 line too
+    # ("configs3_rank_workload") so a scaling curve can be read on the same per-rank shape.
+    nsl = a.ns if a.ns is not None else (8 if world == 1 else 32)
+    family = a.family or ("flatvel" if world == 1 else "curvefault")
+    B, nt = a.batch, a.nt
     ns_tot = nsl * world
     ctx = dict(n_grid=70, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns_tot)
     fwi = FWIForward(dict(ctx), dev, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none,
@@ -262,7 +314,7 @@ def main():
         # ranks share a GPU in the rehearsal: whole-chip persistent grids of two processes cannot be
         # co-resident (they would report "not resident"), so the rehearsal runs the chunked kernels
         fwi._plan(70, 70, dev).set_persistent(False)
-    vtrue = make_model("flatvel", 70, 70, seed=8888, batch=B)
+    vtrue = make_model(family, 70, 70, seed=8888, batch=B)
     vt = torch.from_numpy(vtrue)
     with torch.no_grad():
         y = fwi(v_normalize(vt).to(dev))                         # observed data, local shots
@@ -342,15 +394,15 @@ def main():
         allreduce_us = round(float(np.median(ts_[5:])), 2)
     info = plan.launch_info(B)
     T = info["adj_T"]
+    launches = info["adj_launches"]
     if info["adj_persistent"]:
-        kname = f"k_adj_pr<{T}>"                 # the whole adjoint time loop is ONE launch
-        launches = 1
+        kname = f"k_adj_pr<{T}>"                 # the whole adjoint time loop of a shot group is ONE launch
     else:
         kname = f"k_adj_tb<{T}>"                 # one launch per T steps
-        launches = -(-nt // T)
-    steps_per_launch = nt / launches
+    shot_steps_per_launch = nsl * B * nt / launches
+    steps_per_launch = shot_steps_per_launch / (nsl * B)
     adj_launch_us = adj_ms * 1e3 / launches      # event-timed, incl. the launch's memset nodes
-    adj_bytes = 16.0 * npad * nsl * B * steps_per_launch   # adjoint 16*Npad B per shot-step
+    adj_bytes = 16.0 * npad * shot_steps_per_launch     # adjoint 16*Npad B per shot-step
     fwd_bytes = 12.0 * npad * nsl * B
     achieved = adj_bytes / (adj_launch_us * 1e-6) / 1e9
     traffic = None
@@ -365,8 +417,12 @@ def main():
         "metric": METRIC, "value": round(units / t_step, 1), "unit": "shot-timesteps/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "configs[1]: OpenFWI FlatVel-A 70x70 (310x310 padded), 8 shots/GPU, nt=1000, "
-                               "fwd+adj gradient + TV + Adam step",
+        "config": {"workload": (("configs[1]: OpenFWI FlatVel-A" if (world == 1 and nsl == 8 and family == "flatvel")
+                                 else ("configs[3] shape: OpenFWI CurveFault-B" if (nsl == 32 and family == "curvefault")
+                                       else f"OpenFWI {family}")) +
+                                f" 70x70 (310x310 padded), {nsl} shots/GPU ({ns_tot} total), nt={nt}, "
+                                "fwd+adj gradient + TV + Adam step" +
+                                (" + one RCCL all-reduce of the model gradient" if world > 1 else "")),
                    "global_batch": B, "shots_per_gpu": nsl, "shots_total": ns_tot, "nt": nt,
                    "parallelism": f"shot-parallel x{world}"},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -385,6 +441,8 @@ def main():
         # per-iteration wallclock of the drop-in loop itself (InversionEngine.optimize with TV,
         # metrics and histories included), the metric's second half
         out["per_iter_fwi_wallclock_ms"] = loop_wallclock(fwi, mu0, vt, y, a, dev, world)
+    if world == 1 and a.ns is None and not a.no_red:
+        out["configs3_rank_workload"] = rank_workload_rate(dev, a, 32, "curvefault")
     if world == 1 and not a.no_red:
         out["unet"] = unet_rate(dev)
         out["unet"]["conv_classes"] = conv_class_rates(dev)

@@ -113,8 +113,9 @@ int rdq_fwi_debug_words(rdq_fwi_plan *plan, uint32_t out[32]);
 int rdq_fwi_set_status_buffer(rdq_fwi_plan *plan, uint32_t *words);
 /* Which kernels a forward / adjoint call for batch B runs: out = {forward persistent region
  * height in waves (0 = chunked), the same for the adjoint, forward steps per epoch/launch,
- * adjoint steps per epoch/launch}. */
-int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[4]);
+ * adjoint steps per epoch/launch, forward time-loop launches per call, adjoint time-loop launches
+ * per call} (persistent: one per resident shot group; chunked: ceil(nt / T)). */
+int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[6]);
 /* Diagnostics: 1 = the persistent kernels accumulate per-wave phase times (s_memrealtime, 10 ns
  * ticks); read_profile synchronises the device, returns and clears them:
  * out[0..5] forward {hand-off wait, time steps, publish, waves, first sweep pass, sweep passes},

@@ -81,16 +81,17 @@ class _Geom(ctypes.Structure):
                 ("wavelet", ctypes.POINTER(ctypes.c_double))]
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def lib(variant=""):
+    """The oracle library; variant "fma" is the FMA-contracted build (ensemble member only)."""
+    if variant not in _libs:
+        path = LIB if not variant else LIB.replace(".so", "_" + variant + ".so")
+        if not os.path.exists(path):
             build()
-        _lib = ctypes.CDLL(LIB)
-    return _lib
+        _libs[variant] = ctypes.CDLL(path)
+    return _libs[variant]
 
 
 def _p(a, t=ctypes.c_float):
@@ -100,8 +101,9 @@ def _p(a, t=ctypes.c_float):
 class OracleFWI:
     """CPU restatement of FWIForward (normalize=True, v_denormalize, s_normalize_none)."""
 
-    def __init__(self, ctx, B, sample_temporal=1, sample_spatial=1.0):
+    def __init__(self, ctx, B, sample_temporal=1, sample_spatial=1.0, variant=""):
         self.ctx = dict(ctx)
+        self.variant = variant
         isx, isz, igx, igz = geometry(ctx, sample_spatial)
         self.isx = np.ascontiguousarray(isx, np.int32)
         self.igx = np.ascontiguousarray(igx, np.int32)
@@ -126,7 +128,7 @@ class OracleFWI:
     def coeffs(self, vnorm):
         vn = np.ascontiguousarray(vnorm, np.float32)
         B, Hp, Wp = self._shape(vn)
-        L = lib()
+        L = lib(self.variant)
         vpad = np.empty((B, Hp, Wp), np.float32)
         L.oracle_vpad(ctypes.byref(self.g), _p(vn), _p(vpad))
         f = {k: np.empty((B, Hp, Wp), np.float32) for k in ("alpha", "temp1", "temp2", "kappa", "beta")}
@@ -143,7 +145,7 @@ class OracleFWI:
         g = self.g
         seis = np.zeros((B, g.ns, self.nrec, g.ng), np.float32)
         hist = np.empty((g.nt + 2, B, g.ns, Hp, Wp), np.float32) if keep_history else None
-        lib().oracle_forward(ctypes.byref(g), _p(c["alpha"]), _p(c["temp1"]), _p(c["temp2"]),
+        lib(self.variant).oracle_forward(ctypes.byref(g), _p(c["alpha"]), _p(c["temp1"]), _p(c["temp2"]),
                              _p(c["beta"]), _p(seis), _p(hist) if keep_history else None)
         if keep_history:
             c["hist"] = hist
@@ -156,7 +158,7 @@ class OracleFWI:
         gA = np.empty((B, Hp, Wp), np.float32)
         gK = np.empty(B, np.float64)
         gb = np.empty((B, g.ns), np.float32)
-        lib().oracle_adjoint(ctypes.byref(g), _p(c["alpha"]), _p(c["temp1"]), _p(c["temp2"]),
+        lib(self.variant).oracle_adjoint(ctypes.byref(g), _p(c["alpha"]), _p(c["temp1"]), _p(c["temp2"]),
                              _p(c["kappa"]), _p(c["hist"]), _p(dseis), _p(gA), _p(gK, ctypes.c_double), _p(gb))
         return gA, gK, gb
 
@@ -164,7 +166,7 @@ class OracleFWI:
         g = self.g
         B = gA.shape[0]
         out = np.empty((B, 1, g.nz, g.nx), np.float32)
-        lib().oracle_grad_finalize(ctypes.byref(g), _p(c["vpad"]), _p(gA), _p(gK, ctypes.c_double),
+        lib(self.variant).oracle_grad_finalize(ctypes.byref(g), _p(c["vpad"]), _p(gA), _p(gK, ctypes.c_double),
                                    _p(gb), _p(c["vmin"]), _p(c["argmin"], ctypes.c_int64), _p(out))
         return out
 

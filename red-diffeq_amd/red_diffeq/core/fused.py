@@ -4,7 +4,6 @@ include/red_diffeq_loop.h): fused Adam + clamp (K11) and fused MAE/RMSE/SSIM (K1
 Reference behaviour: red_diffeq/core/inversion.py:80-111 (torch.optim.Adam, clamp_(-1, 1),
 CosineAnnealingLR, MetricsCalculator).  The learning-rate schedule is torch's recursive
 CosineAnnealingLR formula evaluated on the host (a scalar per iteration, no device sync)."""
-import ctypes
 import math
 
 import torch
@@ -65,11 +64,9 @@ class FusedAdamClamp:
         bc2 = 1 - self.beta2 ** self.t
         step_size = (self.lr / bc1) * -1
         lo, hi = self.clamp if self.clamp is not None else (0.0, 0.0)
-        p = self.param.data
-        _hip.check(_hip.lib().rdq_adam_step(p.numel(), _hip.ptr(p), _hip.ptr(g), _hip.ptr(self.exp_avg),
-                                            _hip.ptr(self.exp_avg_sq), self.beta1, self.beta2, self.eps,
-                                            step_size, bc2 ** 0.5, int(self.clamp is not None), float(lo),
-                                            float(hi), _hip.ptr(guard), _hip.stream_of(p)), "rdq_adam_step")
+        torch.ops.red_diffeq.adam_clamp_(self.param.data, g, self.exp_avg, self.exp_avg_sq, self.beta1, self.beta2,
+                                         self.eps, step_size, bc2 ** 0.5, self.clamp is not None, float(lo),
+                                         float(hi), guard)
 
 
 def metrics(pred, true_norm):

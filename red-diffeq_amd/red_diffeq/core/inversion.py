@@ -17,6 +17,7 @@ kernels, reported through the plan's status word) is handled inside the loop, wi
 per iteration: see ``_FaultMonitor``.
 """
 import os
+import time
 import warnings
 from typing import Optional
 
@@ -49,7 +50,9 @@ class _GradAllReduce(torch.autograd.Function):
             g = g.contiguous()
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
             return g, None, None
-        buf = torch.cat([g.reshape(-1), mon.local_word().to(g.dtype)])
+        # the word rides as 0 / 1 (any status code, whatever its sign or bits, counts as a failure):
+        # the sum is the number of failed ranks, exact in the gradient's dtype
+        buf = torch.cat([g.reshape(-1), (mon.local_word() != 0).to(g.dtype)])
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=ctx.group)
         mon.global_word.copy_(buf[-1:])          # != 0 iff some rank's launch failed
         return buf[:-1].view_as(g), None, None
@@ -79,9 +82,15 @@ class _FaultMonitor:
       most two iterations behind, so no extra stall), and everything at the end of the loop.
     * Recovery: the engine rewinds its host state (Adam step count, LR schedule, RNG) to the first
       failed iteration, switches the operator to its chunked kernels and replays from there.
+    * Re-promotion: a failure is usually transient (another kernel sharing the chip made the
+      resident grid wait), so after ``repromote_after`` clean iterations on the chunked kernels the
+      operator goes back to the persistent ones (``FWIForward.restore_persistent``); each further
+      failure doubles that wait.  More than ``max_recoveries`` failures raise.
     Sharded runs guard on the all-reduced word (``_GradAllReduce``), identical on every rank."""
 
-    def __init__(self, fwi_forward, ts, device, sharded):
+    max_recoveries = 8
+
+    def __init__(self, fwi_forward, ts, device, sharded, repromote_after=16):
         self.fwi = fwi_forward
         self.sharded = sharded
         self.host = torch.zeros(ts, dtype=torch.int32, pin_memory=True)
@@ -89,7 +98,9 @@ class _FaultMonitor:
         self.global_word = torch.zeros(1, dtype=torch.int32, device=device)
         self._zero = torch.zeros(1, dtype=torch.int32, device=device)
         self.checked = 0
-        self.recovered = False
+        self.recoveries = 0
+        self.repromote_after = repromote_after
+        self.repromote_at = None          # iteration at which the persistent kernels come back
 
     def local_word(self):
         w = self.fwi.status_word()
@@ -114,24 +125,95 @@ class _FaultMonitor:
         return None
 
     def recover(self, k, ts):
-        if self.recovered:
-            raise RuntimeError(f"FWI kernels failed again at iteration {k} after the fallback to the chunked path")
+        if self.repromote_at is not None:
+            raise RuntimeError(f"FWI kernels failed at iteration {k} on the chunked path")
+        if self.recoveries >= self.max_recoveries:
+            raise RuntimeError(f"persistent FWI launch failed {self.recoveries + 1} times (last at iteration {k})")
+        wait = self.repromote_after << self.recoveries
         warnings.warn(f"persistent FWI launch failed at iteration {k} (status word set); the gradient was "
-                      "not applied; replaying from that iteration on the chunked kernels", RuntimeWarning)
+                      f"not applied; replaying from that iteration on the chunked kernels (persistent kernels "
+                      f"again after {wait} iterations)", RuntimeWarning)
         self.fwi.fallback_to_chunked()
         self.global_word.zero_()
         self.host[k:].zero_()
         self.events[k:] = [None] * (ts - k)
         self.checked = k
-        self.recovered = True
+        self.recoveries += 1
+        self.repromote_at = k + wait
+
+    def maybe_repromote(self, it):
+        """At the start of iteration it: back to the persistent kernels once the wait is over."""
+        if self.repromote_at is not None and it >= self.repromote_at:
+            restore = getattr(self.fwi, "restore_persistent", None)
+            if callable(restore):
+                restore()
+            self.repromote_at = None
+
+    @property
+    def recovered(self):
+        return self.recoveries > 0
+
+
+class _Progress:
+    """The progress bar's MAE / RMSE / SSIM / t postfix without a host sync: an iteration's history
+    row (and t) is copied asynchronously into pinned memory behind an event — at most every
+    `interval` seconds (tqdm's own refresh period: a copy per iteration would cost the stream a
+    device-to-host round trip each time) — and the bar shows the newest iteration whose copy has
+    completed (event.query(), never a wait)."""
+
+    interval = 0.1
+
+    def __init__(self, ts, width, device):
+        self.host = torch.zeros(ts, width + 1, dtype=torch.float32, pin_memory=True)
+        self.events = [None] * ts
+        self.shown = -1
+        self.has_t = False
+        self.last = -1e30
+
+    def record(self, it, row, time_tensor):
+        now = time.monotonic()
+        if now - self.last < self.interval and it != len(self.events) - 1:
+            return
+        self.last = now
+        n = row.numel()
+        self.host[it, :n].copy_(row.reshape(-1), non_blocking=True)
+        if time_tensor is not None:
+            self.host[it, n:n + 1].copy_(time_tensor.float().mean().reshape(1), non_blocking=True)
+            self.has_t = True
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[it] = ev
+
+    def show(self, pbar, it, B):
+        j = None
+        lo = self.shown if self.shown < it else -1        # (after a rewind, it can be behind)
+        for i in range(it, lo, -1):
+            if self.events[i] is not None and self.events[i].query():
+                j = i
+                break
+        if j is None:
+            return
+        self.shown = j
+        h = self.host[j].numpy()
+        row = h[:-1].reshape(-1, B)
+        post = {"MAE": float(row[4].mean()), "RMSE": float(row[5].mean()), "SSIM": float(row[3].mean())}
+        if self.has_t:
+            post["t"] = int(round(float(h[-1])))
+        pbar.set_postfix(post, refresh=False)
 
 
 class InversionEngine:
+
+    # clean chunked iterations before a failed persistent operator is tried again (_FaultMonitor)
+    repromote_after = 16
 
     def __init__(self, diffusion_model, ssim_loss: SSIM, regularization: Optional[str] = None,
                  use_time_weight: bool = False, sigma_x0: float = 0.0001, fixed_timestep: int = None,
                  show_progress: bool = True):
         self.diffusion_model = diffusion_model
+        # optional list: when set, optimize() appends mu's interior (a device copy, after Adam and
+        # the clamp) at every iteration — the per-iteration model trajectory, for parity tests
+        self.model_trace = None
         self.ssim_loss = ssim_loss
         self.device = diffusion_model.device
         self.sigma_x0 = sigma_x0
@@ -192,20 +274,23 @@ class InversionEngine:
             check = getattr(fwi_forward, "check", None)
             if callable(check):
                 check()          # a failure before the loop (e.g. while making y) is the caller's
-            monitor = _FaultMonitor(fwi_forward, ts, self.device, sharded)
+            monitor = _FaultMonitor(fwi_forward, ts, self.device, sharded, self.repromote_after)
         diffusion = regularization == "diffusion"
         overlap = diffusion and mu.is_cuda and not os.environ.get("RDQ_NO_OVERLAP")
         snaps = [None] * ts
 
         pbar = tqdm(total=ts, desc="Optimizing", unit="step", disable=not self.show_progress)
+        prog = _Progress(ts, len(keys) * B, self.device) if self.show_progress and mu.is_cuda else None
+        trace = self.model_trace
         it = 0
         while True:
             while it < ts:
                 k = monitor.first_fault(it - 2) if monitor is not None else None
                 if k is not None:
-                    it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar)
+                    it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar, trace, prog)
                     continue
                 if monitor is not None:   # host state at the start of the iteration (for a replay)
+                    monitor.maybe_repromote(it)
                     snaps[it] = (optimizer.t, scheduler.lr, scheduler.last_epoch, optimizer.lr,
                                  torch.cuda.get_rng_state(mu.device) if diffusion else None)
                 if diffusion:
@@ -259,18 +344,19 @@ class InversionEngine:
                     row[0] = obs_log + reg_lambda * reg_loss.detach()
                     row[1] = obs_log
                     row[2] = reg_loss.detach()
-                if self.show_progress:
-                    h = row.cpu().numpy()
-                    post = {"MAE": float(h[4].mean()), "RMSE": float(h[5].mean()), "SSIM": float(h[3].mean())}
-                    if time_tensor is not None:
-                        post["t"] = int(round(time_tensor.float().mean().item()))
-                    pbar.set_postfix(post)
+                    if trace is not None:
+                        if len(trace) > it:          # replayed after a rewind
+                            del trace[it:]
+                        trace.append(mu.detach()[:, :, 1:-1, 1:-1].clone())
+                if prog is not None:             # no per-iteration sync (the reference's .item()s)
+                    prog.record(it, row, time_tensor)
+                    prog.show(pbar, it, B)
                 pbar.update(1)
                 it += 1
             k = monitor.first_fault(ts - 1) if monitor is not None else None
             if k is None:
                 break
-            it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar)
+            it = self._rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar, trace, prog)
         pbar.close()
 
         H = hist_dev.cpu().numpy()
@@ -284,10 +370,15 @@ class InversionEngine:
         return streams[device]
 
     @staticmethod
-    def _rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar):
+    def _rewind(k, snaps, optimizer, scheduler, monitor, ts, pbar, trace=None, prog=None):
         """Restore the host state of iteration k (mu and the Adam moments are untouched: every step
         since the failure was skipped on the device) and switch to the chunked kernels."""
         monitor.recover(k, ts)
+        if trace is not None:
+            del trace[k:]
+        if prog is not None:
+            prog.events[k:] = [None] * (ts - k)
+            prog.shown = min(prog.shown, k - 1)
         optimizer.t, scheduler.lr, scheduler.last_epoch, optimizer.lr, rng = snaps[k]
         if rng is not None:
             torch.cuda.set_rng_state(rng, optimizer.param.device)

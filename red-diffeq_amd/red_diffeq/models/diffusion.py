@@ -267,12 +267,16 @@ class Unet(nn.Module):
         return super()._apply(fn, *args, **kwargs)
 
     def _weights_version(self):
-        """Graph-cache key of the weights.  A replay reads the parameters' live storage, so in-place
-        updates (optimizer steps, load_state_dict) need no recapture in fp32; the bf16 path reads
-        packed copies, so there the parameters' version counters are part of the key."""
+        """Graph-cache key of the weights.  A replay reads the parameters' storage at the addresses
+        captured, so the key holds every parameter's data_ptr: a parameter replaced without _apply
+        (load_state_dict(assign=True), ``p.data = t``, a new nn.Parameter on a submodule) changes it
+        and forces a recapture.  In-place updates (optimizer steps, load_state_dict
+        copies) keep the addresses and need none in fp32; the bf16 path reads packed copies, so
+        there the parameters' version counters are part of the key too."""
+        ptrs = tuple(p.data_ptr() for p in self.parameters())
         if self.precision == "bf16":
-            return (getattr(self, "_wgen", 0), tuple(p._version for p in self.parameters()))
-        return getattr(self, "_wgen", 0)
+            return (getattr(self, "_wgen", 0), ptrs, tuple(p._version for p in self.parameters()))
+        return (getattr(self, "_wgen", 0), ptrs)
 
     def _graphed(self, x, time):
         ent = self._graph_entry(x, time)

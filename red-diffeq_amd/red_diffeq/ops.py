@@ -19,7 +19,7 @@ torch.compile see them as ordinary operators instead of opaque ctypes calls.
     gn_silu, rmsnorm, linear, time_mlp, linear_silu_multi, sinusoidal_emb, linear_attn, linear_attn_block, attn,
     red_q_sample, red_q_sample_into, red_eps
   loop (include/red_diffeq_loop.h)
-    l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics
+    l1_misfit / l1_misfit_backward, smooth_reg / smooth_reg_backward, metrics, adam_clamp_
 
 No CPU implementation is registered: a CPU tensor reaching an op raises (no fallback).
 """
@@ -228,7 +228,7 @@ def _conv_desc(x, x2, weight, pad, mode):
 
 def _bf16_pack(weight, d, stream):
     per = _BF16_PACKS.setdefault(weight, {})
-    key = (weight._version, d.cin1, d.cin2)
+    key = (weight._version, weight.data_ptr(), d.cin1, d.cin2)   # data_ptr: `p.data = t` replaces storage
     wp = per.get(key)
     if wp is None:
         per.clear()                      # older versions of this tensor are dead
@@ -947,6 +947,35 @@ def metrics(pred: Tensor, true_norm: Tensor) -> Tensor:
 @metrics.register_fake
 def _(pred, true_norm):
     return pred.new_empty(3, pred.shape[0], dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{LIB}::adam_clamp_", mutates_args=("param", "exp_avg", "exp_avg_sq"))
+def adam_clamp_(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, beta1: float, beta2: float,
+                eps: float, step_size: float, bias_correction2_sqrt: float, clamp: bool, lo: float, hi: float,
+                guard: Optional[Tensor] = None) -> None:
+    """K11: one torch.optim.Adam step (step_size = -lr / (1 - beta1^t), bias_correction2_sqrt =
+    sqrt(1 - beta2^t); torch/optim/adam.py's multi-tensor formula) then param.clamp_(lo, hi) when
+    `clamp`, in one launch (reference inversion.py:87-91).  guard: optional int32 device word; the
+    step is a no-op on the device while it is non-zero (the FWI status word of a failed persistent
+    launch)."""
+    _hip.require_device(param)
+    for t in (grad, exp_avg, exp_avg_sq):
+        if t.shape != param.shape or not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError("adam_clamp_: grad / exp_avg / exp_avg_sq must be contiguous fp32 like param")
+    if not param.is_contiguous() or param.dtype != torch.float32:
+        raise ValueError("adam_clamp_: param must be contiguous fp32")
+    if guard is not None and (guard.dtype != torch.int32 or guard.numel() < 1):
+        raise ValueError("adam_clamp_: guard must be an int32 device word")
+    _hip.check(_hip.lib().rdq_adam_step(param.numel(), _hip.ptr(param), _hip.ptr(grad), _hip.ptr(exp_avg),
+                                        _hip.ptr(exp_avg_sq), beta1, beta2, eps, step_size, bias_correction2_sqrt,
+                                        int(clamp), lo, hi, _hip.ptr(guard), _hip.stream_of(param)),
+               "rdq_adam_step")
+
+
+@adam_clamp_.register_fake
+def _(param, grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bias_correction2_sqrt, clamp, lo, hi,
+      guard=None):
+    return None
 
 
 # ------------------------------------------------------------------ forward-only operators

@@ -113,11 +113,12 @@ class FwiPlan:
         return int(out[0]), [int(v) for v in out[1:7]], [int(v) for v in out[16:24]]
 
     def launch_info(self, B):
-        """{'fwd_persistent', 'adj_persistent', 'fwd_T', 'adj_T'} of a call with batch B."""
-        out = (ctypes.c_int32 * 4)()
+        """{'fwd_persistent', 'adj_persistent', 'fwd_T', 'adj_T', 'fwd_launches', 'adj_launches'} of a
+        call with batch B (launches: time-loop kernel launches per call)."""
+        out = (ctypes.c_int32 * 6)()
         _hip.check(self.lib.rdq_fwi_launch_info(self.handle, int(B), out), "rdq_fwi_launch_info")
         return {"fwd_persistent": bool(out[0]), "adj_persistent": bool(out[1]), "fwd_T": int(out[2]),
-                "adj_T": int(out[3])}
+                "adj_T": int(out[3]), "fwd_launches": int(out[4]), "adj_launches": int(out[5])}
 
     def set_profile(self, enable):
         _hip.check(self.lib.rdq_fwi_set_profile(self.handle, int(bool(enable))), "rdq_fwi_set_profile")
@@ -275,11 +276,17 @@ class FWIForward(nn.Module):
         return None if self._last is None else self._last.status_t[:1]
 
     def fallback_to_chunked(self):
-        """After a persistent-launch failure: every plan runs the chunked (non-resident) kernels from
-        now on, and the status words are cleared (stream-ordered)."""
+        """After a persistent-launch failure: every plan runs the chunked (non-resident) kernels until
+        restore_persistent(), and the status words are cleared (stream-ordered)."""
         for plan in self._plans.values():
             plan.set_persistent(False)
             plan.status_t.zero_()
+
+    def restore_persistent(self):
+        """Back to the persistent kernels (where they fit) after fallback_to_chunked(): the engine
+        re-promotes after a number of clean iterations (core/inversion.py _FaultMonitor)."""
+        for plan in self._plans.values():
+            plan.set_persistent(True)
 
     def coefficients(self, v):
         """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""

@@ -30,6 +30,26 @@ def vnorm(v):
     return ((v - 1500) / 3000 * 2 - 1).astype(np.float32)
 
 
+def regenerate_draws(rows, randn_shape):
+    """The reference's global-RNG draws of a long trajectory (tests/golden/make_long.py), re-made
+    from torch's CPU generator (seed 1234, as the fixture run) in call order: rows of (kind 0 randn /
+    1 randint, low, high, numel, float64 sum); every draw is checked against its recorded sum."""
+    import torch
+    g = torch.Generator().manual_seed(1234)
+    out = []
+    for kind, low, high, n, s in rows:
+        if kind == 0:
+            assert n == int(np.prod(randn_shape)), (n, randn_shape)
+            d = torch.randn(randn_shape, generator=g)
+            name = "randn"
+        else:
+            d = torch.randint(int(low), int(high), (int(n),), generator=g)
+            name = "randint"
+        assert float(d.double().sum()) == s, ("regenerated draw differs from the reference's", len(out))
+        out.append((name, d.numpy()))
+    return out
+
+
 class replay_draws:
     """Replay the reference's recorded global-RNG draws (tests/golden/make_golden.py:record_draws)
     in call order: inside the block every torch.randn / rand / randint / randperm call returns the
@@ -38,11 +58,14 @@ class replay_draws:
 
     FNS = ("randn", "rand", "randint", "randperm")
 
-    def __init__(self, z):
+    def __init__(self, z, randn_shape=(1, 1, 72, 72)):
         import torch
         self.torch = torch
-        kinds = [str(k) for k in z["draw_kinds"]] if "draw_kinds" in z.files else []
-        self.queue = [(k, z[f"draw{i}"]) for i, k in enumerate(kinds)]
+        if "draw_rows" in z.files:
+            self.queue = regenerate_draws(z["draw_rows"], randn_shape)
+        else:
+            kinds = [str(k) for k in z["draw_kinds"]] if "draw_kinds" in z.files else []
+            self.queue = [(k, z[f"draw{i}"]) for i, k in enumerate(kinds)]
         self.pos = 0
 
     @staticmethod

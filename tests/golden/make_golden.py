@@ -554,10 +554,46 @@ def gen_ilvr():
     save("ilvr_small", **out)
 
 
+def gen_post():
+    """RED_DiffEq_POST_PROCESS.diffusion_denoise (regularization/diffusion.py:158-200) with the dim-8
+    U-Net of gen_unet: q_sample to t = 6, then 6 p_sample_deterministic steps
+    (models/diffusion.py:431-452); its randn_like draw from a seeded generator, recorded.  Also
+    p_mean_variance / p_sample_deterministic alone at three timesteps."""
+    diff = ref.diffusion.GaussianDiffusion(_unet_dim8(), image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise").eval()
+    g = torch.Generator().manual_seed(31)
+    mu = torch.rand(2, 1, 72, 72, generator=g) * 2 - 1
+    x = torch.randn(2, 1, 72, 72, generator=g).clamp(-2, 2)
+    out = {"mu": mu.numpy(), "x": x.numpy()}
+    with torch.no_grad():
+        for t in (0, 37, 640):
+            mean, var, logvar, xs = diff.p_mean_variance(x, torch.full((2,), t, dtype=torch.long))
+            out[f"pmv{t}_mean"], out[f"pmv{t}_xs"] = mean.numpy(), xs.numpy()
+            out[f"pmv{t}_var"], out[f"pmv{t}_logvar"] = var.reshape(-1).numpy(), logvar.reshape(-1).numpy()
+            m2, xs2 = diff.p_sample_deterministic(x, t)
+            assert torch.equal(m2, mean) and torch.equal(xs2, xs)
+    draws = []
+    gen = torch.Generator().manual_seed(32)
+    orig = torch.randn_like
+
+    def seeded_randn_like(t, **kw):
+        r = torch.randn(t.shape, generator=gen, dtype=t.dtype)
+        draws.append(r.numpy().copy())
+        return r
+    torch.randn_like = seeded_randn_like
+    try:
+        with torch.no_grad():
+            den = ref.reg_diffusion.RED_DiffEq_POST_PROCESS(diff).diffusion_denoise(mu, 6)
+    finally:
+        torch.randn_like = orig
+    assert len(draws) == 1
+    save("post_dim8", noise=draws[0], denoised=den.numpy(), timesteps=np.array(6), **out)
+
+
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
             loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi,
             ilvr=gen_ilvr, loop_rng=gen_loop_rng, loop_red=gen_loop_red, initial=gen_initial, ckpt=gen_ckpt,
-            loop_red_configs2=gen_loop_red_configs2)
+            loop_red_configs2=gen_loop_red_configs2, post=gen_post)
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

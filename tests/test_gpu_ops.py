@@ -228,3 +228,32 @@ def test_unet_bf16_batched_fused_tail(cuda):
         unet_ops.FUSED_EDGES = True
     err = (y - ysep).abs().max().item() / ysep.abs().max().item()
     assert err < 1e-5, err
+
+
+def test_adam_clamp_op(cuda):
+    """K11 as torch.ops.red_diffeq.adam_clamp_ (mutates param / exp_avg / exp_avg_sq): opcheck, and
+    one step equals torch.optim.Adam + clamp_ (reference inversion.py:87-91) within fp32 rounding; a
+    set guard word makes it a no-op."""
+    from red_diffeq import ops
+    g = torch.Generator().manual_seed(3)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).to(cuda)
+    p, gr, m, v = r(2, 1, 9, 9), r(2, 1, 9, 9), r(2, 1, 9, 9) * 0.1, r(2, 1, 9, 9).abs() * 0.01
+    opcheck(ops.adam_clamp_, (p.clone(), gr, m.clone(), v.clone(), 0.9, 0.999, 1e-8, -0.03, 0.5, True, -1.0, 1.0,
+                              None))
+    word = torch.ones(1, dtype=torch.int32, device=cuda)
+    opcheck(ops.adam_clamp_, (p.clone(), gr, m.clone(), v.clone(), 0.9, 0.999, 1e-8, -0.03, 0.5, True, -1.0, 1.0,
+                              word))
+    q = p.clone()
+    ops.adam_clamp_(q, gr, m.clone(), v.clone(), 0.9, 0.999, 1e-8, -0.03, 0.5, True, -1.0, 1.0, word)
+    assert torch.equal(q, p)                                   # guarded: no-op
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=0.03)
+    ref.grad = gr.clone()
+    opt.step()
+    with torch.no_grad():
+        ref.clamp_(-1, 1)
+    q, mq, vq = p.clone(), torch.zeros_like(p), torch.zeros_like(p)
+    ops.adam_clamp_(q, gr, mq, vq, 0.9, 0.999, 1e-8, -0.03 / (1 - 0.9), (1 - 0.999) ** 0.5, True, -1.0, 1.0, None)
+    assert (q - ref.detach()).abs().max().item() <= 1e-6       # torch foreach Adam: same formula, ulp-level order

@@ -459,3 +459,76 @@ def test_unet_graph_replay_equals_eager(cuda):
             net.final_conv.bias.add_(0.5)
         after = net(xs[0], t)
     assert torch.equal(after, eager[0] + 0.5) or (after - eager[0] - 0.5).abs().max() < 1e-6
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_unet_graph_recaptured_after_weights_replaced(cuda, precision):
+    """A captured forward must not replay stale weight storage: weights replaced without
+    _apply — load_state_dict(assign=True), `p.data = t`, a new nn.Parameter on a submodule — are
+    seen by the next no-grad (graph) call, which equals the eager forward of the new weights."""
+    import os
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(15)
+    net = Unet(dim=16, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval().set_precision(precision)
+    x = torch.randn(2, 1, 72, 72, device=cuda)
+    t = torch.tensor([5, 600], device=cuda)
+
+    def eager():
+        os.environ["RDQ_NO_UNET_GRAPH"] = "1"
+        try:
+            with torch.no_grad():
+                return net(x, t)
+        finally:
+            del os.environ["RDQ_NO_UNET_GRAPH"]
+
+    with torch.no_grad():
+        net(x, t)                                            # captured
+        assert net._graphs
+        sd = {k: (v * 1.01 if v.is_floating_point() else v).clone() for k, v in net.state_dict().items()}
+        net.load_state_dict(sd, assign=True)                 # every parameter on new storage
+        got = net(x, t)
+        assert torch.equal(got, eager())
+        w = net.downs[1][0].block1.proj.weight
+        w.data = w.data * 0.9                                 # same Parameter, new storage
+        got = net(x, t)
+        assert torch.equal(got, eager())
+        net.final_conv.weight = nn.Parameter(net.final_conv.weight.detach() * 1.1)   # new Parameter
+        got = net(x, t)
+        assert torch.equal(got, eager())
+
+
+def test_post_process_and_p_sample_deterministic_vs_reference(cuda):
+    """GaussianDiffusion.p_mean_variance / p_sample_deterministic (reference models/diffusion.py:
+    431-452) at t = 0, 37, 640 and RED_DiffEq_POST_PROCESS.diffusion_denoise (regularization/
+    diffusion.py:158-200: q_sample to t = 6, six deterministic reverse steps) with the dim-8 U-Net, vs
+    the reference's outputs (tests/golden/post_dim8.npz; its randn_like draw replayed)."""
+    from red_diffeq.models.diffusion import GaussianDiffusion
+    from red_diffeq.regularization.diffusion import RED_DiffEq_POST_PROCESS
+    net, _ = _load_unet(cuda)
+    z = load_golden("post_dim8")
+    diff = GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                             objective="pred_noise").to(cuda).eval()
+    x = torch.from_numpy(z["x"]).to(cuda)
+    with torch.no_grad():
+        for t in (0, 37, 640):
+            mean, var, logvar, xs = diff.p_mean_variance(x, torch.full((2,), t, dtype=torch.long, device=cuda))
+            close(mean, torch.from_numpy(z[f"pmv{t}_mean"]).to(cuda), rel=1e-4)
+            close(xs, torch.from_numpy(z[f"pmv{t}_xs"]).to(cuda), rel=1e-4)
+            assert np.allclose(var.reshape(-1).cpu().numpy(), z[f"pmv{t}_var"], rtol=1e-6)
+            assert np.allclose(logvar.reshape(-1).cpu().numpy(), z[f"pmv{t}_logvar"], rtol=1e-6)
+            m2, xs2 = diff.p_sample_deterministic(x, t)
+            assert torch.equal(m2, mean) and torch.equal(xs2, xs)
+    noise = torch.from_numpy(z["noise"])
+    orig = torch.randn_like
+    calls = []
+
+    def replay(t, **kw):
+        calls.append(tuple(t.shape))
+        return noise.to(t.device)
+    torch.randn_like = replay
+    try:
+        den = RED_DiffEq_POST_PROCESS(diff).diffusion_denoise(torch.from_numpy(z["mu"]).to(cuda), int(z["timesteps"]))
+    finally:
+        torch.randn_like = orig
+    assert calls == [(2, 1, 72, 72)]
+    close(den, torch.from_numpy(z["denoised"]).to(cuda), rel=1e-4)
