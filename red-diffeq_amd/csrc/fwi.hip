@@ -293,6 +293,28 @@ __device__ __forceinline__ Halo4 exchange_nw(float (*xch)[NW][4][64], int buf, i
     return h;
 }
 
+// exchange_nw in two halves, so a step can schedule work between the barrier and the reads' use
+template <int NW>
+__device__ __forceinline__ void xch_put(float (*xch)[NW][4][64], int buf, int w, int lane, float top0, float top1,
+                                        float bot1, float bot0)
+{
+    xch[buf][w][0][lane] = top0;
+    xch[buf][w][1][lane] = top1;
+    xch[buf][w][2][lane] = bot1;
+    xch[buf][w][3][lane] = bot0;
+}
+template <int NW>
+__device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w, int lane)
+{
+    Halo4 h;
+    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
+    h.u2 = xch[buf][wu][2][lane];
+    h.u1 = xch[buf][wu][3][lane];
+    h.d1 = xch[buf][wd][0][lane];
+    h.d2 = xch[buf][wd][1][lane];
+    return h;
+}
+
 // the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
 __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
                                           int lane, const float (&fa)[4], const float (&fb)[4], Halo4 &ha,
@@ -763,8 +785,9 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
 // wave-uniform bit masks; lane classes: xin (own interior column), bx (interior column within H of
 // the tile's x edge, or a one-tile-wide grid), cx (column within H of the own interior: the
 // T-step dependence cone).
-#define PT_REGION_INIT(NW_)                                                                         \
-    constexpr int R = TB_R, RH = (NW_) * TB_R, H = 2 * T, IW = 64 - 2 * H, IH = RH - 2 * H;        \
+#define PT_REGION_INIT(NW_, RW_)                                                                    \
+    constexpr int R = (RW_), RP = (RW_) / 2, RH = (NW_) * (RW_), H = 2 * T, IW = 64 - 2 * H,       \
+                  IH = RH - 2 * H;                                                                  \
     const int lane = threadIdx.x & 63;                                                              \
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                \
     const PtTile ti = pt_assign(g, a.status, a.xcd_mode);                                           \
@@ -912,65 +935,106 @@ struct FwdPtArgs {
 // operation order per row).  With this pairing the vertical neighbours of pair i are pairs i-1 /
 // i+1 / i-2 / i+2 except at the slab ends, where four pairs are assembled from the halo rows.  The
 // horizontal taps stay per-row DPP lane shifts (DPP has no packed form).
+// Schedule: the step's boundary rows go to LDS, the barrier, the halo reads are issued, and then
+// the work that needs no halo row — every DPP shift, the time terms temp1 P_n - temp2 P_{n-1}, the
+// first vertical sums of the two inner pairs — runs while the reads are in flight
+// (sched_barrier pins the order; the values and their operation order are unchanged: bit-exact).
 #define FWD_STEP(CUR, PRV)                                                                          \
     {                                                                                               \
-        const Halo4 h4 = exchange_nw<NW>(xch, n & 1, w, lane, CUR[0].x, CUR[1].x, CUR[2].y, CUR[3].y); \
-        const f32x2 eU1 = {h4.u1, CUR[3].x}, eU2 = {h4.u2, CUR[2].x};  /* rows (-1,3), (-2,2) */    \
-        const f32x2 eD1 = {CUR[0].y, h4.d1}, eD2 = {CUR[1].y, h4.d2};  /* rows (4,8), (5,9)   */    \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
-            const f32x2 m1 = i >= 1 ? CUR[i - 1] : eU1;                                             \
-            const f32x2 p1 = i <= 2 ? CUR[i + 1] : eD1;                                             \
-            const f32x2 m2 = i >= 2 ? CUR[i - 2] : (i == 1 ? eU1 : eU2);                            \
-            const f32x2 p2 = i <= 1 ? CUR[i + 2] : (i == 2 ? eD1 : eD2);                            \
+        xch_put<NW>(xch, n & 1, w, lane, CUR[0].x, CUR[1].x, CUR[RP - 2].y, CUR[RP - 1].y);                   \
+        __syncthreads();                                                                            \
+        const Halo4 h4 = xch_get<NW>(xch, n & 1, w, lane);                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        f32x2 xl1[RP], xr1[RP], tt[RP], la[RP];                                                         \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             const f32x2 c = CUR[i];                                                                 \
-            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
-            f32x2 s1 = m1 + p1; s1 = s1 + xl1; s1 = s1 + xr1;                                       \
-            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
-            s2.x = s2.x + dpp_shr1(xl1.x); s2.y = s2.y + dpp_shr1(xl1.y);                           \
-            s2.x = s2.x + dpp_shl1(xr1.x); s2.y = s2.y + dpp_shl1(xr1.y);                           \
-            f32x2 lap = kC2 * s1; const f32x2 l2 = kC3 * s2; lap = lap + l2;                        \
+            xl1[i] = f32x2{dpp_shr1(c.x), dpp_shr1(c.y)};                                           \
+            xr1[i] = f32x2{dpp_shl1(c.x), dpp_shl1(c.y)};                                           \
             f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
+            tt[i] = a1;                                                                             \
+        }                                                                                           \
+        _Pragma("unroll") for (int i = 1; i < RP - 1; ++i) {  /* inner pairs: no halo row in s1 */   \
+            f32x2 s1 = CUR[i - 1] + CUR[i + 1]; s1 = s1 + xl1[i]; s1 = s1 + xr1[i];                 \
+            la[i] = kC2 * s1;                                                                       \
+        }                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        const f32x2 eU1 = {h4.u1, CUR[RP - 1].x}, eU2 = {h4.u2, CUR[RP - 2].x};  /* rows (-1,RP-1), (-2,RP-2) */ \
+        const f32x2 eD1 = {CUR[0].y, h4.d1}, eD2 = {CUR[1].y, h4.d2};  /* rows (RP,R), (RP+1,R+1) */ \
+        _Pragma("unroll") for (int i = 0; i < RP; i += RP - 1) {                                          \
+            const f32x2 m1 = i >= 1 ? CUR[i - 1] : eU1;                                             \
+            const f32x2 p1 = i <= RP - 2 ? CUR[i + 1] : eD1;                                        \
+            f32x2 s1 = m1 + p1; s1 = s1 + xl1[i]; s1 = s1 + xr1[i];                                 \
+            la[i] = kC2 * s1;                                                                       \
+        }                                                                                           \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
+            const f32x2 m2 = i >= 2 ? CUR[i - 2] : (i == 1 ? eU1 : eU2);                            \
+            const f32x2 p2 = i <= RP - 3 ? CUR[i + 2] : (i == RP - 2 ? eD1 : eD2);                  \
+            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            s2.x = s2.x + dpp_shr1(xl1[i].x); s2.y = s2.y + dpp_shr1(xl1[i].y);                     \
+            s2.x = s2.x + dpp_shl1(xr1[i].x); s2.y = s2.y + dpp_shl1(xr1[i].y);                     \
+            const f32x2 l2 = kC3 * s2; const f32x2 lap = la[i] + l2;                                \
             const f32x2 a3 = A[i] * lap;                                                            \
-            PRV[i] = a1 + a3;                                                                       \
+            PRV[i] = tt[i] + a3;                                                                    \
         }                                                                                           \
         if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
-            unsigned sm_ = smask;                                                                   \
-            LAUNDER(sm_);                                                                           \
             /* x + (-0) == x bit for bit: the other lanes add -0 instead of branching */            \
             const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if ((sm_ >> r) & 1u) PT_AT(PRV, r) = PT_AT(PRV, r) + add;                                         \
+            if (s1row) {                             /* one source row: one packed add on its pair */ \
+                const f32x2 av = shalf ? f32x2{-0.0f, add} : f32x2{add, -0.0f};                     \
+                int sp_ = spair;                                                                    \
+                LAUNDER(sp_);                                                                       \
+                _Pragma("unroll") for (int i = 0; i < RP; ++i)                                       \
+                    if (i == sp_) PRV[i] = PRV[i] + av;                                             \
+            } else {                                                                                \
+                unsigned sm_ = smask;                                                               \
+                LAUNDER(sm_);                                                                       \
+                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
+                    if ((sm_ >> r) & 1u) PT_AT(PRV, r) = PT_AT(PRV, r) + add;                       \
+            }                                                                                       \
         }                                                                                           \
-        if (a.hist) {                       /* own cells only; issued at once (the faster of the     \
-                                               store placements measured: tools/exp_variants.sh) */ \
-            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(n + 2) * L + so, slice_bytes); \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(PRV, r)), HR, hv[r], 0, CP_NT); \
+        /* history: own cells, issued at once; the epoch's last step is stored after the hand-off   \
+           sweep (FWD_HIST_LAST): on gfx9 vmcnt counts stores, so the sweep's granule loads would   \
+           otherwise wait for them */                                                               \
+        if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
+        if (rrow >= 0) {                             /* receiver row: value kept, stored per epoch */ \
+            int rp_ = rpair;                                                                        \
+            LAUNDER(rp_);                                                                           \
+            f32x2 v_ = PRV[0];                                                                      \
+            _Pragma("unroll") for (int i = 1; i < RP; ++i) if (i == rp_) v_ = PRV[i];                \
+            rv[t] = rhalf ? v_.y : v_.x;                                                            \
         }                                                                                           \
-        if (rrow >= 0 && rec_index(n, g.st) >= 0) {                                                 \
-            float *SK = a.seis + ((size_t)bs * g.nrec + rec_index(n, g.st)) * g.ng;                 \
-            int rr_ = rrow;                                                                         \
-            LAUNDER(rr_);                                                                           \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if (r == rr_ && rec) SK[rcv0] = PT_AT(PRV, r);                                             \
-            if (rmulti) {                                /* several receivers in one column */      \
-                float v_ = 0.0f;                                                                    \
-                _Pragma("unroll") for (int r = 0; r < R; ++r) if (r == rr_) v_ = PT_AT(PRV, r);            \
-                for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = v_;                           \
+    }
+#define FWD_HIST(V, N)                                                                              \
+    {                                                                                               \
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)((N) + 2) * L + so, slice_bytes); \
+        _Pragma("unroll") for (int r = 0; r < R; ++r)                                               \
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(V, r)), HR, hv[r], 0, CP_NT); \
+    }
+// the receiver row's values of the epoch's steps n0 .. n0+T-1 (after the hand-off sweep)
+#define FWD_RECORD                                                                                  \
+    if (rrow >= 0) {                                                                                \
+        _Pragma("unroll") for (int t = 0; t < T; ++t) {                                             \
+            const int n = n0 + t;                                                                   \
+            const int ri_ = n < a.nt ? rec_index(n, g.st) : -1;                                     \
+            if (ri_ >= 0) {                                                                         \
+                float *SK = a.seis + ((size_t)bs * g.nrec + ri_) * g.ng;                            \
+                if (rec) SK[rcv0] = rv[t];                                                          \
+                if (rmulti && rec)                           /* several receivers in one column */  \
+                    for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = rv[t];                    \
             }                                                                                       \
         }                                                                                           \
     }
 
-#define PT_AT(V, r) V[(r) & 3][(r) >> 2]       // row r of a row-pair array
-template <int T, int NW, bool PROF>
+#define PT_AT(V, r) V[(r) % RP][(r) / RP]     // row r of a row-pair array: pair r mod RP, half r / RP
+template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     __shared__ float xch[2][NW][4][64];
     const TBGeo &g = a.g;
-    PT_REGION_INIT(NW)
+    PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[4], C1[4], C2v[4], P0[4], P1[4];              // row pairs {r, r+4}: PT_AT(X, r)
+    f32x2 A[RP], C1[RP], C2v[RP], P0[RP], P1[RP];         // row pairs {r, r+RP}: PT_AT(X, r)
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
     unsigned smask = 0;
     int rrow = -1;
@@ -994,6 +1058,14 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
     const bool rec = rrow >= 0 && xin && rcv0 >= 0;
     const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
+    // source / receiver rows as (row pair, half): the step touches one pair, not all eight rows
+    const bool s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
+    const int sr1 = smask ? __builtin_ctz(smask) : 0;
+    const int spair = sr1 % RP, rpair = rrow >= 0 ? (rrow % RP) : 0;
+    const bool shalf = sr1 >= RP, rhalf = rrow >= RP;
+    float rv[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) rv[t] = 0.0f;
     const size_t L = g.level;
     const int slice_bytes = (int)(g.slice * 4);
     int hv[R];                                            // history store offset of (row, lane), OOB if not own
@@ -1022,7 +1094,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         }
         if (T & 1) {   // keep "P1 = newest" at every epoch boundary
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const f32x2 tmp = P0[i]; P0[i] = P1[i]; P1[i] = tmp; }
+            for (int i = 0; i < RP; ++i) { const f32x2 tmp = P0[i]; P0[i] = P1[i]; P1[i] = tmp; }
         }
         PT_PROF(tst)
         if (e + 1 < nep) {
@@ -1031,10 +1103,15 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             PT_PUBLISH(GR, tag, P0, P1)
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, P0, P1, R)
+            if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
+                                                          // reloads halo cells only)
             FWD_ISSUE
         }
+        FWD_RECORD
     }
 #undef FWD_ISSUE
+#undef FWD_HIST
+#undef FWD_RECORD
     PT_PROF(tsw)
     if (prof && lane == 0) {
         atomicAdd(prof + 0, tsw); atomicAdd(prof + 1, tst); atomicAdd(prof + 2, tpb); atomicAdd(prof + 3, 1ull);
@@ -1046,7 +1123,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
 }
 #undef FWD_STEP
-// The adjoint keeps the forward's row-pair packing (PT_AT(V, r) = V[r & 3][r >> 2]): every add /
+// The adjoint keeps the forward's row-pair packing (PT_AT(V, r) = V[r % RP][r / RP]): every add /
 // mul / fma of the step and of the gradient is one v_pk_*_f32 for two rows.
 
 struct AdjPtArgs {
@@ -1077,7 +1154,7 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
 #define ADJ_PLOAD(PC, PH, HR, SOFF)                                                                 \
     {                                                                                               \
         const int so_ = (SOFF);                                                                     \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PC[i].x = bload_nt(HR, pv[i + 2], so_);                                                 \
             PC[i].y = bload_nt(HR, pv[i + 6], so_);                                                 \
         }                                                                                           \
@@ -1086,12 +1163,12 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
     }
 
 // vertical neighbours of row pair i in a row-pair field X whose four outer rows are in
-// eU1 = {-1, 3}, eU2 = {-2, 2}, eD1 = {4, 8}, eD2 = {5, 9}
+// eU1 = {-1, RP-1}, eU2 = {-2, RP-2}, eD1 = {RP, R}, eD2 = {RP+1, R+1}
 #define PAIR_VERT(X, i, m1, p1, m2, p2)                                                             \
     const f32x2 m1 = (i) >= 1 ? X[(i) - 1] : eU1;                                                   \
-    const f32x2 p1 = (i) <= 2 ? X[(i) + 1] : eD1;                                                   \
+    const f32x2 p1 = (i) <= RP - 2 ? X[(i) + 1] : eD1;                                              \
     const f32x2 m2 = (i) >= 2 ? X[(i) - 2] : ((i) == 1 ? eU1 : eU2);                                \
-    const f32x2 p2 = (i) <= 1 ? X[(i) + 2] : ((i) == 2 ? eD1 : eD2);
+    const f32x2 p2 = (i) <= RP - 3 ? X[(i) + 2] : ((i) == RP - 2 ? eD1 : eD2);
 
 // gradient accumulation of one step (interior rows are the ones stored; every row of a wave that
 // has interior rows is computed: no per-row branch).  CU = L_{k+1}, LN = L_k, P / PH = P_{k-1}.
@@ -1099,9 +1176,9 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
 //   gbeta[s] += L_k(src) w[k-1]
 #define ADJ_GRAD(CU, LN, P, PH, WK)                                                                 \
     if (grad) {                                                                                     \
-        const f32x2 eU1 = {PH[1], P[3].x}, eU2 = {PH[0], P[2].x};                                   \
+        const f32x2 eU1 = {PH[1], P[RP - 1].x}, eU2 = {PH[0], P[RP - 2].x};                         \
         const f32x2 eD1 = {P[0].y, PH[2]}, eD2 = {P[1].y, PH[3]};                                   \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PAIR_VERT(P, i, m1, p1, m2, p2)                                                         \
             const f32x2 c = P[i];                                                                   \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
@@ -1117,7 +1194,7 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
             f32x2 kk = KP[i] * c; const f32x2 dl = CU[i] - l; kk = kk * dl;   /* fp32 term */       \
             if (xin) {                                                       /* fp64 sum */        \
                 if ((rin >> i) & 1u) ksum += (double)kk.x;                                          \
-                if ((rin >> (i + 4)) & 1u) ksum += (double)kk.y;                                    \
+                if ((rin >> (i + RP)) & 1u) ksum += (double)kk.y;                                   \
             }                                                                                       \
         }                                                                                           \
         if (srow >= 0) {                             /* gbeta: the source cell's lane only */      \
@@ -1137,12 +1214,12 @@ __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __buil
     {                                                                                               \
         if (t + 1 < T) ADJ_PLOAD(PN, PHN, HRe, (T - 2 - t) * L4)                                    \
         const float dcur = dv[t];                                                                   \
-        f32x2 q[4];                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) q[i] = A[i] * CUR[i];                         \
-        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[2].y, q[3].y);      \
-        const f32x2 eU1 = {h4.u1, q[3].x}, eU2 = {h4.u2, q[2].x};                                   \
+        f32x2 q[RP];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[RP - 2].y, q[RP - 1].y); \
+        const f32x2 eU1 = {h4.u1, q[RP - 1].x}, eU2 = {h4.u2, q[RP - 2].x};                         \
         const f32x2 eD1 = {q[0].y, h4.d1}, eD2 = {q[1].y, h4.d2};                                   \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PAIR_VERT(q, i, m1, p1, m2, p2)                                                         \
             const f32x2 c = q[i];                                                                   \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
@@ -1180,9 +1257,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     __shared__ float xch[2][NW][4][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
-    PT_REGION_INIT(NW)
+    PT_REGION_INIT(NW, TB_R)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[4], T1v[4], T2v[4], KP[4], L0[4], L1[4], GA[4];
+    f32x2 A[RP], T1v[RP], T2v[RP], KP[RP], L0[RP], L1[RP], GA[RP];
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2};
     int srow = -1, rrow = -1;
 #pragma unroll
@@ -1215,7 +1292,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     float gbacc = 0.0f;
     const size_t L = g.level;
     const int L4 = (int)(L * 4);                          // bytes per history slot (< 2 GB: resident surveys)
-    f32x2 PA[4], PB[4];
+    f32x2 PA[RP], PB[RP];
     float PHA[4], PHB[4];
     int pv[12];                                           // P row (uz0 - 2 + i) offset of this lane
 #pragma unroll
@@ -1265,7 +1342,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         }
         if (T & 1) {   // keep "L1 = newest, PB = the last step's P, PA = free" at every epoch boundary
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < RP; ++i) {
                 const f32x2 tl = L0[i]; L0[i] = L1[i]; L1[i] = tl;
                 const f32x2 tp = PA[i]; PA[i] = PB[i]; PB[i] = tp;
                 const float th = PHA[i]; PHA[i] = PHB[i]; PHB[i] = th;
@@ -1325,50 +1402,70 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 #define ADJR_LOAD(PD, HR, SOFF)                                                                     \
     {                                                                                               \
         const int so_ = (SOFF);                                                                     \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PD[i].x = bload_nt(HR, pr[i], so_);                                                     \
-            PD[i].y = bload_nt(HR, pr[i + 4], so_);                                                 \
+            PD[i].y = bload_nt(HR, pr[i + RP], so_);                                                \
         }                                                                                           \
     }
 
 // gradient of step k (CU = L_{k+1}, LN = L_k; wavelet sample WK = w[k-1]; window P0 = P_k,
-// P1 = P_{k-1}, P2 = P_{k-2})
-#define ADJR_GRAD(CU, LN, WK, P0, P1, P2)                                                           \
-    if (grad) {                                                                                     \
-        f32x2 u[4];                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+// P1 = P_{k-1}, P2 = P_{k-2}), in two halves: PRE forms d = 2c1 P_{k-1} + lap'(P_{k-1}) from the
+// history alone (no L, no neighbour data: it runs while the step's halo reads are in flight),
+// POST accumulates with L_k.
+#define ADJR_GRAD_PRE(WK, P0, P1, P2)                                                               \
+    {                                                                                               \
+        f32x2 u[RP];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             u[i] = fma2(-T1v[i], P1[i], P0[i]);                                                     \
             u[i] = fma2(T2v[i], P2[i], u[i]);                                                       \
         }                                                                                           \
         if (srow >= 0) {                             /* the forward's source add, undone */        \
-            int sr_ = srow;                                                                         \
-            LAUNDER(sr_);                                                                           \
+            int sp_ = spair;                                                                        \
+            LAUNDER(sp_);                                                                           \
             const float sa_ = scol ? bsrc * (WK) : 0.0f;                                            \
-            float ls_ = 0.0f;                                                                       \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if (r == sr_) { PT_AT(u, r) = PT_AT(u, r) - sa_; ls_ = PT_AT(LN, r); }              \
+            const f32x2 sv_ = shalf ? f32x2{0.0f, sa_} : f32x2{sa_, 0.0f};                          \
+            _Pragma("unroll") for (int i = 0; i < RP; ++i) if (i == sp_) u[i] = u[i] - sv_;          \
+        }                                                                                           \
+        /* A d = A 2c1 P_{k-1} + u: the 1/A is applied once to the sum (gA = sum L A d / A) */     \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) dd[i] = fma2(A[i], kC1X2 * P1[i], u[i]);      \
+    }
+#define ADJR_GRAD_POST(CU, LN, WK, P1)                                                              \
+    {                                                                                               \
+        if (srow >= 0) {                                                                            \
+            int sp_ = spair;                                                                        \
+            LAUNDER(sp_);                                                                           \
+            f32x2 lp_ = LN[0];                                                                      \
+            _Pragma("unroll") for (int i = 1; i < RP; ++i) if (i == sp_) lp_ = LN[i];                \
+            const float ls_ = shalf ? lp_.y : lp_.x;                                                \
             const float gb = scol ? ls_ * (WK) : -0.0f;                                             \
             gbacc = gbacc + gb;                                                                     \
         }                                                                                           \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
-            const f32x2 d = fma2(kC1X2, P1[i], u[i] * rA[i]);                                       \
-            GA[i] = fma2(LN[i], d, GA[i]);                                                          \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
+            GA[i] = fma2(LN[i], dd[i], GA[i]);                                                      \
             GK[i] = fma2(P1[i], CU[i] - LN[i], GK[i]);                                              \
         }                                                                                           \
     }
+#define ADJR_GRAD(CU, LN, WK, P0, P1, P2)                                                           \
+    if (grad) {                                                                                     \
+        f32x2 dd[RP];                                                                               \
+        ADJR_GRAD_PRE(WK, P0, P1, P2)                                                               \
+        ADJR_GRAD_POST(CU, LN, WK, P1)                                                              \
+    }
 
 // one adjoint step k: CUR = L_{k+1}, PRV = L_{k+2} -> L_k; window P0 / P1 / P2 as ADJR_GRAD;
-// history slot k-2 (the next step's P_{k-3}) prefetched into PN
+// history slot k-2 (the next step's P_{k-3}) prefetched into PN.  (Moving the gradient's history
+// half between the barrier and the halo reads' use, as FWD_STEP does with its halo-free work,
+// needs 8 more VGPRs than the 168 that 3 waves / SIMD allow: it spilled and ran 2.6x slower.)
 #define ADJR_STEP(CUR, PRV, P0, P1, P2, PN)                                                         \
     {                                                                                               \
         if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
         const float dcur = dv[t];                                                                   \
-        f32x2 q[4];                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) q[i] = A[i] * CUR[i];                         \
-        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[2].y, q[3].y);      \
-        const f32x2 eU1 = {h4.u1, q[3].x}, eU2 = {h4.u2, q[2].x};                                   \
+        f32x2 q[RP];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = exchange_nw<NW>(xch, j & 1, w, lane, q[0].x, q[1].x, q[RP - 2].y, q[RP - 1].y); \
+        const f32x2 eU1 = {h4.u1, q[RP - 1].x}, eU2 = {h4.u2, q[RP - 2].x};                         \
         const f32x2 eD1 = {q[0].y, h4.d1}, eD2 = {q[1].y, h4.d2};                                   \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PAIR_VERT(q, i, m1, p1, m2, p2)                                                         \
             const f32x2 c = q[i];                                                                   \
             const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
@@ -1380,24 +1477,24 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
         }                                                                                           \
         if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
-            int rr_ = rrow;                                                                         \
-            LAUNDER(rr_);                                                                           \
-            _Pragma("unroll") for (int r = 0; r < R; ++r)                                           \
-                if (r == rr_) PT_AT(PRV, r) = PT_AT(PRV, r) + dcur;   /* -0 off the receivers */     \
+            int rp_ = rpair;                                 /* one packed add on the row's pair */  \
+            LAUNDER(rp_);                                                                           \
+            const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
+            _Pragma("unroll") for (int i = 0; i < RP; ++i) if (i == rp_) PRV[i] = PRV[i] + dv_;      \
         }                                                                                           \
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
     }
 
-template <int T, int NW, bool PROF>
+template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     __shared__ float xch[2][NW][4][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
-    PT_REGION_INIT(NW)
+    PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[4], rA[4], T1v[4], T2v[4], L0[4], L1[4], GA[4], GK[4];
+    f32x2 A[RP], T1v[RP], T2v[RP], L0[RP], L1[RP], GA[RP], GK[RP];   // GA accumulates A x the gradient
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2};
     int srow = -1, rrow = -1;
 #pragma unroll
@@ -1405,7 +1502,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
         const int gz = wrap_row(uz0 + r, g.Hp);
         const int o = gz * g.ld + gx;
         PT_AT(A, r) = AL[o]; PT_AT(T1v, r) = AL[g.cstride + o]; PT_AT(T2v, r) = AL[2 * g.cstride + o];
-        PT_AT(rA, r) = 1.0f / PT_AT(A, r);
         PT_AT(L0, r) = 0.0f; PT_AT(L1, r) = 0.0f;         // L_{nt+1} = L_{nt+2} = 0
         PT_AT(GA, r) = 0.0f; PT_AT(GK, r) = 0.0f;
         if (gz == g.isz && ((rin >> r) & 1u)) srow = r;
@@ -1417,6 +1513,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     const int rcv0 = rrow >= 0 ? g.rlane[gx] : -1;
     const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
+    // source / receiver rows as (row pair, half): a step touches one pair, not all eight rows
+    const int spair = srow >= 0 ? (srow % RP) : 0, rpair = rrow >= 0 ? (rrow % RP) : 0;
+    const bool shalf = srow >= RP, rhalf = rrow >= RP;
 #define DLOAD(KK)                                                                                   \
     ({                                                                                              \
         const int ri_ = (KK) >= 1 ? rec_index((KK) - 1, g.st) : -1;                                 \
@@ -1428,12 +1527,12 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     float gbacc = 0.0f;
     const size_t L = g.level;
     const int L4 = (int)(L * 4);                          // bytes per history slot (< 2 GB: resident surveys)
-    f32x2 Q0[4], Q1[4], Q2[4], Q3[4];
-    int pr[8];                                            // history offset of (own row r, lane)
+    f32x2 Q0[RP], Q1[RP], Q2[RP], Q3[RP];
+    int pr[R];                                            // history offset of (own row r, lane)
 #pragma unroll
     for (int r = 0; r < R; ++r) pr[r] = grad ? (PT_ROFS(r) + gx) * 4 : OOB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { Q0[i] = 0.0f; Q1[i] = 0.0f; Q2[i] = 0.0f; Q3[i] = 0.0f; }
+    for (int i = 0; i < RP; ++i) { Q0[i] = 0.0f; Q1[i] = 0.0f; Q2[i] = 0.0f; Q3[i] = 0.0f; }
     // history descriptor of the epoch whose first step is KN: its prefetches read slots
     // KN - 2 .. KN - T - 1, step t at byte offset (T - 1 - t) * L4
 #define HIST_RSRC(KN) rsrc_of(a.hist + (ptrdiff_t)((KN) - T - 1) * (ptrdiff_t)L + (ptrdiff_t)so)
@@ -1475,7 +1574,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
         }
         if (T & 1) {   // keep "L1 = newest" at every epoch boundary
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { const f32x2 tl = L0[i]; L0[i] = L1[i]; L1[i] = tl; }
+            for (int i = 0; i < RP; ++i) { const f32x2 tl = L0[i]; L0[i] = L1[i]; L1[i] = tl; }
         }
         // the last step's window (step T - 1: Q[T-1], Q[T], Q[T+1] mod 4), for the deferred gradient
 #define QW(o) (((T - 1 + (o)) & 3) == 0 ? Q0 : ((T - 1 + (o)) & 3) == 1 ? Q1 : ((T - 1 + (o)) & 3) == 2 ? Q2 : Q3)
@@ -1493,7 +1592,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
         }
         if constexpr ((T & 3) != 0) {   // restore Q0 = the next epoch's P_k
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < RP; ++i) {
                 const f32x2 a0 = QW(1)[i], a1 = QW(2)[i], a2 = QW(3)[i], a3 = QW(4)[i];
                 Q0[i] = a0; Q1[i] = a1; Q2[i] = a2; Q3[i] = a3;
             }
@@ -1516,7 +1615,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if ((rin >> r) & 1u) {
-                a.gA[so + (size_t)PT_ROFS(r) + gx] = PT_AT(GA, r);
+                a.gA[so + (size_t)PT_ROFS(r) + gx] = PT_AT(GA, r) / PT_AT(A, r);
                 const float kp = AL[3 * g.cstride + PT_ROFS(r) + gx];
                 ksum += (double)kp * (double)PT_AT(GK, r);
             }
@@ -1534,6 +1633,8 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 }
 #undef ADJR_STEP
 #undef ADJR_GRAD
+#undef ADJR_GRAD_PRE
+#undef ADJR_GRAD_POST
 #undef ADJR_LOAD
 #undef ADJ_STEP
 #undef ADJ_GRAD
@@ -1871,9 +1972,11 @@ struct rdq_fwi_plan {
     int persist = 1;            // 0 off, 1 auto, 8 / 12: persistent kernels with that region height (waves),
                                 // -1: persistent launches oversubscribed 2x past residency (fault-path test)
     int xcd_mode = 1;           // persistent kernels: XCD-local slices with L2 hand-offs (pt_assign)
-    int cap_fwd8[TB_MAXT + 1] = {0}, cap_adj8[TB_MAXT + 1] = {0};     // resident workgroups (0 = unknown)
-    int cap_fwd12[TB_MAXT + 1] = {0}, cap_adj12[TB_MAXT + 1] = {0};
-    int cap_adjf8[TB_MAXT + 1] = {0}, cap_adjf12[TB_MAXT + 1] = {0};
+    // resident workgroups (0 = unknown) per kernel variant [variant][T]: 0 fwd 64-row, 1..3 fwd 96-row
+    // with 8 / 12 / 24 rows per wave, 4 exact adjoint 64-row, 5 exact 96-row, 6 FMA adjoint 64-row,
+    // 7..8 FMA adjoint 96-row with 8 / 12 rows per wave
+    int capw[11][TB_MAXT + 1] = {};   // [9] fwd 96-row x 6 rows per wave, [10] FMA adjoint 96-row x 6
+    int fwd_rw = 6, adj_rw = 8;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
@@ -2004,16 +2107,35 @@ int resident_capacity(K kernel, int nthreads, int &cache)
     return cache;
 }
 
-template <int NW>
-int capacity_nw(rdq_fwi_plan *p, bool adj, int T)
+// Resident capacity of the persistent kernel a call would launch (occupancy query x CUs).  `NW` is
+// the region-height class (region rows = NW x 8: 64 or 96); the 96-row kernels run 8, 12 or 24 rows
+// per wave (12, 8 or 4 waves per workgroup).  The adjoint's launch must fit both adjoint variants.
+template <int T>
+int capacity_T(rdq_fwi_plan *p, int NW, bool adj)
 {
-    int *c = adj ? (NW == 12 ? p->cap_adj12 : p->cap_adj8) : (NW == 12 ? p->cap_fwd12 : p->cap_fwd8);
-    int *cf = NW == 12 ? p->cap_adjf12 : p->cap_adjf8;   // both adjoint variants: the launch must fit either
+    auto *c = p->capw;
+    if (!adj) {
+        if (NW != 12) return resident_capacity(k_fwd_pt<T, 8, 8, false>, 512, c[0][T]);
+        if (p->fwd_rw == 24) return resident_capacity(k_fwd_pt<T, 4, 24, false>, 256, c[3][T]);
+        if (p->fwd_rw == 6) return resident_capacity(k_fwd_pt<T, 16, 6, false>, 1024, c[9][T]);
+        if (p->fwd_rw == 12) return resident_capacity(k_fwd_pt<T, 8, 12, false>, 512, c[2][T]);
+        return resident_capacity(k_fwd_pt<T, 12, 8, false>, 768, c[1][T]);
+    }
+    if (NW != 12)
+        return std::min(resident_capacity(k_adj_pt<T, 8, false>, 512, c[4][T]),
+                        resident_capacity(k_adj_pr<T, 8, 8, false>, 512, c[6][T]));
+    const int ex = resident_capacity(k_adj_pt<T, 12, false>, 768, c[5][T]);
+    if (p->adj_rw == 12) return std::min(ex, resident_capacity(k_adj_pr<T, 8, 12, false>, 512, c[8][T]));
+    if (p->adj_rw == 6) return std::min(ex, resident_capacity(k_adj_pr<T, 16, 6, false>, 1024, c[10][T]));
+    return std::min(ex, resident_capacity(k_adj_pr<T, 12, 8, false>, 768, c[7][T]));
+}
+int capacity_nw(rdq_fwi_plan *p, int NW, bool adj, int T)
+{
     switch (T) {
-    case 1: return adj ? std::min(resident_capacity(k_adj_pt<1, NW, false>, 64 * NW, c[1]), resident_capacity(k_adj_pr<1, NW, false>, 64 * NW, cf[1])) : resident_capacity(k_fwd_pt<1, NW, false>, 64 * NW, c[1]);
-    case 2: return adj ? std::min(resident_capacity(k_adj_pt<2, NW, false>, 64 * NW, c[2]), resident_capacity(k_adj_pr<2, NW, false>, 64 * NW, cf[2])) : resident_capacity(k_fwd_pt<2, NW, false>, 64 * NW, c[2]);
-    case 3: return adj ? std::min(resident_capacity(k_adj_pt<3, NW, false>, 64 * NW, c[3]), resident_capacity(k_adj_pr<3, NW, false>, 64 * NW, cf[3])) : resident_capacity(k_fwd_pt<3, NW, false>, 64 * NW, c[3]);
-    default: return adj ? std::min(resident_capacity(k_adj_pt<4, NW, false>, 64 * NW, c[4]), resident_capacity(k_adj_pr<4, NW, false>, 64 * NW, cf[4])) : resident_capacity(k_fwd_pt<4, NW, false>, 64 * NW, c[4]);
+    case 1: return capacity_T<1>(p, NW, adj);
+    case 2: return capacity_T<2>(p, NW, adj);
+    case 3: return capacity_T<3>(p, NW, adj);
+    default: return capacity_T<4>(p, NW, adj);
     }
 }
 
@@ -2050,13 +2172,11 @@ unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
         const int ih = NW * TB_R - 4 * T;
         const unsigned Tt = (unsigned)(tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih));
         const unsigned want = 8u * Tt * ((S + 7u) / 8u);
-        const int cap = NW == 12 ? capacity_nw<12>(const_cast<rdq_fwi_plan *>(p), adj, T)
-                                 : capacity_nw<8>(const_cast<rdq_fwi_plan *>(p), adj, T);
+        const int cap = capacity_nw(const_cast<rdq_fwi_plan *>(p), NW, adj, T);
         if (want > grid && (int)want <= cap) grid = want;
     }
     if (p->persist == -1) {   // fault-path test: a grid the device cannot hold resident at once
-        const int cap = NW == 12 ? capacity_nw<12>(const_cast<rdq_fwi_plan *>(p), adj, T)
-                                 : capacity_nw<8>(const_cast<rdq_fwi_plan *>(p), adj, T);
+        const int cap = capacity_nw(const_cast<rdq_fwi_plan *>(p), NW, adj, T);
         grid = std::max(grid, 2u * (unsigned)std::max(cap, 1));
     }
     return grid;
@@ -2071,46 +2191,58 @@ int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
     const int T = adj ? p->adj_T : p->fwd_T;
     const int want = p->persist == -1 ? 1 : p->persist;   // 1 = auto, 8 / 12 = forced
     if (want == 1 || want == 12) {
-        const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw<12>(p, adj, T));
+        const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw(p, 12, adj, T));
         if (k > 0) { if (per) *per = k; return 12; }
     }
     if (want == 1 || want == 8) {
-        const int k = pt_shots_per_launch(p, B, T, 8, capacity_nw<8>(p, adj, T));
+        const int k = pt_shots_per_launch(p, B, T, 8, capacity_nw(p, 8, adj, T));
         if (k > 0) { if (per) *per = k; return 8; }
     }
     return 0;
 }
 
-template <int NW>
-void launch_fwd_pt(int T, dim3 grid, hipStream_t st, const FwdPtArgs &a)
+// the persistent forward of region class NW (64 / 96 rows) with the plan's rows per wave
+template <int T, bool PROF>
+void launch_fwd_pt_T(const rdq_fwi_plan *p, int NW, dim3 grid, hipStream_t st, const FwdPtArgs &a)
 {
-    const dim3 blk(64 * NW);
-    if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW, true>), grid, blk, 0, st, a);
-        return;
-    }
+    if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
+    else if (p->fwd_rw == 24) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 4, 24, PROF>), grid, dim3(256), 0, st, a);
+    else if (p->fwd_rw == 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 8, 12, PROF>), grid, dim3(512), 0, st, a);
+    else if (p->fwd_rw == 6) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 16, 6, PROF>), grid, dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 12, 8, PROF>), grid, dim3(768), 0, st, a);
+}
+void launch_fwd_pt(const rdq_fwi_plan *p, int NW, int T, dim3 grid, hipStream_t st, const FwdPtArgs &a)
+{
+    if (a.prof && T == 4) { launch_fwd_pt_T<4, true>(p, NW, grid, st, a); return; }   // phase-profiled build
     switch (T) {
-    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<1, NW, false>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<2, NW, false>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<3, NW, false>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<4, NW, false>), grid, blk, 0, st, a); break;
+    case 1: launch_fwd_pt_T<1, false>(p, NW, grid, st, a); break;
+    case 2: launch_fwd_pt_T<2, false>(p, NW, grid, st, a); break;
+    case 3: launch_fwd_pt_T<3, false>(p, NW, grid, st, a); break;
+    default: launch_fwd_pt_T<4, false>(p, NW, grid, st, a); break;
     }
 }
 
-template <int NW, bool F>
-void launch_adj_pt(int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
+// the persistent adjoint: FMA / recurrence build (k_adj_pr, the plan's rows per wave for 96-row
+// regions) or the oracle's exact operation order (k_adj_pt, 8 rows per wave)
+template <int T, bool PROF>
+void launch_adj_pt_T(const rdq_fwi_plan *p, int NW, dim3 grid, hipStream_t st, const AdjPtArgs &a)
 {
-    const dim3 blk(64 * NW);
-    if (a.prof && T == 4) {   // phase-profiled build (rdq_fwi_set_profile; depth 4 only)
-        if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, true>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, true>), grid, blk, 0, st, a);
-        return;
-    }
+    if (!p->adj_fma) {
+        if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<T, 8, PROF>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<T, 12, PROF>), grid, dim3(768), 0, st, a);
+    } else if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
+    else if (p->adj_rw == 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 8, 12, PROF>), grid, dim3(512), 0, st, a);
+    else if (p->adj_rw == 6) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 16, 6, PROF>), grid, dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 12, 8, PROF>), grid, dim3(768), 0, st, a);
+}
+void launch_adj_pt(const rdq_fwi_plan *p, int NW, int T, dim3 grid, hipStream_t st, const AdjPtArgs &a)
+{
+    if (a.prof && T == 4) { launch_adj_pt_T<4, true>(p, NW, grid, st, a); return; }   // phase-profiled build
     switch (T) {
-    case 1: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<1, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<1, NW, false>), grid, blk, 0, st, a); break;
-    case 2: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<2, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<2, NW, false>), grid, blk, 0, st, a); break;
-    case 3: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<3, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<3, NW, false>), grid, blk, 0, st, a); break;
-    default: if constexpr (F) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<4, NW, false>), grid, blk, 0, st, a); else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<4, NW, false>), grid, blk, 0, st, a); break;
+    case 1: launch_adj_pt_T<1, false>(p, NW, grid, st, a); break;
+    case 2: launch_adj_pt_T<2, false>(p, NW, grid, st, a); break;
+    case 3: launch_adj_pt_T<3, false>(p, NW, grid, st, a); break;
+    default: launch_adj_pt_T<4, false>(p, NW, grid, st, a); break;
     }
 }
 
@@ -2178,8 +2310,7 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
         a.g.ns_grp = std::min(per, p->g.ns - s0);
         const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, false));
         if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
-        if (NW == 12) launch_fwd_pt<12>(T, grid, st, a);
-        else launch_fwd_pt<8>(T, grid, st, a);
+        launch_fwd_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
     }
     return 0;
@@ -2211,8 +2342,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
         a.g.ns_grp = std::min(per, p->g.ns - s0);
         const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, true));
         if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
-        if (NW == 12) { if (p->adj_fma) launch_adj_pt<12, true>(T, grid, st, a); else launch_adj_pt<12, false>(T, grid, st, a); }
-        else { if (p->adj_fma) launch_adj_pt<8, true>(T, grid, st, a); else launch_adj_pt<8, false>(T, grid, st, a); }
+        launch_adj_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
     }
     return 0;
@@ -2474,6 +2604,19 @@ int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
     return 0;
 }
 
+int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *p, int32_t fwd_rows, int32_t adj_rows)
+{
+    if (!p || (fwd_rows != 6 && fwd_rows != 8 && fwd_rows != 12 && fwd_rows != 24) ||
+        (adj_rows != 6 && adj_rows != 8 && adj_rows != 12))
+        return RDQ_E_INVALID;
+    if (p->fwd_rw != fwd_rows || p->adj_rw != adj_rows) {
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->fwd_rw = fwd_rows;
+    p->adj_rw = adj_rows;
+    return 0;
+}
 int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 {
     if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12 && mode != -1)) return RDQ_E_INVALID;

@@ -10,7 +10,8 @@ import os
 import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libred_diffeq_hip.so")
+# RDQ_HIP_LIB: another build of the same library (A/B timing of kernel variants, tools/)
+LIB_PATH = os.environ.get("RDQ_HIP_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libred_diffeq_hip.so")
 
 c_int32, c_int64, c_float, c_double, c_size_t, c_void_p = (
     ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
@@ -47,6 +48,7 @@ SIGNATURES = {
     "rdq_fwi_set_tuning": (c_int32, [c_void_p, c_int32, c_int32, c_int32]),
     "rdq_fwi_set_variant": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_persistent": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_set_rows_per_wave": (c_int32, [c_void_p, c_int32, c_int32]),
     "rdq_fwi_status": (c_int32, [c_void_p, c_void_p]),
     "rdq_fwi_debug_words": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "rdq_fwi_set_status_buffer": (c_int32, [c_void_p, c_void_p]),

@@ -93,6 +93,12 @@ class FwiPlan:
         flags = (1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
+    def set_rows_per_wave(self, fwd_rows, adj_rows):
+        """Rows per wave of the 64 x 96-region persistent kernels (forward 8 / 12 / 24, adjoint 8 / 12);
+        results are the same for every choice."""
+        _hip.check(self.lib.rdq_fwi_set_rows_per_wave(self.handle, int(fwd_rows), int(adj_rows)),
+                   "rdq_fwi_set_rows_per_wave")
+
     def set_persistent(self, enable):
         """True / 1: persistent launches when they fit (64 x 96 regions first); 12 / 8: persistent with
         that region height only; False / 0: chunked launches.  Results are identical in every mode.
@@ -241,6 +247,8 @@ class FWIForward(nn.Module):
                 self._plans[key].set_variant(xcd_local=False)
             if os.environ.get("RDQ_NO_GRAPHS"):
                 self._plans[key].set_graphs(False)
+            if os.environ.get("RDQ_ROWS_PER_WAVE"):          # "fwd,adj" (tools/ab_rw.sh, red_loop A/B)
+                self._plans[key].set_rows_per_wave(*[int(x) for x in os.environ["RDQ_ROWS_PER_WAVE"].split(",")])
         return self._plans[key]
 
     def _fused_denorm(self):

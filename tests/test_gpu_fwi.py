@@ -96,6 +96,35 @@ def test_gradient_vs_reference_autograd(cuda, name):
     assert err < 5e-6, err
 
 
+@pytest.mark.parametrize("fwd_rows,adj_rows", [(6, 6), (8, 8), (12, 12), (24, 8)])
+@pytest.mark.parametrize("steps", [2, 4])
+def test_rows_per_wave_variants(cuda, fwd_rows, adj_rows, steps):
+    """The 64 x 96-region persistent kernels with 6 / 8 / 12 / 24 rows per wave (16 / 12 / 8 / 4 waves;
+    rdq_fwi_set_rows_per_wave): forward seismograms bit-exact vs the reference, gradient vs the
+    oracle within the FMA build's tolerance, on the 5-shot OpenFWI case and the wrap case."""
+    for name in ("fwd_openfwi_ns5_nt400", "fwd_wrap"):
+        z = load_golden(name)
+        fwi = make_fwi(ctx_of(z))
+        v = torch.from_numpy(vnorm(z["v"])).to(cuda)
+        plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+        plan.set_tuning(steps, steps, 1)
+        plan.set_rows_per_wave(fwd_rows, adj_rows)
+        info = plan.launch_info(v.shape[0])
+        assert info["fwd_persistent"] and info["adj_persistent"], info
+        vg = v.clone().requires_grad_(True)
+        seis = fwi(vg)
+        plan.status()
+        assert bits_equal(seis.detach().cpu().numpy(), z["seis"])
+        ds = torch.from_numpy(np.sign(np.random.default_rng(3).standard_normal(z["seis"].shape)).astype(np.float32))
+        seis.backward(ds.to(cuda))
+        plan.status()
+        f = O.OracleFWI(ctx_of(z), v.shape[0])
+        _, c = f.forward(vnorm(z["v"]), keep_history=True)
+        go = f.finalize(c, *f.adjoint(c, ds.numpy()))
+        err = np.linalg.norm(vg.grad.cpu().numpy() - go) / np.linalg.norm(go)
+        assert err < 5e-6, (name, err)
+
+
 @pytest.mark.parametrize("steps,chains,persist", [(1, 1, True), (2, 1, True), (3, 1, True), (4, 1, True),
                                                   (2, 2, False), (3, 1, False), (4, 3, False)])
 @pytest.mark.parametrize("name,kw", [("fwd_small", {}), ("fwd_small_st3", dict(sample_temporal=3, sample_spatial=0.5)),

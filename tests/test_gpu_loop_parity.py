@@ -137,6 +137,14 @@ def test_tv_long_trajectory_floor(cuda):
     np.testing.assert_allclose(np.array(hist[0]["rmse"], np.float64), z["rmse"].astype(np.float64), atol=1e-4)
 
 
+def _widen(env, w=25):
+    """The ensemble's per-iteration deviation envelope widened by +-w iterations: the trajectories
+    are chaotic (a sign flip moves a cell by +-lr), so when a divergence sets in differs between
+    members by tens of iterations; a pointwise max over five members would flag the timing."""
+    env = np.asarray(env, np.float64)
+    return np.array([env[max(0, i - w):i + w + 1].max() for i in range(len(env))])
+
+
 def _evidence(name, rec):
     """Append a measured-numbers record to $RDQ_EVIDENCE_DIR/<name>.jsonl (GPU evidence runs)."""
     d = os.environ.get("RDQ_EVIDENCE_DIR")
@@ -153,11 +161,14 @@ def test_trajectory_300_within_ensemble(cuda, kind, adjoint):
     (FlatVel-A) and RED-DiffEq (CurveVel-A, dim-8 U-Net, the reference's draws regenerated and
     replayed), ns = 2, nt = 1000, with both persistent adjoints (the default recurrence form and the
     exact-order one).  Bar: at every stored iteration (10, 20, ..., 300) the HIP model's RMSE vs the
-    reference's is within max(1e-4, 1.5 x E_k), where E_k is the largest RMSE vs the reference of the
+    reference's is within max(1e-4, 2 x E_k), where E_k is the largest RMSE vs the reference of the
     five other correct fp32 operators driving the reference engine (tests/golden/make_long.py: the
-    oracle, its FMA build, per-shot gradients, two extra-rounding runs) at iteration k; the 1.5
-    covers a sample max of five.  MAE / RMSE / SSIM / misfit histories likewise within
-    max(atol, 1.5 x the ensemble's per-iteration deviation)."""
+    oracle, its FMA build, per-shot gradients, two extra-rounding runs) over iterations k +- 25
+    (_widen: the trajectories are chaotic, divergence onsets differ by tens of iterations); the 2
+    covers a sample max of five (leave-one-out over the members, 4-member envelopes: model <= 0.58,
+    histories <= 1.05 of the bar).  MAE / RMSE / SSIM / misfit: the same rule on their deviations.
+    North-star terms: the reference's own trajectory is reproducible only to E_k (~6e-3 model RMSE
+    at ts = 300); the 1e-4 bar applies where E_k is below it."""
     z = _with_defaults(load_golden(f"loop_{kind}_300"))
     fwi = make_fwi(ctx_of(z))
     from red_diffeq.utils.data_trans import v_normalize
@@ -172,8 +183,8 @@ def test_trajectory_300_within_ensemble(cuda, kind, adjoint):
     keep = z["keep"].astype(int)
     models = torch.stack(trace).cpu().numpy()[keep - 1, :, 0]          # (n_keep, B=1, 70, 70)
     d = model_rmse(models[:, 0:1], z["models"][:, None])
-    env = z["env_model_rmse"][keep - 1]
-    bar = np.maximum(1e-4, 1.5 * env)
+    env = _widen(z["env_model_rmse"])[keep - 1]
+    bar = np.maximum(1e-4, 2.0 * env)
     rec = {"test": f"trajectory_300[{kind},{adjoint}]", "final_model_rmse_vs_ref": float(d[-1]),
            "max_model_rmse_vs_ref": float(d.max()), "ensemble_final": float(env[-1]),
            "ensemble_max": float(env.max()), "worst_ratio_to_bar": float((d / bar).max()),
@@ -181,9 +192,10 @@ def test_trajectory_300_within_ensemble(cuda, kind, adjoint):
     for k in ("mae", "rmse", "ssim", "obs_losses"):
         got = np.array(hist[0][k], np.float64)
         dev = np.abs(got - z[k].astype(np.float64))
-        lim = np.maximum(1e-6 if k != "obs_losses" else 1e-4 * np.abs(z[k]).max(), 1.5 * z["env_abs_" + k])
+        lim = np.maximum(1e-6 if k != "obs_losses" else 1e-4 * np.abs(z[k]).max(), 2.0 * _widen(z["env_abs_" + k]))
         rec[f"{k}_max_abs_dev"] = float(dev.max())
         rec[f"{k}_worst_ratio_to_bar"] = float((dev / lim).max())
+        rec[f"{k}_worst_iter"] = int(np.argmax(dev / lim)) + 1
     print(json.dumps(rec))
     _evidence("trajectory_300", rec)
     assert np.all(d <= bar), list(zip(keep, d, bar))
