@@ -315,6 +315,79 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
     return h;
 }
 
+// ---- Barrier-free wave-to-wave exchange of the persistent kernels (RDQ_PT_NB).
+// A wave's boundary rows go to LDS as 16-byte slots {row a, tag, row b, tag} (top: rows 0, 1;
+// bottom: rows R-2, R-1), double-buffered by step parity, and the neighbour waves poll their slot
+// until both tags carry the step's number: each wave waits only for the two waves it reads from,
+// not for all NW waves at a workgroup barrier, and a wave publishes its boundary rows as soon as
+// they are computed (its interior rows follow), so the neighbours' data is normally there at the
+// first read.  Overwrite safety of the two buffers: a wave writes step n+1's rows only after it
+// read both neighbours' step-n rows, which they wrote after reading its step n-1 rows (LDS
+// instructions of one wave execute in order).  Each 8-byte half carries its own tag, so a torn
+// 16-byte read is re-polled, never consumed.
+#ifndef RDQ_PT_NB_FWD
+#define RDQ_PT_NB_FWD 1                                   // forward: 1.364 -> 1.287 ms at configs[1]
+#endif
+#ifndef RDQ_PT_NB_ADJ
+#define RDQ_PT_NB_ADJ 0                                   // recurrence adjoint: 1.659 -> 1.688 ms (not used)
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
+template <int NW>
+__device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
+{
+    const u32x4 z = {0u, XQ_NONE, 0u, XQ_NONE};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) { xq[b][w][0][lane] = z; xq[b][w][1][lane] = z; }
+}
+// LDS-qualified slot pointers: ds_read_b128 / ds_write_b128 (a volatile generic pointer would be
+// flat accesses with sc0 sc1 and a full wait after each); the poll re-reads after a compiler memory
+// barrier, so no load is hoisted out of it.
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+template <int NW>
+__device__ __forceinline__ void xq_put(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, unsigned tag, float top0,
+                                       float top1, float bot1, float bot0)
+{
+    lds_u32x4 *q = (lds_u32x4 *)&xq[buf][w][0][lane];
+    q[0] = u32x4{__float_as_uint(top0), tag, __float_as_uint(top1), tag};
+    q[64] = u32x4{__float_as_uint(bot1), tag, __float_as_uint(bot0), tag};
+}
+// rows -2, -1 (the upper wave's R-2, R-1) and R, R+1 (the lower wave's 0, 1); waves 0 / NW-1 read
+// their own slot there (rows outside the region: any value, the halo absorbs it).  `live` false =
+// the launch already failed: no wait.
+// Two halves so a step can run its halo-free work while the reads are in flight: xq_load issues
+// the reads, xq_wait checks the tags (re-polling until they match) and unpacks the rows.
+template <int NW>
+__device__ __forceinline__ void xq_load(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, u32x4 &u, u32x4 &d)
+{
+    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
+    asm volatile("" ::: "memory");
+    u = *(const lds_u32x4 *)&xq[buf][wu][1][lane];
+    d = *(const lds_u32x4 *)&xq[buf][wd][0][lane];
+}
+template <int NW>
+__device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, unsigned tag, u32x4 u,
+                                         u32x4 d, unsigned *status, bool &live)
+{
+    if (!__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (unsigned it = 1;; ++it) {
+            xq_load<NW>(xq, buf, w, lane, u, d);
+            if (__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) break;
+            if (!live) break;
+            if ((it & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s
+                __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                live = false;
+                break;
+            }
+        }
+    }
+    Halo4 h;
+    h.u2 = __uint_as_float(u.x); h.u1 = __uint_as_float(u.z);
+    h.d1 = __uint_as_float(d.x); h.d2 = __uint_as_float(d.z);
+    return h;
+}
+
 // the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
 __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
                                           int lane, const float (&fa)[4], const float (&fb)[4], Halo4 &ha,
@@ -844,14 +917,15 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
             _Pragma("unroll") for (int g_ = 0; g_ < R; g_ += (SG)) {                                \
                 u32x4 x_[(SG)];                                                                     \
                 int o_[(SG)];                                                                       \
-                _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
-                    const int r = g_ + i_;                                                          \
-                    const bool rowin_ = (rin_ >> r) & 1u, rowcy_ = (rcy_ >> r) & 1u;                \
+                constexpr int GN_ = (SG) < R ? (SG) : R;   /* SG need not divide R: rows past R skipped */ \
+                _Pragma("unroll") for (int i_ = 0; i_ < GN_; ++i_) {                                \
+                    const int r = g_ + i_ < R ? g_ + i_ : R - 1;                                    \
+                    const bool rowin_ = g_ + i_ < R && ((rin_ >> r) & 1u), rowcy_ = g_ + i_ < R && ((rcy_ >> r) & 1u); \
                     o_[i_] = rowin_ ? vo_hx : (rowcy_ ? vo_cx : OOB);                               \
                     x_[i_] = gran_get(GR, o_[i_], PT_ROFS(r) * 16);                                 \
                 }                                                                                   \
-                _Pragma("unroll") for (int i_ = 0; i_ < (SG); ++i_) {                               \
-                    const int r = g_ + i_;                                                          \
+                _Pragma("unroll") for (int i_ = 0; i_ < GN_; ++i_) {                                \
+                    const int r = g_ + i_ < R ? g_ + i_ : R - 1;                                    \
                     const bool nd_ = o_[i_] != OOB;                                                 \
                     ok_ = ok_ && (!nd_ || (x_[i_].y == (TAG) && x_[i_].w == (TAG)));                \
                     PT_AT(V0, r) = nd_ ? __uint_as_float(x_[i_].x) : PT_AT(V0, r);                  \
@@ -1025,12 +1099,97 @@ struct FwdPtArgs {
         }                                                                                           \
     }
 
-#define PT_AT(V, r) V[(r) % RP][(r) / RP]     // row r of a row-pair array: pair r mod RP, half r / RP
+// Row r of a row-pair array.  Stacked pairs {i, i+RP} (PT_MIR false: the exact-order adjoint) or
+// mirrored pairs {i, R-1-i} (PT_MIR true: the barrier-free kernels).  In the mirrored form the four
+// boundary rows 0, 1, R-2, R-1 are pairs 0 and 1 alone, so a step can finish (and publish) them
+// before its interior pairs; the vertical neighbours of pair i are still pairs i-1 / i+1 / i-2 /
+// i+2 (the .y half runs the other way, and the stencil's sums are symmetric), except at the slab
+// ends (halo rows) and in the middle, where a pair meets itself swapped.
+template <int RP, bool M>
+__device__ constexpr int pt_pair(int r) { return M ? (r < RP ? r : 2 * RP - 1 - r) : r % RP; }
+template <int RP, bool M>
+__device__ constexpr int pt_half(int r) { return M ? (r < RP ? 0 : 1) : r / RP; }
+#define PT_AT(V, r) V[pt_pair<RP, PT_MIR>(r)][pt_half<RP, PT_MIR>(r)]
+__device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
+// vertical neighbours (rows -1, +1, -2, +2) of mirrored pair i of X; E1 = rows {-1, R}, E2 = {-2, R+1}
+#define MIR_VERT(X, i, m1, p1, m2, p2)                                                              \
+    const f32x2 m1 = (i) >= 1 ? X[(i) - 1] : E1;                                                    \
+    const f32x2 p1 = (i) <= RP - 2 ? X[(i) + 1] : swp(X[RP - 1]);                                   \
+    const f32x2 m2 = (i) >= 2 ? X[(i) - 2] : ((i) == 1 ? E1 : E2);                                  \
+    const f32x2 p2 = (i) <= RP - 3 ? X[(i) + 2] : ((i) == RP - 2 ? swp(X[RP - 1]) : swp(X[RP - 2]));
+
+// Barrier-free forward step (RDQ_PT_NB): the halo-free work of every pair (DPP shifts, time
+// terms) first, then the wait for the neighbours' boundary rows, the two boundary pairs, their
+// publication for the next step, and the interior pairs after it.  Per row the operations and
+// their order are FWD_STEP's (bit-exact).
+#define FWD_PAIRS_NB(CUR, PRV, LO, HI)                                                                        \
+    {                                                                                               \
+        _Pragma("unroll") for (int i = (LO); i < (HI); ++i) {                                        \
+            MIR_VERT(CUR, i, m1, p1, m2, p2)                                                        \
+            f32x2 s1 = m1 + p1; s1 = s1 + xl1[i]; s1 = s1 + xr1[i];                                 \
+            const f32x2 la = kC2 * s1;                                                              \
+            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            s2.x = s2.x + dpp_shr1(xl1[i].x); s2.y = s2.y + dpp_shr1(xl1[i].y);                     \
+            s2.x = s2.x + dpp_shl1(xr1[i].x); s2.y = s2.y + dpp_shl1(xr1[i].y);                     \
+            const f32x2 l2 = kC3 * s2; const f32x2 lap = la + l2;                                   \
+            const f32x2 a3 = A[i] * lap;                                                            \
+            PRV[i] = tt[i] + a3;                                                                    \
+        }                                                                                           \
+        if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
+            const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
+            if (s1row) {                                                                            \
+                const f32x2 av = shalf ? f32x2{-0.0f, add} : f32x2{add, -0.0f};                     \
+                int sp_ = spair;                                                                    \
+                LAUNDER(sp_);                                                                       \
+                _Pragma("unroll") for (int i = (LO); i < (HI); ++i)                                  \
+                    if (i == sp_) PRV[i] = PRV[i] + av;                                             \
+            } else {                                                                                \
+                unsigned sm_ = smask;                                                               \
+                LAUNDER(sm_);                                                                       \
+                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
+                    if (pt_pair<RP, PT_MIR>(r) >= (LO) && pt_pair<RP, PT_MIR>(r) < (HI) && ((sm_ >> r) & 1u)) \
+                        PT_AT(PRV, r) = PT_AT(PRV, r) + add;                                        \
+            }                                                                                       \
+        }                                                                                           \
+    }
+#define FWD_STEP_NB(CUR, PRV)                                                                       \
+    {                                                                                               \
+        u32x4 xu_, xd_;                                                                             \
+        xq_load<NW>(xq, n & 1, w, lane, xu_, xd_);                                                  \
+        f32x2 xl1[RP], xr1[RP], tt[RP];                                                             \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
+            const f32x2 c = CUR[i];                                                                 \
+            xl1[i] = f32x2{dpp_shr1(c.x), dpp_shr1(c.y)};                                           \
+            xr1[i] = f32x2{dpp_shl1(c.x), dpp_shl1(c.y)};                                           \
+            f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
+            tt[i] = a1;                                                                             \
+        }                                                                                           \
+        const Halo4 h4 = xq_wait<NW>(xq, n & 1, w, lane, (unsigned)n + 1u, xu_, xd_, a.status, live); \
+        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
+        FWD_PAIRS_NB(CUR, PRV, 0, 2)                                                                          \
+        if (t + 1 < T)                                                                              \
+            xq_put<NW>(xq, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0].x, PRV[1].x, PRV[1].y, PRV[0].y); \
+        FWD_PAIRS_NB(CUR, PRV, 2, RP)                                                                         \
+        if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
+        if (rrow >= 0) {                             /* receiver row: value kept, stored per epoch */ \
+            int rp_ = rpair;                                                                        \
+            LAUNDER(rp_);                                                                           \
+            f32x2 v_ = PRV[0];                                                                      \
+            _Pragma("unroll") for (int i = 1; i < RP; ++i) if (i == rp_) v_ = PRV[i];                \
+            rv[t] = rhalf ? v_.y : v_.x;                                                            \
+        }                                                                                           \
+    }
+
 template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
+    constexpr bool PT_MIR = RDQ_PT_NB_FWD != 0;
+#if RDQ_PT_NB_FWD
+    __shared__ u32x4 xq[2][NW][2][64];
+#else
     __shared__ float xch[2][NW][4][64];
+#endif
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
@@ -1061,8 +1220,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     // source / receiver rows as (row pair, half): the step touches one pair, not all eight rows
     const bool s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
     const int sr1 = smask ? __builtin_ctz(smask) : 0;
-    const int spair = sr1 % RP, rpair = rrow >= 0 ? (rrow % RP) : 0;
-    const bool shalf = sr1 >= RP, rhalf = rrow >= RP;
+    const int spair = PT_MIR ? (sr1 < RP ? sr1 : R - 1 - sr1) : sr1 % RP;
+    const int rpair = rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP;
+    const bool shalf = sr1 >= RP, rhalf = rrow >= RP;     // the half is r >= RP in both pairings
     float rv[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) rv[t] = 0.0f;
@@ -1082,6 +1242,14 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
 #define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
+#if RDQ_PT_NB_FWD
+    xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
+    __syncthreads();
+    xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // P_0 = 0, step 0's tag
+#define FWD_STEP_SEL FWD_STEP_NB
+#else
+#define FWD_STEP_SEL FWD_STEP
+#endif
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
         PT_PROF(tsw)
@@ -1089,8 +1257,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         for (int t = 0; t < T; ++t) {
             const int n = n0 + t;
             if (n >= a.nt) break;
-            if (t & 1) FWD_STEP(P0, P1)
-            else FWD_STEP(P1, P0)
+            if (t & 1) FWD_STEP_SEL(P0, P1)
+            else FWD_STEP_SEL(P1, P0)
         }
         if (T & 1) {   // keep "P1 = newest" at every epoch boundary
 #pragma unroll
@@ -1106,9 +1274,14 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
             FWD_ISSUE
+#if RDQ_PT_NB_FWD
+            // the next step's boundary rows, with the halo cells the sweep reloaded
+            xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
+#endif
         }
         FWD_RECORD
     }
+#undef FWD_STEP_SEL
 #undef FWD_ISSUE
 #undef FWD_HIST
 #undef FWD_RECORD
@@ -1254,6 +1427,7 @@ template <int T, int NW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
+    constexpr bool PT_MIR = false;                        // stacked pairs {i, i+4} (ADJ_PLOAD / ADJ_GRAD)
     __shared__ float xch[2][NW][4][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
@@ -1404,7 +1578,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         const int so_ = (SOFF);                                                                     \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             PD[i].x = bload_nt(HR, pr[i], so_);                                                     \
-            PD[i].y = bload_nt(HR, pr[i + RP], so_);                                                \
+            PD[i].y = bload_nt(HR, pr[PT_MIR ? R - 1 - i : i + RP], so_);                           \
         }                                                                                           \
     }
 
@@ -1485,11 +1659,58 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
     }
 
+// Barrier-free adjoint step (RDQ_PT_NB, mirrored pairs): wait for the neighbours' A L_{k+1} rows,
+// the boundary pairs of L_k (receiver residual included), their A L_k published for the next step,
+// then the interior pairs and the gradient.  Per row the operations are ADJR_STEP's.
+#define ADJR_PAIRS_NB(CUR, PRV, LO, HI)                                                                       \
+    {                                                                                               \
+        _Pragma("unroll") for (int i = (LO); i < (HI); ++i) {                                        \
+            MIR_VERT(q, i, m1, p1, m2, p2)                                                          \
+            const f32x2 c = q[i];                                                                   \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
+            f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
+            n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
+            const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
+            PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
+        }                                                                                           \
+        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+            int rp_ = rpair;                                                                        \
+            LAUNDER(rp_);                                                                           \
+            const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
+            _Pragma("unroll") for (int i = (LO); i < (HI); ++i) if (i == rp_) PRV[i] = PRV[i] + dv_; \
+        }                                                                                           \
+    }
+#define ADJR_STEP_NB(CUR, PRV, P0, P1, P2, PN)                                                      \
+    {                                                                                               \
+        if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
+        const float dcur = dv[t];                                                                   \
+        u32x4 xu_, xd_;                                                                             \
+        xq_load<NW>(xq, j & 1, w, lane, xu_, xd_);                                                  \
+        f32x2 q[RP];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = xq_wait<NW>(xq, j & 1, w, lane, (unsigned)j + 1u, xu_, xd_, a.status, live); \
+        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
+        ADJR_PAIRS_NB(CUR, PRV, 0, 2)                                                                         \
+        if (t + 1 < T) {                                                                            \
+            const f32x2 qa = A[0] * PRV[0], qb = A[1] * PRV[1];                                     \
+            xq_put<NW>(xq, (j + 1) & 1, w, lane, (unsigned)j + 2u, qa.x, qb.x, qb.y, qa.y);         \
+        }                                                                                           \
+        ADJR_PAIRS_NB(CUR, PRV, 2, RP)                                                                        \
+        if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
+    }
+
 template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
+    constexpr bool PT_MIR = RDQ_PT_NB_ADJ != 0;
+#if RDQ_PT_NB_ADJ
+    __shared__ u32x4 xq[2][NW][2][64];
+#else
     __shared__ float xch[2][NW][4][64];
+#endif
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
@@ -1514,8 +1735,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
     // source / receiver rows as (row pair, half): a step touches one pair, not all eight rows
-    const int spair = srow >= 0 ? (srow % RP) : 0, rpair = rrow >= 0 ? (rrow % RP) : 0;
-    const bool shalf = srow >= RP, rhalf = rrow >= RP;
+    const int spair = srow < 0 ? 0 : PT_MIR ? (srow < RP ? srow : R - 1 - srow) : srow % RP;
+    const int rpair = rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP;
+    const bool shalf = srow >= RP, rhalf = rrow >= RP;   // the half is r >= RP in both pairings
 #define DLOAD(KK)                                                                                   \
     ({                                                                                              \
         const int ri_ = (KK) >= 1 ? rec_index((KK) - 1, g.st) : -1;                                 \
@@ -1558,6 +1780,14 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
+#if RDQ_PT_NB_ADJ
+    xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
+    __syncthreads();
+    xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // A L_{nt+1} = 0, step 0's tag
+#define ADJR_STEP_SEL ADJR_STEP_NB
+#else
+#define ADJR_STEP_SEL ADJR_STEP
+#endif
     for (int e = 0; e < nep; ++e) {
         const int ke = a.nt - e * T;                      // first step k of this epoch
         const bool last = e + 1 == nep;
@@ -1567,10 +1797,10 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             const int j = e * T + t;
             if (j >= a.nt) break;
             const int k = ke - t;
-            if ((t & 3) == 0) ADJR_STEP(L1, L0, Q0, Q1, Q2, Q3)
-            else if ((t & 3) == 1) ADJR_STEP(L0, L1, Q1, Q2, Q3, Q0)
-            else if ((t & 3) == 2) ADJR_STEP(L1, L0, Q2, Q3, Q0, Q1)
-            else ADJR_STEP(L0, L1, Q3, Q0, Q1, Q2)
+            if ((t & 3) == 0) ADJR_STEP_SEL(L1, L0, Q0, Q1, Q2, Q3)
+            else if ((t & 3) == 1) ADJR_STEP_SEL(L0, L1, Q1, Q2, Q3, Q0)
+            else if ((t & 3) == 2) ADJR_STEP_SEL(L1, L0, Q2, Q3, Q0, Q1)
+            else ADJR_STEP_SEL(L0, L1, Q3, Q0, Q1, Q2)
         }
         if (T & 1) {   // keep "L1 = newest" at every epoch boundary
 #pragma unroll
@@ -1588,6 +1818,13 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             ADJ_ISSUE
+#if RDQ_PT_NB_ADJ
+            {   // the next step's boundary rows of A L_{k+1}, with the halo cells the sweep reloaded
+                const int jn = (e + 1) * T;
+                const f32x2 qa = A[0] * L1[0], qb = A[1] * L1[1];
+                xq_put<NW>(xq, jn & 1, w, lane, (unsigned)jn + 1u, qa.x, qb.x, qb.y, qa.y);
+            }
+#endif
             PT_PROF(tsw)
         }
         if constexpr ((T & 3) != 0) {   // restore Q0 = the next epoch's P_k
@@ -1598,6 +1835,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             }
         }
     }
+#undef ADJR_STEP_SEL
 #undef QW
 #undef DLOAD
 #undef ADJ_ISSUE
@@ -1632,6 +1870,11 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
 }
 #undef ADJR_STEP
+#undef ADJR_STEP_NB
+#undef ADJR_PAIRS_NB
+#undef FWD_STEP_NB
+#undef FWD_PAIRS_NB
+#undef MIR_VERT
 #undef ADJR_GRAD
 #undef ADJR_GRAD_PRE
 #undef ADJR_GRAD_POST
@@ -2488,6 +2731,16 @@ int run_cached(rdq_fwi_plan *p, int kind, int B, std::initializer_list<const voi
 // ======================================================================================= C ABI
 extern "C" {
 
+// The recurrence adjoint (k_adj_pr) recovers lap'(P_{k-1}) = (P_k - T1 P_{k-1} + T2 P_{k-2} - src) / A
+// from three history levels: a difference of nearly equal values whenever the field is smooth on
+// the grid scale.  With an absorbing sponge (the reference's nbc = 120) the field keeps its
+// wavelength and the gradient stays within ~1e-5 of the exact order (profiles/r3/
+// small_dt_adjoint.jsonl: 1.0e-5 at dt = 1 ms, 3.9e-5 at dt / 4); a thin sponge lets the wave wrap
+// round the periodic grid into long standing modes and the cancellation costs 5e-3 (tests/
+// golden/fwd_wrap: nbc = 4).  Below RDQ_RECURRENCE_MIN_NBC the plan runs the exact-order adjoint.
+constexpr int RDQ_RECURRENCE_MIN_NBC = 20;
+static bool recurrence_ok(const rdq_fwi_plan *p) { return p->g.nbc >= RDQ_RECURRENCE_MIN_NBC; }
+
 int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
 {
     if (!geom || !out || geom->nz < 1 || geom->nx < 1 || geom->nbc < 0 || geom->nt < 1 || geom->ns < 1 ||
@@ -2543,6 +2796,7 @@ int rdq_fwi_plan_create(const rdq_fwi_geom *geom, rdq_fwi_plan **out)
     if (e == hipSuccess) e = hipMalloc(&p->d_status_own, 256);
     if (e == hipSuccess) e = hipMemset(p->d_status_own, 0, 256);
     p->d_status = p->d_status_own;
+    p->adj_fma = recurrence_ok(p);
     if (e != hipSuccess) { rdq_fwi_plan_destroy(p); return -(int)e; }
     *out = p;
     return 0;
@@ -2592,7 +2846,8 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
     if (!p || (flags & ~7)) return RDQ_E_INVALID;
-    const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0, fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0;
+    const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0;
+    const bool fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0 && recurrence_ok(p);
     const int xcd = (flags & RDQ_VARIANT_NO_XCD_LOCAL) ? 0 : 1;
     if (p->fwd_gen != gen || p->adj_fma != fma || p->xcd_mode != xcd) {
         drop_graphs(p);

@@ -96,6 +96,45 @@ def test_gradient_vs_reference_autograd(cuda, name):
     assert err < 5e-6, err
 
 
+@pytest.mark.parametrize("dt,f", [(0.001, 15.0), (0.0005, 15.0), (0.00025, 15.0), (0.001, 7.5)])
+def test_recurrence_adjoint_at_small_dt(cuda, dt, f):
+    """The default persistent adjoint rebuilds lap'(P_{k-1}) from three history levels and divides by
+    A = (v dt / dx)^2, so rounding in P grows like eps / (omega dt)^2 as dt or f shrinks.  Every
+    reference config runs dt = 0.001, f = 15 Hz; this pins the error at 2x and 4x smaller dt and at
+    half the frequency against the oracle, next to the exact-order adjoint (rdq_fwi_set_variant
+    flag 2) on the same inputs.  Bars (rel-L2 of dL/dv vs the oracle, sign residuals): exact order
+    1e-6 (measured 0), recurrence 2e-5 at the reference's dt and f (measured 1.0e-5), 1e-4 below them
+    (measured 2.3e-5 at dt / 2, 3.9e-5 at dt / 4, 4.6e-6 at f / 2; profiles/r3/small_dt_adjoint.jsonl)."""
+    z = load_golden("grad_openfwi_ns1")
+    ctx = ctx_of(z)
+    ctx["dt"], ctx["f"] = dt, f
+    nt = int(ctx["nt"])
+    vn0 = vnorm(z["v_init"])
+    fo = O.OracleFWI(ctx, vn0.shape[0])
+    seis_o, c = fo.forward(vn0, keep_history=True)
+    ds = np.sign(np.random.default_rng(11).standard_normal(seis_o.shape)).astype(np.float32)
+    go = fo.finalize(c, *fo.adjoint(c, ds))
+    errs = {}
+    for exact in (False, True):
+        fwi = make_fwi(ctx)
+        vn = torch.from_numpy(vn0).to(cuda).requires_grad_(True)
+        plan = fwi._plan(vn.shape[2], vn.shape[3], cuda)
+        plan.set_variant(adj_exact=exact)
+        seis = fwi(vn)
+        seis.backward(torch.from_numpy(ds).to(cuda))
+        plan.status()
+        assert plan.launch_info(1)["adj_persistent"]
+        errs[exact] = float(np.linalg.norm(vn.grad.cpu().numpy() - go) / np.linalg.norm(go))
+    rec = {"dt": dt, "f": f, "nt": nt, "grad_rel_l2_recurrence": errs[False], "grad_rel_l2_exact": errs[True]}
+    d = os.environ.get("RDQ_EVIDENCE_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "small_dt_adjoint.jsonl"), "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
+    assert errs[True] < 1e-6, rec
+    assert errs[False] < (2e-5 if (dt, f) == (0.001, 15.0) else 1e-4), rec
+
+
 @pytest.mark.parametrize("fwd_rows,adj_rows", [(6, 6), (8, 8), (12, 12), (24, 8)])
 @pytest.mark.parametrize("steps", [2, 4])
 def test_rows_per_wave_variants(cuda, fwd_rows, adj_rows, steps):
