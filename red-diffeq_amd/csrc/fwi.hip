@@ -1271,9 +1271,12 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             PT_PUBLISH(GR, tag, P0, P1)
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, P0, P1, R)
+            // the next epoch's wavelet loads BEFORE the last step's history stores: vmcnt counts loads
+            // and stores in order, so the source wave's first use of wv[0] would otherwise wait for
+            // those stores' write acknowledgements (and its neighbours for it)
+            FWD_ISSUE
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
-            FWD_ISSUE
 #if RDQ_PT_NB_FWD
             // the next step's boundary rows, with the halo cells the sweep reloaded
             xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
@@ -1573,6 +1576,10 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 // epoch: P_k, P_{k-1}, P_{k-2} = Q[t], Q[t+1], Q[t+2] mod 4, prefetch into Q[t+3]): no copies for
 // T = 4; other depths restore the order once per epoch.
 
+#ifdef RDQ_EXP_NOHIST   // timing experiment only (wrong results): no history loads in the adjoint
+#define ADJR_LOAD(PD, HR, SOFF)                                                                     \
+    { _Pragma("unroll") for (int i = 0; i < RP; ++i) PD[i] = PD[i] * A[i]; }
+#else
 #define ADJR_LOAD(PD, HR, SOFF)                                                                     \
     {                                                                                               \
         const int so_ = (SOFF);                                                                     \
@@ -1581,6 +1588,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             PD[i].y = bload_nt(HR, pr[PT_MIR ? R - 1 - i : i + RP], so_);                           \
         }                                                                                           \
     }
+#endif
 
 // gradient of step k (CU = L_{k+1}, LN = L_k; wavelet sample WK = w[k-1]; window P0 = P_k,
 // P1 = P_{k-1}, P2 = P_{k-2}), in two halves: PRE forms d = 2c1 P_{k-1} + lap'(P_{k-1}) from the
@@ -1752,7 +1760,8 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     f32x2 Q0[RP], Q1[RP], Q2[RP], Q3[RP];
     int pr[R];                                            // history offset of (own row r, lane)
 #pragma unroll
-    for (int r = 0; r < R; ++r) pr[r] = grad ? (PT_ROFS(r) + gx) * 4 : OOB;
+    for (int r = 0; r < R; ++r)   // own cells only: the gradient is kept for those alone (halo lanes load 0)
+        pr[r] = (xin && ((rin >> r) & 1u)) ? (PT_ROFS(r) + gx) * 4 : OOB;
 #pragma unroll
     for (int i = 0; i < RP; ++i) { Q0[i] = 0.0f; Q1[i] = 0.0f; Q2[i] = 0.0f; Q3[i] = 0.0f; }
     // history descriptor of the epoch whose first step is KN: its prefetches read slots
