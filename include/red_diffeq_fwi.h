@@ -102,8 +102,9 @@ int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *plan, int32_t fwd_rows, int32_t adj_rows);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the
- * device, with 64 x 96 regions if they fit, else 64 x 64; 12 / 8 = only that region height;
- * 0 = always the chunked launches.  Identical results in every mode.  -1 (fault-path tests only):
+ * device: small surveys (at most 200 workgroups, e.g. 3 OpenFWI shots) in 64 x 64 regions of 16
+ * waves x 4 rows, otherwise 64 x 96 regions if they fit, else 64 x 64 regions of 8 waves x 8 rows;
+ * 16 / 12 / 8 = only that region class; 0 = always the chunked launches.  Identical results in every mode.  -1 (fault-path tests only):
  * persistent launches oversubscribed to twice the resident capacity, so they report "not resident"
  * through the status word instead of computing. */
 int rdq_fwi_set_persistent(rdq_fwi_plan *plan, int32_t mode);
@@ -121,7 +122,8 @@ int rdq_fwi_debug_words(rdq_fwi_plan *plan, uint32_t out[32]);
  * asynchronously to pinned host memory).  Replaces the plan's internal words for later launches. */
 int rdq_fwi_set_status_buffer(rdq_fwi_plan *plan, uint32_t *words);
 /* Which kernels a forward / adjoint call for batch B runs: out = {forward persistent region
- * height in waves (0 = chunked), the same for the adjoint, forward steps per epoch/launch,
+ * class (16 = 64 x 64 regions of 16 waves x 4 rows, 12 = 64 x 96 regions, 8 = 64 x 64 of 8 waves x 8
+ * rows; 0 = chunked), the same for the adjoint, forward steps per epoch/launch,
  * adjoint steps per epoch/launch, forward time-loop launches per call, adjoint time-loop launches
  * per call} (persistent: one per resident shot group; chunked: ceil(nt / T)). */
 int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[6]);

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -988,7 +989,11 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
 // Re-materialise a wave-uniform value inside the time loop: stops the compiler from hoisting the
 // per-row compares on it out of the loop as live 64-bit lane masks (which spill to VGPR lanes and
 // cost v_readlane pairs in every step).
-#define LAUNDER(x) asm volatile("" : "+s"(x))
+#define LAUNDER(x)                                                                                  \
+    do {                                                                                            \
+        x = __builtin_amdgcn_readfirstlane(x);   /* uniform by construction: never a VGPR->SGPR copy */ \
+        asm volatile("" : "+s"(x));                                                                 \
+    } while (0)
 
 struct FwdPtArgs {
     TBGeo g;
@@ -1135,7 +1140,7 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
             const f32x2 a3 = A[i] * lap;                                                            \
             PRV[i] = tt[i] + a3;                                                                    \
         }                                                                                           \
-        if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
+        if ((HI) > (LO) && smask) {                  /* pde.py:80-81 (uniform: source row waves) */ \
             const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
             if (s1row) {                                                                            \
                 const f32x2 av = shalf ? f32x2{-0.0f, add} : f32x2{add, -0.0f};                     \
@@ -1220,8 +1225,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     // source / receiver rows as (row pair, half): the step touches one pair, not all eight rows
     const bool s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
     const int sr1 = smask ? __builtin_ctz(smask) : 0;
-    const int spair = PT_MIR ? (sr1 < RP ? sr1 : R - 1 - sr1) : sr1 % RP;
-    const int rpair = rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP;
+    // wave-uniform by construction; readfirstlane makes that visible to the compiler (LAUNDER "+s")
+    const int spair = __builtin_amdgcn_readfirstlane(PT_MIR ? (sr1 < RP ? sr1 : R - 1 - sr1) : sr1 % RP);
+    const int rpair = __builtin_amdgcn_readfirstlane(rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP);
     const bool shalf = sr1 >= RP, rhalf = rrow >= RP;     // the half is r >= RP in both pairings
     float rv[T];
 #pragma unroll
@@ -1271,12 +1277,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             PT_PUBLISH(GR, tag, P0, P1)
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, P0, P1, R)
-            // the next epoch's wavelet loads BEFORE the last step's history stores: vmcnt counts loads
-            // and stores in order, so the source wave's first use of wv[0] would otherwise wait for
-            // those stores' write acknowledgements (and its neighbours for it)
-            FWD_ISSUE
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
+            FWD_ISSUE                                     // (before the stores: 1.32 -> 1.375 ms, not used)
 #if RDQ_PT_NB_FWD
             // the next step's boundary rows, with the halo cells the sweep reloaded
             xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
@@ -1683,7 +1686,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
             PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
         }                                                                                           \
-        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+        if ((HI) > (LO) && rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: receiver wave */ \
             int rp_ = rpair;                                                                        \
             LAUNDER(rp_);                                                                           \
             const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
@@ -1743,8 +1746,8 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     const float *DSb = a.dseis + (size_t)bs * g.nrec * g.dstride;
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(DSb);
     // source / receiver rows as (row pair, half): a step touches one pair, not all eight rows
-    const int spair = srow < 0 ? 0 : PT_MIR ? (srow < RP ? srow : R - 1 - srow) : srow % RP;
-    const int rpair = rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP;
+    const int spair = __builtin_amdgcn_readfirstlane(srow < 0 ? 0 : PT_MIR ? (srow < RP ? srow : R - 1 - srow) : srow % RP);
+    const int rpair = __builtin_amdgcn_readfirstlane(rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP);
     const bool shalf = srow >= RP, rhalf = rrow >= RP;   // the half is r >= RP in both pairings
 #define DLOAD(KK)                                                                                   \
     ({                                                                                              \
@@ -1760,8 +1763,8 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     f32x2 Q0[RP], Q1[RP], Q2[RP], Q3[RP];
     int pr[R];                                            // history offset of (own row r, lane)
 #pragma unroll
-    for (int r = 0; r < R; ++r)   // own cells only: the gradient is kept for those alone (halo lanes load 0)
-        pr[r] = (xin && ((rin >> r) & 1u)) ? (PT_ROFS(r) + gx) * 4 : OOB;
+    for (int r = 0; r < R; ++r)   // every lane (own cells only, halo lanes at OOB: 1.66 -> 1.73 ms)
+        pr[r] = grad ? (PT_ROFS(r) + gx) * 4 : OOB;
 #pragma unroll
     for (int i = 0; i < RP; ++i) { Q0[i] = 0.0f; Q1[i] = 0.0f; Q2[i] = 0.0f; Q3[i] = 0.0f; }
     // history descriptor of the epoch whose first step is KN: its prefetches read slots
@@ -2227,7 +2230,8 @@ struct rdq_fwi_plan {
     // resident workgroups (0 = unknown) per kernel variant [variant][T]: 0 fwd 64-row, 1..3 fwd 96-row
     // with 8 / 12 / 24 rows per wave, 4 exact adjoint 64-row, 5 exact 96-row, 6 FMA adjoint 64-row,
     // 7..8 FMA adjoint 96-row with 8 / 12 rows per wave
-    int capw[11][TB_MAXT + 1] = {};   // [9] fwd 96-row x 6 rows per wave, [10] FMA adjoint 96-row x 6
+    int capw[13][TB_MAXT + 1] = {};   // [9] fwd 96-row x 6 rows per wave, [10] FMA adjoint 96-row x 6,
+                                      // [11] / [12] fwd / FMA adjoint 64-row x 4 rows per wave (class 16)
     int fwd_rw = 6, adj_rw = 8;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
@@ -2367,6 +2371,7 @@ int capacity_T(rdq_fwi_plan *p, int NW, bool adj)
 {
     auto *c = p->capw;
     if (!adj) {
+        if (NW == 16) return resident_capacity(k_fwd_pt<T, 16, 4, false>, 1024, c[11][T]);
         if (NW != 12) return resident_capacity(k_fwd_pt<T, 8, 8, false>, 512, c[0][T]);
         if (p->fwd_rw == 24) return resident_capacity(k_fwd_pt<T, 4, 24, false>, 256, c[3][T]);
         if (p->fwd_rw == 6) return resident_capacity(k_fwd_pt<T, 16, 6, false>, 1024, c[9][T]);
@@ -2375,7 +2380,8 @@ int capacity_T(rdq_fwi_plan *p, int NW, bool adj)
     }
     if (NW != 12)
         return std::min(resident_capacity(k_adj_pt<T, 8, false>, 512, c[4][T]),
-                        resident_capacity(k_adj_pr<T, 8, 8, false>, 512, c[6][T]));
+                        NW == 16 ? resident_capacity(k_adj_pr<T, 16, 4, false>, 1024, c[12][T])
+                                 : resident_capacity(k_adj_pr<T, 8, 8, false>, 512, c[6][T]));
     const int ex = resident_capacity(k_adj_pt<T, 12, false>, 768, c[5][T]);
     if (p->adj_rw == 12) return std::min(ex, resident_capacity(k_adj_pr<T, 8, 12, false>, 512, c[8][T]));
     if (p->adj_rw == 6) return std::min(ex, resident_capacity(k_adj_pr<T, 16, 6, false>, 1024, c[10][T]));
@@ -2391,10 +2397,14 @@ int capacity_nw(rdq_fwi_plan *p, int NW, bool adj, int T)
     }
 }
 
+// Region classes of the persistent kernels: 12 = 64 x 96 regions (the plan's rows per wave),
+// 8 = 64 x 64 regions of 8 waves x 8 rows, 16 = 64 x 64 regions of 16 waves x 4 rows.
+static int region_rows(int NW) { return NW == 12 ? 96 : 64; }
+
 // tiles (padded to the 8-XCD deal) of one (model, shot) slice at depth T with NW-wave regions
 unsigned pt_tiles_padded(const rdq_fwi_plan *p, int T, int NW)
 {
-    const int ih = NW * TB_R - 4 * T;
+    const int ih = region_rows(NW) - 4 * T;
     const int nt_ = tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih);
     return (unsigned)((nt_ + 7) / 8 * 8);
 }
@@ -2421,7 +2431,7 @@ unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
     const unsigned S = (unsigned)B * (unsigned)nsg;
     unsigned grid = pt_tiles_padded(p, T, NW) * S;
     if (p->xcd_mode) {
-        const int ih = NW * TB_R - 4 * T;
+        const int ih = region_rows(NW) - 4 * T;
         const unsigned Tt = (unsigned)(tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih));
         const unsigned want = 8u * Tt * ((S + 7u) / 8u);
         const int cap = capacity_nw(const_cast<rdq_fwi_plan *>(p), NW, adj, T);
@@ -2437,11 +2447,21 @@ unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
 // region height (waves) of the persistent kernel for this call, 0 = not resident -> chunked.
 // Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).  `per` = shots
 // per launch (the survey runs as ceil(ns / per) launches).
+// Small surveys first: a launch of at most PT_SMALL_WG workgroups in 64 x 64 regions of 16 waves x
+// 4 rows runs each step with 2/3 of the 96-row kernels' per-wave work on CUs the 96-row launch leaves
+// idle (profiles/r3/pt64_ab.txt, configs[1] geometry: 3 shots = 168 workgroups, forward 1.30 -> 1.14
+// ms, adjoint 1.65 -> 1.44; at 5 shots, 280, no slice fits one XCD and it is slower).
+constexpr unsigned PT_SMALL_WG = 200;
 int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
 {
     if (!p->persist) return 0;
     const int T = adj ? p->adj_T : p->fwd_T;
-    const int want = p->persist == -1 ? 1 : p->persist;   // 1 = auto, 8 / 12 = forced
+    const int want = p->persist == -1 ? 1 : p->persist;   // 1 = auto, 8 / 12 / 16 = forced
+    if (want == 1 || want == 16) {
+        const int k = pt_shots_per_launch(p, B, T, 16, capacity_nw(p, 16, adj, T));
+        const bool small = k >= p->g.ns && pt_tiles_padded(p, T, 16) * (unsigned)(B * p->g.ns) <= PT_SMALL_WG;
+        if (k > 0 && (want == 16 || small)) { if (per) *per = k; return 16; }
+    }
     if (want == 1 || want == 12) {
         const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw(p, 12, adj, T));
         if (k > 0) { if (per) *per = k; return 12; }
@@ -2457,7 +2477,8 @@ int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
 template <int T, bool PROF>
 void launch_fwd_pt_T(const rdq_fwi_plan *p, int NW, dim3 grid, hipStream_t st, const FwdPtArgs &a)
 {
-    if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
+    if (NW == 16) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 16, 4, PROF>), grid, dim3(1024), 0, st, a);
+    else if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
     else if (p->fwd_rw == 24) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 4, 24, PROF>), grid, dim3(256), 0, st, a);
     else if (p->fwd_rw == 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 8, 12, PROF>), grid, dim3(512), 0, st, a);
     else if (p->fwd_rw == 6) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_pt<T, 16, 6, PROF>), grid, dim3(1024), 0, st, a);
@@ -2482,7 +2503,8 @@ void launch_adj_pt_T(const rdq_fwi_plan *p, int NW, dim3 grid, hipStream_t st, c
     if (!p->adj_fma) {
         if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<T, 8, PROF>), grid, dim3(512), 0, st, a);
         else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pt<T, 12, PROF>), grid, dim3(768), 0, st, a);
-    } else if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
+    } else if (NW == 16) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 16, 4, PROF>), grid, dim3(1024), 0, st, a);
+    else if (NW != 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 8, 8, PROF>), grid, dim3(512), 0, st, a);
     else if (p->adj_rw == 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 8, 12, PROF>), grid, dim3(512), 0, st, a);
     else if (p->adj_rw == 6) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 16, 6, PROF>), grid, dim3(1024), 0, st, a);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_pr<T, 12, 8, PROF>), grid, dim3(768), 0, st, a);
@@ -2549,7 +2571,7 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     if (int e = zero_regions({{hist, hist ? 2 * L * sizeof(float) : 0}, {ring, 4 * L * sizeof(unsigned long long)},
                               {p->d_status + 16, 8 * sizeof(unsigned)}}, st))
         return e;
-    const int ih = NW * TB_R - 4 * T;
+    const int ih = region_rows(NW) - 4 * T;
     a.g.tiles_x = tiles_x(p->Wp, T);
     a.g.ntiles = a.g.tiles_x * ((p->Hp + ih - 1) / ih);
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
@@ -2581,7 +2603,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
                               {gbeta, (size_t)B * p->g.ns * sizeof(float)}, {p->d_status + 16, 8 * sizeof(unsigned)}},
                              st))
         return e;
-    const int ih = NW * TB_R - 4 * T;
+    const int ih = region_rows(NW) - 4 * T;
     a.g.tiles_x = tiles_x(p->Wp, T);
     a.g.ntiles = a.g.tiles_x * ((p->Hp + ih - 1) / ih);
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.dseis = dseis;
@@ -2883,7 +2905,7 @@ int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *p, int32_t fwd_rows, int32_t adj_row
 }
 int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 {
-    if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12 && mode != -1)) return RDQ_E_INVALID;
+    if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12 && mode != 16 && mode != -1)) return RDQ_E_INVALID;
     if (p->persist != mode) {
         drop_graphs(p);
         p->cache.clear();

@@ -100,8 +100,9 @@ class FwiPlan:
                    "rdq_fwi_set_rows_per_wave")
 
     def set_persistent(self, enable):
-        """True / 1: persistent launches when they fit (64 x 96 regions first); 12 / 8: persistent with
-        that region height only; False / 0: chunked launches.  Results are identical in every mode.
+        """True / 1: persistent launches when they fit (small surveys in 64 x 64 regions of 16 waves x
+        4 rows, else 64 x 96 regions, else 64 x 64 of 8 waves x 8 rows); 16 / 12 / 8: persistent with
+        that region class only; False / 0: chunked launches.  Results are identical in every mode.
         -1 (fault-path tests): persistent launches oversubscribed past residency, which fail."""
         mode = int(enable) if not isinstance(enable, bool) else int(enable)
         _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, mode), "rdq_fwi_set_persistent")
@@ -119,11 +120,13 @@ class FwiPlan:
         return int(out[0]), [int(v) for v in out[1:7]], [int(v) for v in out[16:24]]
 
     def launch_info(self, B):
-        """{'fwd_persistent', 'adj_persistent', 'fwd_T', 'adj_T', 'fwd_launches', 'adj_launches'} of a
+        """{'fwd_persistent', 'adj_persistent', 'fwd_class' / 'adj_class' (persistent region class: 16 /
+        12 / 8, 0 = chunked), 'fwd_T', 'adj_T', 'fwd_launches', 'adj_launches'} of a
         call with batch B (launches: time-loop kernel launches per call)."""
         out = (ctypes.c_int32 * 6)()
         _hip.check(self.lib.rdq_fwi_launch_info(self.handle, int(B), out), "rdq_fwi_launch_info")
-        return {"fwd_persistent": bool(out[0]), "adj_persistent": bool(out[1]), "fwd_T": int(out[2]),
+        return {"fwd_persistent": bool(out[0]), "adj_persistent": bool(out[1]),
+                "fwd_class": int(out[0]), "adj_class": int(out[1]), "fwd_T": int(out[2]),
                 "adj_T": int(out[3]), "fwd_launches": int(out[4]), "adj_launches": int(out[5])}
 
     def set_profile(self, enable):

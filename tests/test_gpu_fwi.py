@@ -164,6 +164,35 @@ def test_rows_per_wave_variants(cuda, fwd_rows, adj_rows, steps):
         assert err < 5e-6, (name, err)
 
 
+@pytest.mark.parametrize("steps", [2, 4])
+def test_region_class_16_small_surveys(cuda, steps):
+    """64 x 64 regions of 16 waves x 4 rows (rdq_fwi_set_persistent(16); the automatic choice for
+    launches of <= 200 workgroups, e.g. 1-3 OpenFWI shots): forward seismograms bit-exact vs the
+    reference and the gradient vs the oracle within the FMA build's tolerance, on the 1-shot and the
+    5-shot (two shot groups) OpenFWI cases and the wrap case (exact-order adjoint there)."""
+    for name, mode in (("fwd_openfwi_ns1", 1), ("fwd_openfwi_ns5_nt400", 16), ("fwd_wrap", 16)):
+        z = load_golden(name)
+        fwi = make_fwi(ctx_of(z))
+        v = torch.from_numpy(vnorm(z["v"])).to(cuda)
+        plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+        plan.set_tuning(steps, steps, 1)
+        plan.set_persistent(mode)
+        info = plan.launch_info(v.shape[0])
+        assert info["fwd_class"] == 16 and info["adj_class"] == 16, (name, info)
+        vg = v.clone().requires_grad_(True)
+        seis = fwi(vg)
+        plan.status()
+        assert bits_equal(seis.detach().cpu().numpy(), z["seis"]), name
+        ds = torch.from_numpy(np.sign(np.random.default_rng(5).standard_normal(z["seis"].shape)).astype(np.float32))
+        seis.backward(ds.to(cuda))
+        plan.status()
+        f = O.OracleFWI(ctx_of(z), v.shape[0])
+        _, c = f.forward(vnorm(z["v"]), keep_history=True)
+        go = f.finalize(c, *f.adjoint(c, ds.numpy()))
+        err = np.linalg.norm(vg.grad.cpu().numpy() - go) / np.linalg.norm(go)
+        assert err < (5e-6 if z["seis"].shape[2] < 1000 else 2e-5), (name, err)
+
+
 @pytest.mark.parametrize("steps,chains,persist", [(1, 1, True), (2, 1, True), (3, 1, True), (4, 1, True),
                                                   (2, 2, False), (3, 1, False), (4, 3, False)])
 @pytest.mark.parametrize("name,kw", [("fwd_small", {}), ("fwd_small_st3", dict(sample_temporal=3, sample_spatial=0.5)),
