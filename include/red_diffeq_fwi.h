@@ -96,9 +96,9 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* Rows per wave of the 64 x 96-region persistent kernels: forward 6, 8, 12 or 24 (16, 12, 8 or 4
  * waves per workgroup), adjoint (FMA build) 6, 8 or 12.  Same region geometry and results.  The time
- * step is latency-bound, so more resident waves win (configs[1], tools/ab_rw.sh): forward 6 rows
- * 1.37 ms, 8 rows 1.40, 12 rows 1.63, 24 rows 2.42; adjoint 8 rows 1.67 ms, 6 rows 1.95 (128 VGPRs:
- * spills), 12 rows 2.08.  Default 6 / 8. */
+ * step is latency-bound, so more resident waves win (configs[1], tools/ab_rw.sh, tools/ab_adj_nb6.sh):
+ * forward 6 rows 1.31 ms (barrier-free exchange), 8 rows 1.40, 12 rows 1.63, 24 rows 2.42; adjoint
+ * 6 rows 1.65 ms, 8 rows 1.67, 12 rows 2.08.  Default 6 / 6. */
 int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *plan, int32_t fwd_rows, int32_t adj_rows);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the

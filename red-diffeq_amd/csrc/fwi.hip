@@ -2232,7 +2232,8 @@ struct rdq_fwi_plan {
     // 7..8 FMA adjoint 96-row with 8 / 12 rows per wave
     int capw[13][TB_MAXT + 1] = {};   // [9] fwd 96-row x 6 rows per wave, [10] FMA adjoint 96-row x 6,
                                       // [11] / [12] fwd / FMA adjoint 64-row x 4 rows per wave (class 16)
-    int fwd_rw = 6, adj_rw = 8;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave)
+    int fwd_rw = 6, adj_rw = 6;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave;
+                                  // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
