@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=${1:-gpurun_out/r3/evidence}
 mkdir -p $O
 if [ "$2" != "notests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "pytest rc=$?"; tail -30 $O/gpu_tests.log; exit 1; }
+  RDQ_EVIDENCE_DIR=$O timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "pytest rc=$?"; tail -30 $O/gpu_tests.log; exit 1; }
   tail -1 $O/gpu_tests.log
 fi
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || exit $?
