@@ -366,7 +366,12 @@ class InversionEngine:
     def _side_stream(self, device):
         streams = self.__dict__.setdefault("_streams", {})
         if device not in streams:
-            streams[device] = torch.cuda.Stream(device=device)
+            xcds = os.environ.get("RDQ_SIDE_XCDS", "")     # e.g. "5,6,7": U-Net only on those XCDs
+            if xcds:
+                from .. import _hip
+                streams[device] = _hip.xcd_stream(device, sum(1 << int(x) for x in xcds.split(",")))
+            else:
+                streams[device] = torch.cuda.Stream(device=device)
         return streams[device]
 
     @staticmethod
