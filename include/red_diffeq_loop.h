@@ -40,13 +40,6 @@ size_t rdq_metrics_ws_bytes(int32_t B, int32_t H, int32_t W);
 int rdq_metrics(int32_t B, int32_t H, int32_t W, const float *pred, const int64_t strides[4], const float *true_norm,
                 float *out, void *ws, hipStream_t stream);
 
-/* A stream whose kernels run only on the CUs of the XCDs in xcd_mask (bit x = XCD x): a CU-masked
- * HIP stream (hipExtStreamCreateWithCUMask) built from the device's CU -> XCD map (read once per
- * device with a probe kernel on one-CU streams).  *ncus = CUs selected (nullable).  For the RED
- * loop's U-Net beside persistent FWI launches that keep their slices on the other XCDs. */
-int rdq_stream_create_on_xcds(uint32_t xcd_mask, hipStream_t *out, int32_t *ncus);
-int rdq_stream_destroy(hipStream_t stream);
-
 #ifdef __cplusplus
 }
 #endif

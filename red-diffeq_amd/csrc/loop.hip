@@ -10,8 +10,6 @@
 
 #include <cmath>
 #include <cstdint>
-#include <vector>
-#include <hip/hip_ext.h>
 
 #include "red_diffeq_loop.h"
 
@@ -150,75 +148,7 @@ __global__ void k_metrics_final(MetArgs a)
 
 }  // namespace
 
-// ---- XCD-restricted streams.  Which XCD a CU-mask bit selects is read from the device, once: for
-// every CU a one-CU stream runs a kernel whose workgroups report HW_REG_XCC_ID.
-__global__ __launch_bounds__(64) void k_xcc_id(unsigned *out)
-{
-    if (threadIdx.x == 0) {
-        unsigned x;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-        __hip_atomic_store(out + blockIdx.x, (x & 7u) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-static int cu_xcd_map(std::vector<int> &map)
-{
-    static std::vector<int> cache;
-    static int dev_cached = -1;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (dev == dev_cached) { map = cache; return 0; }
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) return -1;
-    unsigned *d = nullptr;
-    if (hipMalloc(&d, 4 * sizeof(unsigned)) != hipSuccess) return -1;
-    const int words = (cus + 31) / 32;
-    std::vector<int> m(cus, -1);
-    bool ok = true;
-    for (int i = 0; i < cus && ok; ++i) {
-        std::vector<uint32_t> mask(words, 0u);
-        mask[i / 32] = 1u << (i % 32);
-        hipStream_t s;
-        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask.data()) != hipSuccess) { ok = false; break; }
-        unsigned h[4] = {0, 0, 0, 0};
-        ok = hipMemsetAsync(d, 0, sizeof(h), s) == hipSuccess;
-        if (ok) {
-            hipLaunchKernelGGL(k_xcc_id, dim3(4), dim3(64), 0, s, d);
-            ok = hipGetLastError() == hipSuccess &&
-                 hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
-                 hipStreamSynchronize(s) == hipSuccess;
-        }
-        ok = (hipStreamDestroy(s) == hipSuccess) && ok;
-        int x = -1;
-        for (unsigned v : h)
-            if (v) { if (x >= 0 && x != (int)v - 1) x = -2; else if (x != -2) x = (int)v - 1; }
-        m[i] = x;                                  // -2: the CU bit spread over several XCDs
-    }
-    if (hipFree(d) != hipSuccess || !ok) return -1;
-    cache = m;
-    dev_cached = dev;
-    map = m;
-    return 0;
-}
-
 extern "C" {
-
-int rdq_stream_create_on_xcds(uint32_t xcd_mask, hipStream_t *out, int32_t *ncus)
-{
-    if (!out || !(xcd_mask & 0xFFu)) return RDQ_E_INVALID;
-    std::vector<int> map;
-    if (cu_xcd_map(map)) return RDQ_E_INVALID;
-    const int cus = (int)map.size(), words = (cus + 31) / 32;
-    std::vector<uint32_t> mask(words, 0u);
-    int n = 0;
-    for (int i = 0; i < cus; ++i)
-        if (map[i] >= 0 && ((xcd_mask >> map[i]) & 1u)) { mask[i / 32] |= 1u << (i % 32); ++n; }
-    if (!n) return RDQ_E_INVALID;
-    if (hipExtStreamCreateWithCUMask(out, (uint32_t)words, mask.data()) != hipSuccess) return RDQ_E_INVALID;
-    if (ncus) *ncus = n;
-    return 0;
-}
-
-int rdq_stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? 0 : RDQ_E_INVALID; }
 
 int rdq_adam_step(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq, float beta1,
                   float beta2, float eps, float step_size, float bc2_sqrt, int32_t clamp, float lo, float hi,

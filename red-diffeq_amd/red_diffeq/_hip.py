@@ -139,8 +139,6 @@ SIGNATURES = {
     "rdq_metrics_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "rdq_metrics": (c_int32, [c_int32, c_int32, c_int32, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p, c_void_p,
                               c_void_p]),
-    "rdq_stream_create_on_xcds": (c_int32, [ctypes.c_uint32, ctypes.POINTER(c_void_p), ctypes.POINTER(c_int32)]),
-    "rdq_stream_destroy": (c_int32, [c_void_p]),
 }
 
 
@@ -186,20 +184,3 @@ def stream_of(t):
 
 def ptr(t):
     return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)
-
-
-_xcd_streams = {}
-
-
-def xcd_stream(device, xcd_mask):
-    """A torch stream whose kernels run only on the XCDs of xcd_mask (bit x = XCD x; a CU-masked
-    HIP stream from rdq_stream_create_on_xcds), cached per (device, mask) for the process."""
-    device = torch.device(device)
-    key = (device.index, int(xcd_mask))
-    if key not in _xcd_streams:
-        h, n = c_void_p(), c_int32()
-        with torch.cuda.device(device):
-            check(lib().rdq_stream_create_on_xcds(int(xcd_mask), ctypes.byref(h), ctypes.byref(n)),
-                  "rdq_stream_create_on_xcds")
-        _xcd_streams[key] = (torch.cuda.ExternalStream(h.value, device=device), n.value)
-    return _xcd_streams[key][0]

@@ -250,6 +250,10 @@ class InversionEngine:
         # per-iteration histories stay on the device; ONE copy to the host after the loop (the
         # reference syncs six times per iteration, inversion.py:97-111)
         hist_dev = torch.zeros(ts, len(keys), B, dtype=torch.float32, device=self.device)
+        # (mae, rmse, ssim) -> (ssim, mae, rmse) by a device index: indexing with a Python list
+        # copies the list to the device synchronously, which held the host to the device once per
+        # iteration (the next iteration's launches then started on an idle GPU)
+        metric_order = torch.tensor([2, 0, 1], device=self.device)
 
         y = add_noise_to_seismic(y, noise_std, noise_type=noise_type, generator=None)
         y, mask = missing_trace(y, missing_number, return_mask=True, generator=None)
@@ -336,7 +340,7 @@ class InversionEngine:
 
                 with torch.no_grad():
                     row = hist_dev[it]
-                    row[3:6] = fused_metrics(mu[:, :, 1:-1, 1:-1], true_norm)[[2, 0, 1]]   # ssim, mae, rmse
+                    row[3:6] = fused_metrics(mu[:, :, 1:-1, 1:-1], true_norm).index_select(0, metric_order)
                     obs_log = loss_obs.detach()
                     if sharded:
                         obs_log = obs_log.clone()
@@ -366,12 +370,7 @@ class InversionEngine:
     def _side_stream(self, device):
         streams = self.__dict__.setdefault("_streams", {})
         if device not in streams:
-            xcds = os.environ.get("RDQ_SIDE_XCDS", "")     # e.g. "5,6,7": U-Net only on those XCDs
-            if xcds:
-                from .. import _hip
-                streams[device] = _hip.xcd_stream(device, sum(1 << int(x) for x in xcds.split(",")))
-            else:
-                streams[device] = torch.cuda.Stream(device=device)
+            streams[device] = torch.cuda.Stream(device=device)
         return streams[device]
 
     @staticmethod

@@ -1,7 +1,8 @@
 """Where the reference notebook configuration's iteration goes (CurveFault, ns = 5, nt = 1000): the
 InversionEngine loop with the diffusion regulariser (U-Net on the side stream, and with
 RDQ_NO_OVERLAP=1 serialised) against the same loop with regularization "tv" and "none" (the FWI
-floor).  python tools/notebook_floor.py [steps] -> one JSON line (ms per iteration)."""
+floor).  python tools/notebook_floor.py [steps] [regs, e.g. diffusion,none] -> one JSON line (ms per
+iteration)."""
 import json
 import os
 import sys
@@ -12,7 +13,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "red-diffeq_amd")]
 import torch  # noqa: E402
 
 
-def loop_ms(dev, reg, ns=5, steps=20, warmup=3):
+def make_loop(dev, reg, ns=5):
+    """run(ts, sync=True) -> seconds of one InversionEngine.optimize call of ts iterations."""
     from red_diffeq.core.inversion import InversionEngine
     from red_diffeq.models.diffusion import GaussianDiffusion, Unet
     from red_diffeq.solvers.pde import FWIForward
@@ -32,13 +34,20 @@ def loop_ms(dev, reg, ns=5, steps=20, warmup=3):
     reg = None if reg == "none" else reg
     eng = InversionEngine(diff, SSIM(), regularization=reg, sigma_x0=1e-4, show_progress=False)
 
-    def run(ts):
-        torch.cuda.synchronize()
+    def run(ts, sync=True):
+        if sync:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization=reg)
-        torch.cuda.synchronize()
+        if sync:
+            torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    return run
+
+
+def loop_ms(dev, reg, ns=5, steps=20, warmup=3):
+    run = make_loop(dev, reg, ns)
     run(1)
     t_w = run(warmup)
     t_all = run(warmup + steps)
@@ -48,6 +57,7 @@ def loop_ms(dev, reg, ns=5, steps=20, warmup=3):
 if __name__ == "__main__":
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda:0")
-    out = {k: loop_ms(dev, k, steps=steps) for k in ("diffusion", "tv", "none")}
+    regs = sys.argv[2].split(",") if len(sys.argv) > 2 else ("diffusion", "tv", "none")
+    out = {k: loop_ms(dev, k, steps=steps) for k in regs}
     out["env"] = {k: v for k, v in os.environ.items() if k.startswith("RDQ_")}
     print(json.dumps(out), flush=True)

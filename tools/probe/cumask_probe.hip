@@ -1,6 +1,6 @@
 // Which XCD does each CU-mask bit select?  For every CU i a stream with only bit i of the CU mask set
 // (hipExtStreamCreateWithCUMask) runs 64 one-wave workgroups that record HW_REG_XCC_ID; prints
-// "cu <i>: xcd <x> (<n> workgroups)".  Also times a 4096-workgroup kernel on a mask of whole XCDs.
+// "cu <i>: xcd <x> (<n> workgroups) per-xcd <8 counts>".
 // Build: hipcc --offload-arch=gfx950 -O3 -o cumask_probe cumask_probe.hip ; run: ./cumask_probe
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -37,7 +37,8 @@ int main()
         hipStreamSynchronize(s);
         int n = 0, x = -1, nx = 0;
         for (int k = 0; k < 8; ++k) if (h[k]) { n += h[k]; x = k; ++nx; }
-        printf("cu %d: xcd %d (%d workgroups%s)\n", i, x, n, nx > 1 ? ", several XCDs" : "");
+        printf("cu %d: xcd %d (%d workgroups%s) per-xcd %u %u %u %u %u %u %u %u\n", i, x, n, nx > 1 ? ", several XCDs" : "",
+               h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
         hipStreamDestroy(s);
     }
     hipFree(d_out);

@@ -30,12 +30,7 @@ v = v_normalize(torch.from_numpy(make_model("curvefault", 70, 70, batch=1))).to(
 plan = fwi._plan(70, 70, dev)
 sz = plan.sizes(1)
 dseis = torch.randn(1, ns, sz.nrec, plan.ng, device=dev)
-xcds = os.environ.get("RDQ_SIDE_XCDS", "")          # e.g. "5,6,7": a CU-masked side stream
-if xcds:
-    from red_diffeq import _hip  # noqa: E402
-    side = _hip.xcd_stream(dev, sum(1 << int(x) for x in xcds.split(",")))
-else:
-    side = torch.cuda.Stream(device=dev)
+side = torch.cuda.Stream(device=dev)
 main = torch.cuda.current_stream(dev)
 
 
@@ -96,7 +91,7 @@ with torch.no_grad():
         corun("forward")
         corun("adjoint")
     med = lambda xs_: sorted(xs_)[len(xs_) // 2]   # noqa: E731
-    out = {"ns": ns, "side_xcds": xcds, "info": plan.launch_info(1),
+    out = {"ns": ns, "info": plan.launch_info(1),
            "unet_alone_ms": med([unet_alone() for _ in range(7)])}
     for ph in ("forward", "adjoint"):
         r = [corun(ph) for _ in range(7)]
