@@ -232,6 +232,12 @@ template <int TAPS> struct CcCfg;
 template <> struct CcCfg<9> { static constexpr int CPS = 8, BK = 72, NA = 9, QPR = 18, NWQ = 5; };
 template <> struct CcCfg<1> { static constexpr int CPS = 64, BK = 64, NA = 8, QPR = 16, NWQ = 4; };
 constexpr int CC_BN = 64, CC_BM = 32, CC_LDA = CC_BM + 16;
+#ifndef RDQ_CC_WPOL
+#define RDQ_CC_WPOL 0          // cache policy of the implicit-GEMM conv's weight loads
+#endif
+#ifndef RDQ_CC_APOL
+#define RDQ_CC_APOL 0          // ... and of its activation loads
+#endif
 constexpr int CC_SC1 = 16;             // buffer cache policy sc1: write-through stores, L1-bypassing loads
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
@@ -326,10 +332,10 @@ __device__ __forceinline__ void conv_cc_seg(const CcArgs &a, int bx, int by, int
         const __amdgpu_buffer_rsrc_t rs = first ? rx : rx2;
 #pragma unroll
         for (int t = 0; t < NA; ++t)
-            ra[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, first ? vo1[t] : vo2[t], soff, 0));
+            ra[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, first ? vo1[t] : vo2[t], soff, RDQ_CC_APOL));
 #pragma unroll
         for (int r = 0; r < NWQ; ++r)
-            rw[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwt, vw[r], s * BK * 4, 0));
+            rw[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwt, vw[r], s * BK * 4, RDQ_CC_WPOL));
     };
     // RMS: per-pixel 1 / max(||x||, eps) from a pass over all input channels (sums of squares per
     // channel lane in channel order, combined over the 8 lanes in order), g staged in LDS
