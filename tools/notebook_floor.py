@@ -34,11 +34,21 @@ def make_loop(dev, reg, ns=5):
     reg = None if reg == "none" else reg
     eng = InversionEngine(diff, SSIM(), regularization=reg, sigma_x0=1e-4, show_progress=False)
 
+    # RDQ_MAIN_PRIO=1: the whole loop on a high-priority stream (the FWI and its serial tail ahead of
+    # the side stream's U-Net kernels at every dispatch)
+    hp = torch.cuda.Stream(device=dev, priority=-1) if os.environ.get("RDQ_MAIN_PRIO") else None
+
     def run(ts, sync=True):
         if sync:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization=reg)
+        if hp is not None:
+            hp.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(hp):
+                eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization=reg)
+            torch.cuda.current_stream(dev).wait_stream(hp)
+        else:
+            eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization=reg)
         if sync:
             torch.cuda.synchronize()
         return time.perf_counter() - t0
