@@ -2,6 +2,8 @@
 a side stream next to the forward / adjoint (5 OpenFWI shots: 5 slices on 5 XCDs, 28 of their 32
 CUs each).  Times one U-Net forward (graph replay, static I/O) alone, then started together with a
 persistent forward, then together with an adjoint, each on its own stream with HIP events.
+RDQ_CORUN_NULL=1: a graph of 114 one-workgroup kernels instead of the U-Net (same launch count, no
+work): separates dispatch interference from the U-Net's compute / memory traffic.
 python tools/unet_corun.py [ns] -> one JSON line."""
 import json
 import os
@@ -31,6 +33,21 @@ plan = fwi._plan(70, 70, dev)
 sz = plan.sizes(1)
 dseis = torch.randn(1, ns, sz.nrec, plan.ng, device=dev)
 side = torch.cuda.Stream(device=dev)
+if os.environ.get("RDQ_CORUN_NULL"):
+    tiny = torch.zeros(256, device=dev)
+    g_null = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        tiny.add_(1.0)
+        side.synchronize()
+        with torch.cuda.graph(g_null, stream=side):
+            for _ in range(114):
+                tiny.add_(1.0)
+
+    class _Null:
+        @staticmethod
+        def replay_static(*_):
+            g_null.replay()
+    net = _Null()
 main = torch.cuda.current_stream(dev)
 
 
@@ -91,7 +108,7 @@ with torch.no_grad():
         corun("forward")
         corun("adjoint")
     med = lambda xs_: sorted(xs_)[len(xs_) // 2]   # noqa: E731
-    out = {"ns": ns, "info": plan.launch_info(1),
+    out = {"ns": ns, "null": bool(os.environ.get("RDQ_CORUN_NULL")), "info": plan.launch_info(1),
            "unet_alone_ms": med([unet_alone() for _ in range(7)])}
     for ph in ("forward", "adjoint"):
         r = [corun(ph) for _ in range(7)]
