@@ -330,3 +330,34 @@ def test_metrics_vs_reference_calculator(cuda):
     np.testing.assert_allclose(out[0], z["m_mae"], rtol=1e-5)
     np.testing.assert_allclose(out[1], z["m_rmse"], rtol=1e-5)
     np.testing.assert_allclose(out[2], z["m_ssim"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("reg", ["tv", "diffusion"])
+def test_loop_has_no_per_iteration_host_sync(cuda, reg):
+    """InversionEngine.optimize enqueues its iterations without a host <-> device synchronisation:
+    under torch.cuda.set_sync_debug_mode("warn"), ts = 2 and ts = 8 report the same synchronising
+    calls (the setup's host-to-device copies and the one history read after the loop).  Indexing a
+    device tensor with a Python list (the metric reorder removed in round 3) was one such call per
+    iteration and held the next forward until the host caught up."""
+    import warnings
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden("loop_red_openfwi")
+    fwi = make_fwi(ctx_of(z))
+    eng = InversionEngine(dim8_diffusion(cuda), SSIM(window_size=11), reg, sigma_x0=1e-4, show_progress=False)
+    mu0, vt = torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"])
+    y = torch.from_numpy(z["y"]).to(cuda)
+
+    def syncs(ts):
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            torch.cuda.set_sync_debug_mode("warn")
+            try:
+                eng.optimize(mu0, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization=reg)
+            finally:
+                torch.cuda.set_sync_debug_mode(0)
+        return [f"{x.filename}:{x.lineno}" for x in w if "synchroniz" in str(x.message)]
+
+    syncs(2)                      # warm-up (graph capture, plan creation)
+    a, b = syncs(2), syncs(8)
+    assert len(a) == len(b), (a, b)
