@@ -119,6 +119,12 @@ int rdq_unet_head(const rdq_conv_desc *d, const float *x, const float *w, const 
 size_t rdq_conv2d_bf16_wpack_bytes(const rdq_conv_desc *d);
 int rdq_conv2d_bf16_pack(const rdq_conv_desc *d, const float *w, void *wp, hipStream_t stream);
 size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
+/* Process-wide U-Net kernel options (test / A-B switches; set before capturing graphs):
+ *   RDQ_UNET_OPT_BF16_PER_TAP = 1: rdq_conv2d_bf16 always runs the per-tap kernel instead of the
+ *   halo-staged 3x3 kernel (the two share the operand rounding; tests/test_gpu_unet.py compares them).
+ * Returns the previous value, or RDQ_E_INVALID for an unknown option. */
+#define RDQ_UNET_OPT_BF16_PER_TAP 1
+int rdq_unet_set_option(int32_t option, int32_t value);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 

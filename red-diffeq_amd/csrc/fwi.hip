@@ -316,7 +316,7 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
     return h;
 }
 
-// ---- Barrier-free wave-to-wave exchange of the persistent kernels (RDQ_PT_NB).
+// ---- Barrier-free wave-to-wave exchange of the persistent forward.
 // A wave's boundary rows go to LDS as 16-byte slots {row a, tag, row b, tag} (top: rows 0, 1;
 // bottom: rows R-2, R-1), double-buffered by step parity, and the neighbour waves poll their slot
 // until both tags carry the step's number: each wave waits only for the two waves it reads from,
@@ -326,12 +326,6 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
 // read both neighbours' step-n rows, which they wrote after reading its step n-1 rows (LDS
 // instructions of one wave execute in order).  Each 8-byte half carries its own tag, so a torn
 // 16-byte read is re-polled, never consumed.
-#ifndef RDQ_PT_NB_FWD
-#define RDQ_PT_NB_FWD 1                                   // forward: 1.364 -> 1.287 ms at configs[1]
-#endif
-#ifndef RDQ_PT_NB_ADJ
-#define RDQ_PT_NB_ADJ 0                                   // recurrence adjoint: 1.659 -> 1.688 ms (not used)
-#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
 template <int NW>
@@ -1014,75 +1008,6 @@ struct FwdPtArgs {
 // operation order per row).  With this pairing the vertical neighbours of pair i are pairs i-1 /
 // i+1 / i-2 / i+2 except at the slab ends, where four pairs are assembled from the halo rows.  The
 // horizontal taps stay per-row DPP lane shifts (DPP has no packed form).
-// Schedule: the step's boundary rows go to LDS, the barrier, the halo reads are issued, and then
-// the work that needs no halo row — every DPP shift, the time terms temp1 P_n - temp2 P_{n-1}, the
-// first vertical sums of the two inner pairs — runs while the reads are in flight
-// (sched_barrier pins the order; the values and their operation order are unchanged: bit-exact).
-#define FWD_STEP(CUR, PRV)                                                                          \
-    {                                                                                               \
-        xch_put<NW>(xch, n & 1, w, lane, CUR[0].x, CUR[1].x, CUR[RP - 2].y, CUR[RP - 1].y);                   \
-        __syncthreads();                                                                            \
-        const Halo4 h4 = xch_get<NW>(xch, n & 1, w, lane);                                          \
-        __builtin_amdgcn_sched_barrier(0);                                                          \
-        f32x2 xl1[RP], xr1[RP], tt[RP], la[RP];                                                         \
-        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
-            const f32x2 c = CUR[i];                                                                 \
-            xl1[i] = f32x2{dpp_shr1(c.x), dpp_shr1(c.y)};                                           \
-            xr1[i] = f32x2{dpp_shl1(c.x), dpp_shl1(c.y)};                                           \
-            f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
-            tt[i] = a1;                                                                             \
-        }                                                                                           \
-        _Pragma("unroll") for (int i = 1; i < RP - 1; ++i) {  /* inner pairs: no halo row in s1 */   \
-            f32x2 s1 = CUR[i - 1] + CUR[i + 1]; s1 = s1 + xl1[i]; s1 = s1 + xr1[i];                 \
-            la[i] = kC2 * s1;                                                                       \
-        }                                                                                           \
-        __builtin_amdgcn_sched_barrier(0);                                                          \
-        const f32x2 eU1 = {h4.u1, CUR[RP - 1].x}, eU2 = {h4.u2, CUR[RP - 2].x};  /* rows (-1,RP-1), (-2,RP-2) */ \
-        const f32x2 eD1 = {CUR[0].y, h4.d1}, eD2 = {CUR[1].y, h4.d2};  /* rows (RP,R), (RP+1,R+1) */ \
-        _Pragma("unroll") for (int i = 0; i < RP; i += RP - 1) {                                          \
-            const f32x2 m1 = i >= 1 ? CUR[i - 1] : eU1;                                             \
-            const f32x2 p1 = i <= RP - 2 ? CUR[i + 1] : eD1;                                        \
-            f32x2 s1 = m1 + p1; s1 = s1 + xl1[i]; s1 = s1 + xr1[i];                                 \
-            la[i] = kC2 * s1;                                                                       \
-        }                                                                                           \
-        _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
-            const f32x2 m2 = i >= 2 ? CUR[i - 2] : (i == 1 ? eU1 : eU2);                            \
-            const f32x2 p2 = i <= RP - 3 ? CUR[i + 2] : (i == RP - 2 ? eD1 : eD2);                  \
-            f32x2 s2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
-            s2.x = s2.x + dpp_shr1(xl1[i].x); s2.y = s2.y + dpp_shr1(xl1[i].y);                     \
-            s2.x = s2.x + dpp_shl1(xr1[i].x); s2.y = s2.y + dpp_shl1(xr1[i].y);                     \
-            const f32x2 l2 = kC3 * s2; const f32x2 lap = la[i] + l2;                                \
-            const f32x2 a3 = A[i] * lap;                                                            \
-            PRV[i] = tt[i] + a3;                                                                    \
-        }                                                                                           \
-        if (smask) {                                 /* pde.py:80-81 (uniform: source row waves) */ \
-            /* x + (-0) == x bit for bit: the other lanes add -0 instead of branching */            \
-            const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
-            if (s1row) {                             /* one source row: one packed add on its pair */ \
-                const f32x2 av = shalf ? f32x2{-0.0f, add} : f32x2{add, -0.0f};                     \
-                int sp_ = spair;                                                                    \
-                LAUNDER(sp_);                                                                       \
-                _Pragma("unroll") for (int i = 0; i < RP; ++i)                                       \
-                    if (i == sp_) PRV[i] = PRV[i] + av;                                             \
-            } else {                                                                                \
-                unsigned sm_ = smask;                                                               \
-                LAUNDER(sm_);                                                                       \
-                _Pragma("unroll") for (int r = 0; r < R; ++r)                                       \
-                    if ((sm_ >> r) & 1u) PT_AT(PRV, r) = PT_AT(PRV, r) + add;                       \
-            }                                                                                       \
-        }                                                                                           \
-        /* history: own cells, issued at once; the epoch's last step is stored after the hand-off   \
-           sweep (FWD_HIST_LAST): on gfx9 vmcnt counts stores, so the sweep's granule loads would   \
-           otherwise wait for them */                                                               \
-        if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
-        if (rrow >= 0) {                             /* receiver row: value kept, stored per epoch */ \
-            int rp_ = rpair;                                                                        \
-            LAUNDER(rp_);                                                                           \
-            f32x2 v_ = PRV[0];                                                                      \
-            _Pragma("unroll") for (int i = 1; i < RP; ++i) if (i == rp_) v_ = PRV[i];                \
-            rv[t] = rhalf ? v_.y : v_.x;                                                            \
-        }                                                                                           \
-    }
 #define FWD_HIST(V, N)                                                                              \
     {                                                                                               \
         const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)((N) + 2) * L + so, slice_bytes); \
@@ -1123,10 +1048,10 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
     const f32x2 m2 = (i) >= 2 ? X[(i) - 2] : ((i) == 1 ? E1 : E2);                                  \
     const f32x2 p2 = (i) <= RP - 3 ? X[(i) + 2] : ((i) == RP - 2 ? swp(X[RP - 1]) : swp(X[RP - 2]));
 
-// Barrier-free forward step (RDQ_PT_NB): the halo-free work of every pair (DPP shifts, time
+// Barrier-free forward step: the halo-free work of every pair (DPP shifts, time
 // terms) first, then the wait for the neighbours' boundary rows, the two boundary pairs, their
 // publication for the next step, and the interior pairs after it.  Per row the operations and
-// their order are FWD_STEP's (bit-exact).
+// their order are the reference's (bit-exact).
 #define FWD_PAIRS_NB(CUR, PRV, LO, HI)                                                                        \
     {                                                                                               \
         _Pragma("unroll") for (int i = (LO); i < (HI); ++i) {                                        \
@@ -1189,12 +1114,9 @@ template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
-    constexpr bool PT_MIR = RDQ_PT_NB_FWD != 0;
-#if RDQ_PT_NB_FWD
+    constexpr bool PT_MIR = true;                         // mirrored pairs (barrier-free exchange:
+                                                          // 1.364 -> 1.287 ms at configs[1])
     __shared__ u32x4 xq[2][NW][2][64];
-#else
-    __shared__ float xch[2][NW][4][64];
-#endif
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
@@ -1248,14 +1170,10 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
 #define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
-#if RDQ_PT_NB_FWD
     xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
     __syncthreads();
     xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // P_0 = 0, step 0's tag
 #define FWD_STEP_SEL FWD_STEP_NB
-#else
-#define FWD_STEP_SEL FWD_STEP
-#endif
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
         PT_PROF(tsw)
@@ -1280,10 +1198,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
             FWD_ISSUE                                     // (before the stores: 1.32 -> 1.375 ms, not used)
-#if RDQ_PT_NB_FWD
             // the next step's boundary rows, with the halo cells the sweep reloaded
             xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
-#endif
         }
         FWD_RECORD
     }
@@ -1301,7 +1217,6 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         }
     }
 }
-#undef FWD_STEP
 // The adjoint keeps the forward's row-pair packing (PT_AT(V, r) = V[r % RP][r / RP]): every add /
 // mul / fma of the step and of the gradient is one v_pk_*_f32 for two rows.
 
@@ -1579,10 +1494,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 // epoch: P_k, P_{k-1}, P_{k-2} = Q[t], Q[t+1], Q[t+2] mod 4, prefetch into Q[t+3]): no copies for
 // T = 4; other depths restore the order once per epoch.
 
-#ifdef RDQ_EXP_NOHIST   // timing experiment only (wrong results): no history loads in the adjoint
-#define ADJR_LOAD(PD, HR, SOFF)                                                                     \
-    { _Pragma("unroll") for (int i = 0; i < RP; ++i) PD[i] = PD[i] * A[i]; }
-#else
 #define ADJR_LOAD(PD, HR, SOFF)                                                                     \
     {                                                                                               \
         const int so_ = (SOFF);                                                                     \
@@ -1591,7 +1502,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             PD[i].y = bload_nt(HR, pr[PT_MIR ? R - 1 - i : i + RP], so_);                           \
         }                                                                                           \
     }
-#endif
 
 // gradient of step k (CU = L_{k+1}, LN = L_k; wavelet sample WK = w[k-1]; window P0 = P_k,
 // P1 = P_{k-1}, P2 = P_{k-2}), in two halves: PRE forms d = 2c1 P_{k-1} + lap'(P_{k-1}) from the
@@ -1639,7 +1549,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 
 // one adjoint step k: CUR = L_{k+1}, PRV = L_{k+2} -> L_k; window P0 / P1 / P2 as ADJR_GRAD;
 // history slot k-2 (the next step's P_{k-3}) prefetched into PN.  (Moving the gradient's history
-// half between the barrier and the halo reads' use, as FWD_STEP does with its halo-free work,
+// half between the barrier and the halo reads' use, as the forward does with its halo-free work,
 // needs 8 more VGPRs than the 168 that 3 waves / SIMD allow: it spilled and ran 2.6x slower.)
 #define ADJR_STEP(CUR, PRV, P0, P1, P2, PN)                                                         \
     {                                                                                               \
@@ -1670,58 +1580,13 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
     }
 
-// Barrier-free adjoint step (RDQ_PT_NB, mirrored pairs): wait for the neighbours' A L_{k+1} rows,
-// the boundary pairs of L_k (receiver residual included), their A L_k published for the next step,
-// then the interior pairs and the gradient.  Per row the operations are ADJR_STEP's.
-#define ADJR_PAIRS_NB(CUR, PRV, LO, HI)                                                                       \
-    {                                                                                               \
-        _Pragma("unroll") for (int i = (LO); i < (HI); ++i) {                                        \
-            MIR_VERT(q, i, m1, p1, m2, p2)                                                          \
-            const f32x2 c = q[i];                                                                   \
-            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
-            f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
-            f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
-            n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
-            n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
-            const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
-            PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
-        }                                                                                           \
-        if ((HI) > (LO) && rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: receiver wave */ \
-            int rp_ = rpair;                                                                        \
-            LAUNDER(rp_);                                                                           \
-            const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
-            _Pragma("unroll") for (int i = (LO); i < (HI); ++i) if (i == rp_) PRV[i] = PRV[i] + dv_; \
-        }                                                                                           \
-    }
-#define ADJR_STEP_NB(CUR, PRV, P0, P1, P2, PN)                                                      \
-    {                                                                                               \
-        if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
-        const float dcur = dv[t];                                                                   \
-        u32x4 xu_, xd_;                                                                             \
-        xq_load<NW>(xq, j & 1, w, lane, xu_, xd_);                                                  \
-        f32x2 q[RP];                                                                                \
-        _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
-        const Halo4 h4 = xq_wait<NW>(xq, j & 1, w, lane, (unsigned)j + 1u, xu_, xd_, a.status, live); \
-        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
-        ADJR_PAIRS_NB(CUR, PRV, 0, 2)                                                                         \
-        if (t + 1 < T) {                                                                            \
-            const f32x2 qa = A[0] * PRV[0], qb = A[1] * PRV[1];                                     \
-            xq_put<NW>(xq, (j + 1) & 1, w, lane, (unsigned)j + 2u, qa.x, qb.x, qb.y, qa.y);         \
-        }                                                                                           \
-        ADJR_PAIRS_NB(CUR, PRV, 2, RP)                                                                        \
-        if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
-    }
-
 template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
-    constexpr bool PT_MIR = RDQ_PT_NB_ADJ != 0;
-#if RDQ_PT_NB_ADJ
-    __shared__ u32x4 xq[2][NW][2][64];
-#else
+    constexpr bool PT_MIR = false;                        // stacked pairs {i, i+RP}; the adjoint keeps the
+                                                          // barrier (barrier-free form: 1.659 -> 1.688 ms)
     __shared__ float xch[2][NW][4][64];
-#endif
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
@@ -1792,14 +1657,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
-#if RDQ_PT_NB_ADJ
-    xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
-    __syncthreads();
-    xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // A L_{nt+1} = 0, step 0's tag
-#define ADJR_STEP_SEL ADJR_STEP_NB
-#else
 #define ADJR_STEP_SEL ADJR_STEP
-#endif
     for (int e = 0; e < nep; ++e) {
         const int ke = a.nt - e * T;                      // first step k of this epoch
         const bool last = e + 1 == nep;
@@ -1830,13 +1688,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             PT_PROF(tpb)
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             ADJ_ISSUE
-#if RDQ_PT_NB_ADJ
-            {   // the next step's boundary rows of A L_{k+1}, with the halo cells the sweep reloaded
-                const int jn = (e + 1) * T;
-                const f32x2 qa = A[0] * L1[0], qb = A[1] * L1[1];
-                xq_put<NW>(xq, jn & 1, w, lane, (unsigned)jn + 1u, qa.x, qb.x, qb.y, qa.y);
-            }
-#endif
             PT_PROF(tsw)
         }
         if constexpr ((T & 3) != 0) {   // restore Q0 = the next epoch's P_k
@@ -1882,8 +1733,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + tile] = red[0];
 }
 #undef ADJR_STEP
-#undef ADJR_STEP_NB
-#undef ADJR_PAIRS_NB
 #undef FWD_STEP_NB
 #undef FWD_PAIRS_NB
 #undef MIR_VERT

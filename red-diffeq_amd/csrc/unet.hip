@@ -2896,12 +2896,22 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d)
     return S > 1 ? (size_t)S * d->B * d->H * d->W * d->cout * sizeof(float) : 0;
 }
 
+static int g_bf16_per_tap = 0;   // RDQ_UNET_OPT_BF16_PER_TAP
+
+int rdq_unet_set_option(int32_t option, int32_t value)
+{
+    if (option != RDQ_UNET_OPT_BF16_PER_TAP) return RDQ_E_INVALID;
+    const int old = g_bf16_per_tap;
+    g_bf16_per_tap = value != 0;
+    return old;
+}
+
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
 {
     if (!conv_desc_ok(d) || !x || !wp || !y || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
         return RDQ_E_INVALID;
-    if (conv3_ok(d) && !getenv("RDQ_NO_CONV3")) {
+    if (conv3_ok(d) && !g_bf16_per_tap) {
         C3Args c{};
         c.d = *d; c.x = x; c.x2 = x2; c.w = static_cast<const __bf16 *>(wp); c.bias = bias; c.res = residual; c.y = y;
         c.cinp = bf_cinp(d);

@@ -110,9 +110,10 @@ class _FaultMonitor:
         return self.global_word if self.sharded else self.local_word()
 
     def record(self, it):
-        self.host[it:it + 1].copy_(self.guard(), non_blocking=True)
+        g = self.guard()
+        self.host[it:it + 1].copy_(g, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(g.device))   # the stream the copy was issued on
         self.events[it] = ev
 
     def first_fault(self, upto):
@@ -181,7 +182,7 @@ class _Progress:
             self.host[it, n:n + 1].copy_(time_tensor.float().mean().reshape(1), non_blocking=True)
             self.has_t = True
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(row.device))   # the copies' stream, not the current device's
         self.events[it] = ev
 
     def show(self, pbar, it, B):

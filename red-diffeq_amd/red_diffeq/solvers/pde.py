@@ -69,6 +69,8 @@ class FwiPlan:
             _hip.check(self.lib.rdq_fwi_plan_create(ctypes.byref(g), ctypes.byref(h)), "rdq_fwi_plan_create")
         self.handle = h
         self._sizes = {}
+        self.persist_mode = 1                      # rdq_fwi_set_persistent mode (the C default: auto)
+        self._saved_mode = None                    # mode before fallback_to_chunked (None: not fallen back)
         # status words in torch memory (caller-owned, rdq_fwi_set_status_buffer): word 0 != 0 once a
         # persistent launch gave up; read stream-ordered (Adam guard, async host copies)
         self.status_t = torch.zeros(64, dtype=torch.int32, device=device)
@@ -94,8 +96,8 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_rows_per_wave(self, fwd_rows, adj_rows):
-        """Rows per wave of the 64 x 96-region persistent kernels (forward 8 / 12 / 24, adjoint 8 / 12);
-        results are the same for every choice."""
+        """Rows per wave of the 64 x 96-region persistent kernels (forward 6 / 8 / 12 / 24, adjoint
+        6 / 8 / 12; 6 is the default for both); results are the same for every choice."""
         _hip.check(self.lib.rdq_fwi_set_rows_per_wave(self.handle, int(fwd_rows), int(adj_rows)),
                    "rdq_fwi_set_rows_per_wave")
 
@@ -106,6 +108,7 @@ class FwiPlan:
         -1 (fault-path tests): persistent launches oversubscribed past residency, which fail."""
         mode = int(enable) if not isinstance(enable, bool) else int(enable)
         _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, mode), "rdq_fwi_set_persistent")
+        self.persist_mode = mode
 
     def status(self, stream=None):
         """Synchronise and raise if a persistent launch's neighbour hand-off timed out."""
@@ -288,16 +291,25 @@ class FWIForward(nn.Module):
 
     def fallback_to_chunked(self):
         """After a persistent-launch failure: every plan runs the chunked (non-resident) kernels until
-        restore_persistent(), and the status words are cleared (stream-ordered)."""
+        restore_persistent(), and the status words are cleared (stream-ordered).  Each plan's mode
+        is saved once (a second fallback before the restore keeps the first saved mode)."""
         for plan in self._plans.values():
+            if plan._saved_mode is None:
+                plan._saved_mode = plan.persist_mode
             plan.set_persistent(False)
             plan.status_t.zero_()
 
     def restore_persistent(self):
         """Back to the persistent kernels (where they fit) after fallback_to_chunked(): the engine
-        re-promotes after a number of clean iterations (core/inversion.py _FaultMonitor)."""
+        re-promotes after a number of clean iterations (core/inversion.py _FaultMonitor).  Each plan
+        gets back the mode it had before the fallback: a plan pinned to the chunked kernels (0) or to
+        one region class (8 / 12 / 16) keeps it; the fault-path test mode (-1) comes back as auto (1)."""
         for plan in self._plans.values():
-            plan.set_persistent(True)
+            mode = plan._saved_mode
+            if mode is None:
+                continue                           # never fell back: nothing to restore
+            plan._saved_mode = None
+            plan.set_persistent(1 if mode == -1 else mode)
 
     def coefficients(self, v):
         """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""

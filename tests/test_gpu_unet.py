@@ -360,8 +360,8 @@ def test_conv_bf16_concat_residual_upsample_unshuffle(cuda):
 def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
     """The halo-staged 3x3 kernel (batched U-Net sizes, >= 512 tiles of 256 pixels x 64 channels):
     against the fp32 torch conv of the bf16-rounded operands, and against the per-tap bf16 kernel
-    (RDQ_NO_CONV3) with which it shares the operand rounding."""
-    import os
+    (rdq_unet_set_option(RDQ_UNET_OPT_BF16_PER_TAP)) with which it shares the operand rounding."""
+    from red_diffeq import _hip
     from red_diffeq.models import unet_ops as ops
     F = torch.nn.functional
     torch.manual_seed(14)
@@ -373,11 +373,11 @@ def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
     md = ops.UPSAMPLE2 if mode == "up" else ops.PLAIN
     with ops.precision("bf16"):
         got = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
-        os.environ["RDQ_NO_CONV3"] = "1"
+        assert _hip.lib().rdq_unet_set_option(1, 1) == 0          # RDQ_UNET_OPT_BF16_PER_TAP
         try:
             per_tap = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
         finally:
-            del os.environ["RDQ_NO_CONV3"]
+            _hip.lib().rdq_unet_set_option(1, 0)
     xin = R.upsample_nearest2(a) if mode == "up" else (torch.cat((a, b), 1) if cin2 else a)
     ref = F.conv2d(_bf(xin), _bf(conv.weight), conv.bias, padding=1) + (r if res else 0)
     close(got, ref, rel=2e-5)

@@ -317,3 +317,44 @@ def test_bench_launches_n_ranks_itself(monkeypatch):
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_fallback_restores_each_plans_own_persistent_mode():
+    """re-promotion after a persistent fault puts back every plan's own mode.  A plan
+    pinned to the chunked kernels stays chunked, a plan pinned to one region class keeps it, and the
+    fault-path test mode (-1) comes back as auto (1).  Stub plans: only set_persistent / status_t are
+    touched, so no GPU is needed."""
+    from red_diffeq.solvers.pde import FWIForward, FwiPlan
+
+    class Stub:
+        def __init__(self, mode):
+            self.persist_mode, self._saved_mode, self.status_t = mode, None, torch.ones(4)
+            self.calls = []
+
+        set_persistent = FwiPlan.set_persistent
+
+        @property
+        def lib(self):
+            stub = self
+
+            class L:
+                def rdq_fwi_set_persistent(self, h, mode):
+                    stub.calls.append(mode)
+                    return 0
+            return L()
+
+        handle = None
+
+    ctx = dict(n_grid=70, ns=2, ng=70, dx=10.0, nt=200, nbc=20, f=15.0, dt=0.001, sz=10, gz=10)
+    fwi = FWIForward(ctx, torch.device("cpu"))
+    pinned, failing, cls12 = Stub(0), Stub(-1), Stub(12)
+    fwi._plans = {"a": pinned, "b": failing, "c": cls12}
+    fwi.fallback_to_chunked()
+    fwi.fallback_to_chunked()                  # a second fault before the restore keeps the saved modes
+    assert [p.persist_mode for p in (pinned, failing, cls12)] == [0, 0, 0]
+    assert all(float(p.status_t.sum()) == 0 for p in (pinned, failing, cls12))
+    fwi.restore_persistent()
+    assert [p.persist_mode for p in (pinned, failing, cls12)] == [0, 1, 12]
+    assert all(p._saved_mode is None for p in (pinned, failing, cls12))
+    fwi.restore_persistent()                   # nothing saved: no change
+    assert [p.persist_mode for p in (pinned, failing, cls12)] == [0, 1, 12]
