@@ -89,10 +89,14 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
  *                          cancellation is not fp32-accurate (5e-3 at nbc = 4);
  *   RDQ_VARIANT_NO_XCD_LOCAL the persistent kernels publish every neighbour hand-off write-through
  *                          (sc1) instead of keeping whole slices on one XCD (read from HW_REG_XCC_ID)
- *                          with L2-resident hand-offs (identical results; slower). */
+ *                          with L2-resident hand-offs (identical results; slower);
+ *   RDQ_VARIANT_NARROW_CHUNKED the chunked (non-resident) kernels run 64-column regions, one column
+ *                          per lane, instead of 128-column regions of two columns per lane
+ *                          (identical results; more halo traffic). */
 #define RDQ_VARIANT_FWD_GEN 1
 #define RDQ_VARIANT_ADJ_EXACT 2
 #define RDQ_VARIANT_NO_XCD_LOCAL 4
+#define RDQ_VARIANT_NARROW_CHUNKED 8
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* Rows per wave of the 64 x 96-region persistent kernels: forward 6, 8, 12 or 24 (16, 12, 8 or 4
  * waves per workgroup), adjoint (FMA build) 6, 8 or 12.  Same region geometry and results.  The time

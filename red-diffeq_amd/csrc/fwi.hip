@@ -327,6 +327,8 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
 // instructions of one wave execute in order).  Each 8-byte half carries its own tag, so a torn
 // 16-byte read is re-polled, never consumed.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
 template <int NW>
 __device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
@@ -714,6 +716,343 @@ __global__ __launch_bounds__(64 * TB_NW, 4) void k_adj_tb(AdjTBArgs a)
     }
     if (tid == 0) a.gk_part[(size_t)bs * a.nblk + ti.tile] += red[0];
 }
+
+// --------------------------------------------------------------------------------------- K1/K2
+// Chunked kernels on WIDE regions (configs[4]-size grids; the default chunked layout).  A region is
+// 128 columns x NW*R rows: every lane holds TWO adjacent columns {2l, 2l+1} of R rows as one f32x2
+// per row, so every add / mul of the stencil is one packed v_pk_*_f32 for two cells, and the
+// horizontal taps of a column pair need four DPP lane shifts (x-1 of column 2l is lane l-1's .y, x-2
+// its .x; x+1 of column 2l+1 is lane l+1's .x, x+2 its .y) instead of four per cell.  The region's
+// halo H = 2T is then 16 of 128 columns instead of 16 of 64: a tile re-reads (128 x RH) / (112 x IH)
+// of what it stores instead of (64 x 64) / (48 x 48), and its 512-B rows span 4-5 128-B lines per
+// 112 owned columns instead of 3 per 48 (profiles/r3: the 64-column adjoint moved 1.34x its
+// algorithmic bytes at configs[4]).  Same per-cell operations in the same order as k_fwd_tb /
+// k_adj_tb (bit-exact with them and with the oracle).  PAIR (even Wp): a lane's two columns are
+// adjacent in memory, one 8-byte access; odd Wp wraps a pair across the domain edge, two 4-byte ones.
+constexpr int TW_W = 128;                // wide region columns (two per lane)
+
+template <bool PAIR, int CP = 0>
+__device__ __forceinline__ f32x2 ld2(__amdgpu_buffer_rsrc_t r, int v0, int v1, int soff)
+{
+    if constexpr (PAIR) {
+        const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, v0, soff, CP);
+        return f32x2{__uint_as_float(x.x), __uint_as_float(x.y)};
+    } else {
+        return f32x2{__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, v0, soff, CP)),
+                     __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, v1, soff, CP))};
+    }
+}
+template <bool PAIR, int CP = 0>
+__device__ __forceinline__ void st2(f32x2 v, __amdgpu_buffer_rsrc_t r, int v0, int v1, int soff)
+{
+    if constexpr (PAIR) {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(v.x), __float_as_uint(v.y)}, r, v0, soff, CP);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, v0, soff, CP);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, v1, soff, CP);
+    }
+}
+
+// the four horizontal taps of a column pair c = {x, x+1} (lane shifts; region edges read 0)
+struct HTaps { f32x2 l1, r1, l2, r2; };
+__device__ __forceinline__ HTaps htaps(f32x2 c)
+{
+    const float sx = dpp_shr1(c.x), sy = dpp_shr1(c.y), lx = dpp_shl1(c.x), ly = dpp_shl1(c.y);
+    HTaps h;
+    h.l1 = f32x2{sy, c.x}; h.r1 = f32x2{c.y, lx};
+    h.l2 = f32x2{sx, sy};  h.r2 = f32x2{lx, ly};
+    return h;
+}
+
+// boundary rows 0, 1, R-2, R-1 of every wave through LDS; rows -2, -1, R, R+1 of this wave back
+struct Halo2 { f32x2 u2, u1, d1, d2; };
+template <int NW, int R>
+__device__ __forceinline__ void tw_put(f32x2 (*x)[NW][4][64], int buf, int w, int lane, const f32x2 *v)
+{
+    x[buf][w][0][lane] = v[0]; x[buf][w][1][lane] = v[1];
+    x[buf][w][2][lane] = v[R - 2]; x[buf][w][3][lane] = v[R - 1];
+}
+template <int NW>
+__device__ __forceinline__ Halo2 tw_get(f32x2 (*x)[NW][4][64], int buf, int w, int lane)
+{
+    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;   // (edge waves: halo rows)
+    Halo2 h;
+    h.u2 = x[buf][wu][2][lane]; h.u1 = x[buf][wu][3][lane];
+    h.d1 = x[buf][wd][0][lane]; h.d2 = x[buf][wd][1][lane];
+    return h;
+}
+#define TW_VERT(ARR, r, H2, m2, m1, p1, p2)                                       \
+    const f32x2 m2 = (r) >= 2 ? ARR[(r) - 2] : ((r) == 1 ? H2.u1 : H2.u2);        \
+    const f32x2 m1 = (r) >= 1 ? ARR[(r) - 1] : H2.u1;                            \
+    const f32x2 p1 = (r) + 1 < R ? ARR[(r) + 1] : H2.d1;                         \
+    const f32x2 p2 = (r) + 2 < R ? ARR[(r) + 2] : ((r) + 2 == R ? H2.d1 : H2.d2);
+
+// Region geometry shared by the wide kernels (flat locals: uniform values stay SGPRs).
+#define TW_REGION_INIT()                                                                           \
+    constexpr int H = 2 * T, IW = TW_W - 2 * H, RH = NW * R, IH = RH - 2 * H;                      \
+    const TBGeo &g = a.g;                                                                          \
+    const int lane = threadIdx.x & 63;                                                             \
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                                \
+    const TileId ti = decode_tile(blockIdx.x, g.tiles_x, g.ntiles, g.B * g.ns_grp);                \
+    if (!ti.valid) return;                                          /* whole workgroup: uniform */ \
+    const int b = ti.sl / g.ns_grp, s = g.s_off + (ti.sl - b * g.ns_grp), bs = b * g.ns + s;       \
+    const int ux = ti.tx * IW - H + 2 * lane;                       /* unwrapped column of .x */   \
+    const int gx0 = wrapn(ux, g.Wp), gx1 = wrapn(ux + 1, g.Wp);                                    \
+    const bool lin = lane >= H / 2 && lane < 64 - H / 2;            /* interior lane (both cols) */\
+    const bool xin0 = lin && ux < g.Wp, xin1 = lin && ux + 1 < g.Wp;                               \
+    const int uz0 = ti.ty * IH - H + w * R;                                                        \
+    const size_t so = (size_t)bs * g.slice;                                                        \
+    const int sbytes = (int)(g.slice * 4);                                                         \
+    const int v0 = gx0 * 4, v1 = gx1 * 4;                           /* lane byte offsets in a row */\
+    const int vi0 = xin0 ? v0 : OOB, vi1 = xin1 ? v1 : OOB;         /* own (interior) cells only */\
+    int rofs[R];                                                    /* wave-uniform gz * ld */     \
+    unsigned rin = 0;                                               /* wave-uniform interior rows */\
+    _Pragma("unroll") for (int r = 0; r < R; ++r) {                                                \
+        const int uz = uz0 + r;                                                                    \
+        rofs[r] = wrapn(uz, g.Hp) * g.ld;                                                          \
+        const int rr = w * R + r;                                                                  \
+        if (rr >= H && rr < RH - H && uz < g.Hp) rin |= 1u << r;                                   \
+    }
+
+template <int T, int NW, int R, bool GEN, bool PAIR>
+__global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
+{
+    __shared__ f32x2 xch[2][NW][4][64];
+    TW_REGION_INIT()
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    f32x2 A[R], C1[R], C2v[R], P0[R], P1[R];
+    unsigned smask = 0;
+    int rrow = -1;
+    {
+        const __amdgpu_buffer_rsrc_t RPv = rsrc_of(a.in_prev + so, sbytes), RCu = rsrc_of(a.in_cur + so, sbytes);
+        const __amdgpu_buffer_rsrc_t RA = rsrc_of(AL, sbytes), R1 = rsrc_of(AL + g.cstride, sbytes),
+                                     R2 = rsrc_of(AL + 2 * g.cstride, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int gz = wrapn(uz0 + r, g.Hp);
+            if constexpr (GEN) {   // regenerated from the 20 KB-per-row model (L2-resident) instead of 3 fields
+                const Coef c0 = gen_coef(a.cg, b, gz, gx0), c1 = gen_coef(a.cg, b, gz, gx1);
+                A[r] = f32x2{c0.al, c1.al}; C1[r] = f32x2{c0.t1, c1.t1}; C2v[r] = f32x2{c0.t2, c1.t2};
+            } else {
+                A[r] = ld2<PAIR>(RA, v0, v1, rofs[r] * 4);
+                C1[r] = ld2<PAIR>(R1, v0, v1, rofs[r] * 4);
+                C2v[r] = ld2<PAIR>(R2, v0, v1, rofs[r] * 4);
+            }
+            P0[r] = ld2<PAIR>(RPv, v0, v1, rofs[r] * 4);
+            P1[r] = ld2<PAIR>(RCu, v0, v1, rofs[r] * 4);
+            if (gz == g.isz) smask |= 1u << r;          // (tiny domains: a wave can hold the row twice)
+            if (gz == g.igz) rrow = r;
+        }
+    }
+    const int isx = g.isx[s];
+    const bool sc0 = gx0 == isx, sc1 = gx1 == isx;
+    const float bsrc = smask ? a.coeffs[4 * g.cstride + (size_t)b * g.slice + (size_t)g.isz * g.ld + isx] : 0.0f;
+    // receivers of the lane's two columns (usually one each), read once
+    int rs0 = 0, re0 = 0, rs1 = 0, re1 = 0;
+    if (rrow >= 0) { rs0 = g.rcv_start[gx0]; re0 = g.rcv_start[gx0 + 1]; rs1 = g.rcv_start[gx1]; re1 = g.rcv_start[gx1 + 1]; }
+    const int rc0 = xin0 && rs0 < re0 ? g.rcv_list[rs0] : -1, rc1 = xin1 && rs1 < re1 ? g.rcv_list[rs1] : -1;
+    const bool rmulti = __any(re0 - rs0 > 1 || re1 - rs1 > 1);   // wave-uniform
+    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {       // exactly T steps (the host launches a shorter tail as its own T)
+        f32x2 *cur = (t & 1) ? P0 : P1;     // P_{n+t}
+        f32x2 *prv = (t & 1) ? P1 : P0;     // P_{n+t-1} -> P_{n+t+1}
+        tw_put<NW, R>(xch, t & 1, w, lane, cur);
+        __syncthreads();
+        const Halo2 h2 = tw_get<NW>(xch, t & 1, w, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            TW_VERT(cur, r, h2, zm2, zm1, zp1, zp2)
+            const f32x2 c = cur[r];
+            const HTaps x = htaps(c);
+            // pde.py:79, reference evaluation order per cell
+            f32x2 s1 = zm1 + zp1; s1 = s1 + x.l1; s1 = s1 + x.r1;
+            f32x2 s2 = zm2 + zp2; s2 = s2 + x.l2; s2 = s2 + x.r2;
+            f32x2 lap = kC2 * s1; const f32x2 l2 = kC3 * s2; lap = lap + l2;
+            f32x2 a1 = C1[r] * c; const f32x2 a2 = C2v[r] * prv[r]; a1 = a1 - a2;
+            const f32x2 a3 = A[r] * lap;
+            prv[r] = a1 + a3;
+        }
+        if (smask) {                                                   // pde.py:80-81
+            const float add = bsrc * a.w[t];
+            const f32x2 av = {sc0 ? add : -0.0f, sc1 ? add : -0.0f};   // x + (-0) == x bit for bit
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (smask & (1u << r)) prv[r] = prv[r] + av;
+        }
+        const int n = a.n0 + t;
+        if (a.hist) {
+            const __amdgpu_buffer_rsrc_t HS = rsrc_of(a.hist + (size_t)(n + 2) * g.level + so, sbytes);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (rin & (1u << r)) st2<PAIR, CP_NT>(prv[r], HS, vi0, vi1, rofs[r] * 4);   // streaming
+        }
+        if (rrow >= 0 && (rin & (1u << rrow)) && (n % g.st) == 0) {   // pde.py:82-83
+            f32x2 val = prv[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) if (r == rrow) val = prv[r];
+            float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;
+            if (rc0 >= 0) SK[rc0] = val.x;
+            if (rc1 >= 0) SK[rc1] = val.y;
+            if (rmulti) {
+                if (xin0) for (int j = rs0 + 1; j < re0; ++j) SK[g.rcv_list[j]] = val.x;
+                if (xin1) for (int j = rs1 + 1; j < re1; ++j) SK[g.rcv_list[j]] = val.y;
+            }
+        }
+    }
+    if (a.out_cur) {   // ring path: keep the last two levels
+        constexpr bool odd = (T & 1) != 0;      // after T steps the newest level is in P0 if odd
+        const __amdgpu_buffer_rsrc_t OC = rsrc_of(a.out_cur + so, sbytes), OP = rsrc_of(a.out_prev + so, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (rin & (1u << r)) {
+                st2<PAIR>(odd ? P0[r] : P1[r], OC, vi0, vi1, rofs[r] * 4);
+                st2<PAIR>(odd ? P1[r] : P0[r], OP, vi0, vi1, rofs[r] * 4);
+            }
+    }
+}
+
+// Adjoint on wide regions, the oracle's exact operation order (k_adj_tb's per-cell arithmetic):
+//   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
+//   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k)
+//   gbeta[s] += L_k(src) w[k-1]           (own cells; gA loaded and stored once per launch)
+template <int T, int NW, int R, bool PAIR>
+__global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
+{
+    __shared__ f32x2 xq[2][NW][4][64];
+    __shared__ f32x2 xp[2][NW][4][64];
+    TW_REGION_INIT()
+    const float *AL = a.coeffs + (size_t)b * g.slice;
+    f32x2 A[R], KP[R], L0[R], L1[R], GA[R];   // temp1 / temp2 re-derived per step (bit-identical)
+    unsigned pmask = 0, smask = 0, rmask = 0;            // wave-uniform row masks
+    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2}, k2 = {2.0f, 2.0f}, k1 = {1.0f, 1.0f};
+    {
+        const __amdgpu_buffer_rsrc_t RA = rsrc_of(AL, sbytes), RK = rsrc_of(AL + 3 * g.cstride, sbytes);
+        const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(a.in_l1 + so, sbytes), RL2 = rsrc_of(a.in_l2 + so, sbytes);
+        const __amdgpu_buffer_rsrc_t RG = rsrc_of(a.gA + so, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int gz = wrapn(uz0 + r, g.Hp);
+            A[r] = ld2<PAIR>(RA, v0, v1, rofs[r] * 4);
+            KP[r] = ld2<PAIR>(RK, v0, v1, rofs[r] * 4);
+            L1[r] = ld2<PAIR>(RL1, v0, v1, rofs[r] * 4);   // L_{k+1}
+            L0[r] = ld2<PAIR>(RL2, v0, v1, rofs[r] * 4);   // L_{k+2}
+            GA[r] = (rin & (1u << r)) ? ld2<PAIR>(RG, vi0, vi1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+            const int rr = w * R + r;
+            if (rr >= H - 2 && rr < RH - H + 2) pmask |= 1u << r;
+            if (gz == g.isz) smask |= 1u << r;
+            if (gz == g.igz) rmask |= 1u << r;
+        }
+    }
+    const int isx = g.isx[s];
+    const bool sc0 = xin0 && gx0 == isx, sc1 = xin1 && gx1 == isx;   // the source cell is an own cell
+    const int rcv0 = rmask ? g.rlane[gx0] : -1, rcv1 = rmask ? g.rlane[gx1] : -1;
+    const __amdgpu_buffer_rsrc_t DSR = rsrc_of(a.dseis + (size_t)bs * g.nrec * g.dstride);
+    const bool gbl = (smask & rin) && (sc0 || sc1);
+    float gbacc = gbl ? a.gbeta[bs] : 0.0f;
+    double ksum = 0.0;
+    // history P_{k-1} on the rows whose stencil the interior needs, prefetched one step ahead
+    f32x2 Pn[R];
+    {
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, v0, v1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {       // exactly T steps (the host launches a shorter tail as its own T)
+        __builtin_amdgcn_sched_barrier(0);  // no step's work moved into another (live ranges: no spills)
+        const int k = a.k0 - t;
+        f32x2 *cur = (t & 1) ? L0 : L1;     // L_{k+1}
+        f32x2 *prv = (t & 1) ? L1 : L0;     // L_{k+2} -> L_k
+        f32x2 P[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) P[r] = Pn[r];
+        if (t + 1 < T) {
+            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(k - 1) * g.level + so, sbytes);
+#pragma unroll
+            for (int r = 0; r < R; ++r) if (pmask & (1u << r)) Pn[r] = ld2<PAIR>(HR, v0, v1, rofs[r] * 4);
+        }
+        // this step's receiver residuals, loaded before the stencil so their latency hides under it
+        const bool rstep = rmask && ((k - 1) % g.st) == 0;   // wave-uniform
+        f32x2 dsv = {-0.0f, -0.0f};
+        if (rstep) {
+            const int ro = ((k - 1) / g.st) * g.dstride;
+            const float d0 = bload(DSR, rcv0 >= 0 ? (ro + rcv0) * 4 : OOB, 0);
+            const float d1 = bload(DSR, rcv1 >= 0 ? (ro + rcv1) * 4 : OOB, 0);
+            dsv = f32x2{rcv0 >= 0 ? d0 : -0.0f, rcv1 >= 0 ? d1 : -0.0f};
+        }
+        f32x2 q[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) q[r] = A[r] * cur[r];
+        tw_put<NW, R>(xq, t & 1, w, lane, q);
+        tw_put<NW, R>(xp, t & 1, w, lane, P);
+        __syncthreads();
+        const Halo2 hq = tw_get<NW>(xq, t & 1, w, lane);
+        const Halo2 hp = tw_get<NW>(xp, t & 1, w, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            TW_VERT(q, r, hq, qm2, qm1, qp1, qp2)
+            const HTaps x = htaps(q[r]);
+            f32x2 n1 = qm1 + qp1; n1 = n1 + x.l1; n1 = n1 + x.r1;
+            f32x2 n2 = qm2 + qp2; n2 = n2 + x.l2; n2 = n2 + x.r2;
+            f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;
+            f32x2 t1 = kC1X2 * A[r]; t1 = t1 + k2; t1 = t1 - KP[r];      // pde.py:69
+            const f32x2 t2 = k1 - KP[r];                                  // pde.py:70
+            f32x2 l = t1 * cur[r]; const f32x2 l2 = t2 * prv[r]; l = l - l2; l = l + nb;
+            prv[r] = l;
+        }
+        if (rstep) {                            // adjoint of the receiver sampling
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (rmask & (1u << r)) prv[r] = prv[r] + dsv;      // -0 on lanes without a receiver
+        }
+        // gradient accumulators (own cells are the ones stored; halo lanes compute and discard)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!(rin & (1u << r))) continue;   // wave-uniform
+            TW_VERT(P, r, hp, pm2, pm1, pp1, pp2)
+            const f32x2 pc = P[r];
+            const HTaps x = htaps(pc);
+            f32x2 s1 = pm1 + pp1; s1 = s1 + x.l1; s1 = s1 + x.r1;
+            f32x2 s2 = pm2 + pp2; s2 = s2 + x.l2; s2 = s2 + x.r2;
+            f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;
+            f32x2 d = kC1X2 * pc; d = d + lap;
+            const f32x2 l = prv[r];
+            const f32x2 c = l * d;
+            GA[r] = GA[r] + c;
+            f32x2 kk = KP[r] * pc; const f32x2 dl = cur[r] - l; kk = kk * dl;   // fp32 term, fp64 sum
+            ksum += xin0 ? (double)kk.x : 0.0;
+            ksum += xin1 ? (double)kk.y : 0.0;
+            if ((smask & (1u << r)) && (sc0 || sc1)) { const float gb = (sc0 ? l.x : l.y) * a.w[t]; gbacc = gbacc + gb; }
+        }
+    }
+    {
+        constexpr bool odd = (T & 1) != 0;      // newest level (L_{k0-T+1}) is in L0 if odd
+        const __amdgpu_buffer_rsrc_t O1 = rsrc_of(a.out_l1 + so, sbytes), O2 = rsrc_of(a.out_l2 + so, sbytes);
+        const __amdgpu_buffer_rsrc_t RG = rsrc_of(a.gA + so, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (rin & (1u << r)) {
+                st2<PAIR>(odd ? L0[r] : L1[r], O1, vi0, vi1, rofs[r] * 4);
+                st2<PAIR>(odd ? L1[r] : L0[r], O2, vi0, vi1, rofs[r] * 4);
+                st2<PAIR>(GA[r], RG, vi0, vi1, rofs[r] * 4);
+            }
+    }
+    if (gbl) a.gbeta[bs] = gbacc;
+    // deterministic workgroup reduction of the sponge-coefficient partial sum (LDS of the exchange)
+    double *red = reinterpret_cast<double *>(&xq[0][0][0][0]);
+    __syncthreads();
+    const int tid = threadIdx.x;
+    red[tid] = ksum;
+    __syncthreads();
+    for (int w2 = 32 * NW; w2 > 0; w2 >>= 1) {
+        if (tid < w2) red[tid] += red[tid + w2];
+        __syncthreads();
+    }
+    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + ti.tile] += red[0];
+}
+#undef TW_VERT
+#undef TW_REGION_INIT
 
 // --------------------------------------------------------------------------------------- K1/K2
 // Persistent variants: ONE launch runs the whole time loop.  Every workgroup keeps its region
@@ -2087,6 +2426,7 @@ struct rdq_fwi_plan {
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
+    bool wide = true;           // chunked kernels on 128-column regions (k_fwd_tw / k_adj_tw) vs 64-column
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;
     std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins
@@ -2099,8 +2439,6 @@ namespace {
 int tiles_x(int Wp, int T) { return (Wp + (64 - 4 * T) - 1) / (64 - 4 * T); }
 int tiles_y(int Hp, int T) { return (Hp + (TB_RH - 4 * T) - 1) / (TB_RH - 4 * T); }
 
-// gk_part is sized for the smallest tile interior (T = TB_MAXT): most workgroups
-int adj_blocks(const rdq_fwi_plan *p) { return tiles_x(p->Wp, TB_MAXT) * tiles_y(p->Hp, TB_MAXT); }
 
 TBGeo tb_geo(const rdq_fwi_plan *p, int B)
 {
@@ -2200,6 +2538,54 @@ void launch_adj(int T, dim3 grid, hipStream_t st, const Args &a)
     }
 }
 
+// wide chunked regions: forward 16 waves x 8 rows (128 x 128), adjoint 16 waves x 4 rows (128 x 64:
+// its seven two-column fields per row fill the 128 VGPRs of a 1024-thread workgroup)
+constexpr int TW_FWD_NW = 16, TW_FWD_R = 8, TW_ADJ_NW = 16, TW_ADJ_R = 4;
+int tw_tiles_x(int Wp, int T) { return (Wp + (TW_W - 4 * T) - 1) / (TW_W - 4 * T); }
+int tw_tiles_y(int Hp, int T, bool adj)
+{
+    const int ih = (adj ? TW_ADJ_NW * TW_ADJ_R : TW_FWD_NW * TW_FWD_R) - 4 * T;
+    return (Hp + ih - 1) / ih;
+}
+
+template <int TT>
+void launch_fwd_w_T(bool gen, bool pair, dim3 grid, hipStream_t st, const FwdTBArgs &a)
+{
+    const dim3 blk(64 * TW_FWD_NW);
+    if (gen) {
+        if (pair) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_tw<TT, TW_FWD_NW, TW_FWD_R, true, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_tw<TT, TW_FWD_NW, TW_FWD_R, true, false>), grid, blk, 0, st, a);
+    } else {
+        if (pair) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_tw<TT, TW_FWD_NW, TW_FWD_R, false, true>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_tw<TT, TW_FWD_NW, TW_FWD_R, false, false>), grid, blk, 0, st, a);
+    }
+}
+void launch_fwd_w(int T, bool gen, bool pair, dim3 grid, hipStream_t st, const FwdTBArgs &a)
+{
+    switch (T) {
+    case 1: launch_fwd_w_T<1>(gen, pair, grid, st, a); break;
+    case 2: launch_fwd_w_T<2>(gen, pair, grid, st, a); break;
+    case 3: launch_fwd_w_T<3>(gen, pair, grid, st, a); break;
+    default: launch_fwd_w_T<4>(gen, pair, grid, st, a); break;
+    }
+}
+template <int TT>
+void launch_adj_w_T(bool pair, dim3 grid, hipStream_t st, const AdjTBArgs &a)
+{
+    const dim3 blk(64 * TW_ADJ_NW);
+    if (pair) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, false>), grid, blk, 0, st, a);
+}
+void launch_adj_w(int T, bool pair, dim3 grid, hipStream_t st, const AdjTBArgs &a)
+{
+    switch (T) {
+    case 1: launch_adj_w_T<1>(pair, grid, st, a); break;
+    case 2: launch_adj_w_T<2>(pair, grid, st, a); break;
+    case 3: launch_adj_w_T<3>(pair, grid, st, a); break;
+    default: launch_adj_w_T<4>(pair, grid, st, a); break;
+    }
+}
+
 // Workgroups of a persistent kernel the device holds at once (occupancy query x CUs).
 template <class K>
 int resident_capacity(K kernel, int nthreads, int &cache)
@@ -2257,6 +2643,24 @@ unsigned pt_tiles_padded(const rdq_fwi_plan *p, int T, int NW)
     const int ih = region_rows(NW) - 4 * T;
     const int nt_ = tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih);
     return (unsigned)((nt_ + 7) / 8 * 8);
+}
+
+// Per-(model, shot) slots of the sponge-term partials gk_part: one per tile of whichever kernel runs
+// the adjoint (persistent classes, narrow or wide chunked, every depth T), sized to the largest tile
+// count over all of them, so no region shape can outgrow the buffer the caller allocated
+// (rdq_fwi_sizes) and the finalize sums (k_fin_rows: unused slots stay zero).
+int gk_blocks(const rdq_fwi_plan *p)
+{
+    int n = 0;
+    for (int T = 1; T <= TB_MAXT; ++T) {
+        n = std::max(n, tiles_x(p->Wp, T) * tiles_y(p->Hp, T));                  // narrow chunked (64 x 64)
+        n = std::max(n, tw_tiles_x(p->Wp, T) * tw_tiles_y(p->Hp, T, true));      // wide chunked (128 x 64)
+        for (int NW : {8, 12, 16}) {                                             // persistent region classes
+            const int ih = region_rows(NW) - 4 * T;
+            n = std::max(n, tiles_x(p->Wp, T) * ((p->Hp + ih - 1) / ih));
+        }
+    }
+    return n;
 }
 
 // Shots per persistent launch: every slice of one launch must be resident at once, so a survey
@@ -2447,7 +2851,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.g = tb_geo(p, B);
     const int T = p->adj_T;
     const size_t L = a.g.level;
-    const int nblk_alloc = adj_blocks(p);
+    const int nblk_alloc = gk_blocks(p);
     if (int e = zero_regions({{ring, 4 * L * sizeof(unsigned long long)}, {gA, L * sizeof(float)},
                               {gk, (size_t)B * p->g.ns * nblk_alloc * sizeof(double)},
                               {gbeta, (size_t)B * p->g.ns * sizeof(float)}, {p->d_status + 16, 8 * sizeof(unsigned)}},
@@ -2491,12 +2895,14 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
-        a.g.tiles_x = tiles_x(p->Wp, T);
-        a.g.ntiles = a.g.tiles_x * tiles_y(p->Hp, T);
-        const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
         for (int n0 = 0, i = 0; n0 < nt; n0 += T, ++i) {
             a.n0 = n0;
             a.nsteps = std::min(T, nt - n0);
+            // tile grid of this launch's depth (the wide kernels run a short tail as its own T)
+            const int Tl = p->wide ? a.nsteps : T;
+            a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
+            a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, false) : tiles_y(p->Hp, Tl));
+            const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
             if (hist) {
                 a.in_prev = hist + (size_t)n0 * L;          // slot n0   = P_{n0-1}
@@ -2509,7 +2915,8 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
                 a.out_prev = ring + (size_t)(2 * pout) * L;
                 a.out_cur = ring + (size_t)(2 * pout + 1) * L;
             }
-            launch_fwd(T, p->fwd_gen, grid, cs, a);
+            if (p->wide) launch_fwd_w(a.nsteps, p->fwd_gen, (p->Wp & 1) == 0, grid, cs, a);   // (tail: T' < T)
+            else launch_fwd(T, p->fwd_gen, grid, cs, a);
         }
     }
     RDQ_CHECK(hipGetLastError());
@@ -2523,7 +2930,7 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     a.g = tb_geo(p, B);
     const size_t L = a.g.level;
     const int T = p->adj_T, S = chain_count(p), ns = p->g.ns;
-    const int nblk_alloc = adj_blocks(p);
+    const int nblk_alloc = gk_blocks(p);
     RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
     RDQ_CHECK(hipMemsetAsync(gA, 0, L * sizeof(float), st));
     RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * ns * nblk_alloc * sizeof(double), st));
@@ -2535,19 +2942,21 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
-        a.g.tiles_x = tiles_x(p->Wp, T);
-        a.g.ntiles = a.g.tiles_x * tiles_y(p->Hp, T);
-        const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
         for (int k0 = p->g.nt, i = 0; k0 >= 1; k0 -= T, ++i) {
             a.k0 = k0;
             a.nsteps = std::min(T, k0);
+            const int Tl = p->wide ? a.nsteps : T;
+            a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
+            a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
+            const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
             const int pin = i & 1, pout = pin ^ 1;
             a.in_l1 = ring + (size_t)(2 * pin) * L;
             a.in_l2 = ring + (size_t)(2 * pin + 1) * L;
             a.out_l1 = ring + (size_t)(2 * pout) * L;
             a.out_l2 = ring + (size_t)(2 * pout + 1) * L;
-            launch_adj(T, grid, cs, a);
+            if (p->wide) launch_adj_w(a.nsteps, (p->Wp & 1) == 0, grid, cs, a);   // (tail: T' < T)
+            else launch_adj(T, grid, cs, a);
         }
     }
     RDQ_CHECK(hipGetLastError());
@@ -2726,17 +3135,19 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
 
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
-    if (!p || (flags & ~7)) return RDQ_E_INVALID;
+    if (!p || (flags & ~15)) return RDQ_E_INVALID;
     const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0;
     const bool fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0 && recurrence_ok(p);
     const int xcd = (flags & RDQ_VARIANT_NO_XCD_LOCAL) ? 0 : 1;
-    if (p->fwd_gen != gen || p->adj_fma != fma || p->xcd_mode != xcd) {
+    const bool wide = (flags & RDQ_VARIANT_NARROW_CHUNKED) == 0;
+    if (p->fwd_gen != gen || p->adj_fma != fma || p->xcd_mode != xcd || p->wide != wide) {
         drop_graphs(p);
         p->cache.clear();
     }
     p->fwd_gen = gen;
     p->adj_fma = fma;
     p->xcd_mode = xcd;
+    p->wide = wide;
     return 0;
 }
 
@@ -2860,7 +3271,7 @@ int rdq_fwi_sizes(const rdq_fwi_plan *p, int32_t B, rdq_fwi_sizes_t *o)
     o->ring = 4 * (size_t)B * ns * slice * sizeof(unsigned long long);
     if (p->rmulti) o->ring += (size_t)B * ns * p->nrec * p->ncolr * sizeof(float);   // folded residuals
     o->gA = (size_t)B * ns * slice * sizeof(float);
-    o->gk_part = (size_t)B * ns * adj_blocks(p) * sizeof(double);
+    o->gk_part = (size_t)B * ns * gk_blocks(p) * sizeof(double);
     o->gbeta = (size_t)B * ns * sizeof(float);
     o->colsum = (size_t)B * p->Hp * p->g.nx * sizeof(double);
     return 0;
@@ -2945,7 +3356,7 @@ int rdq_fwi_grad_finalize(const rdq_fwi_plan *p, int32_t B, const float *coeffs,
     vstat_ptrs(vstat, B, &vmin, &amin);
     FinArgs a;
     a.B = B; a.ns = p->g.ns; a.nz = p->g.nz; a.nx = p->g.nx; a.nbc = p->g.nbc; a.Hp = p->Hp; a.Wp = p->Wp;
-    a.ld = p->ld; a.isz = p->g.isz; a.nblk = adj_blocks(p); a.dt = p->g.dt; a.dx = p->g.dx;
+    a.ld = p->ld; a.isz = p->g.isz; a.nblk = gk_blocks(p); a.dt = p->g.dt; a.dx = p->g.dx;
     a.scale = vel_mode == 0 ? 1500.0 : 1.0;
     a.slice = (size_t)p->Hp * p->ld; a.cstride = (size_t)B * a.slice;
     a.coeffs = coeffs; a.gA = gA; a.gbeta = gbeta; a.vmin = vmin; a.amin = amin; a.gk_part = gk;

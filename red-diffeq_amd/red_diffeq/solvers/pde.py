@@ -88,11 +88,13 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
-    def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True):
+    def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True, wide_chunked=True):
         """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
         the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction; xcd_local:
-        persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs."""
-        flags = (1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
+        persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs;
+        wide_chunked: chunked kernels on 128-column regions (two columns per lane) instead of 64."""
+        flags = ((1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
+                 | (0 if wide_chunked else 8))
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_rows_per_wave(self, fwd_rows, adj_rows):

@@ -1,7 +1,8 @@
 """configs[4] (Marmousi-scale) FWI propagator timing on one MI355X: a 500 x 3000 synthetic model
 (740 x 3240 padded, Npad = 2,397,600), `--ns` shots per GPU (16 = 128 shots sharded 8-way), ng = nx
 receivers, nt = 1000, store-all history (16 shots: 155 GB of HBM).  One launch of this size does not
-fit resident on the chip, so the chunked temporal-blocked kernels (k_fwd_tb / k_adj_tb) run it.
+fit resident on the chip, so the chunked temporal-blocked kernels (k_fwd_tw / k_adj_tw; --narrow:
+k_fwd_tb / k_adj_tb) run it.
 
 Prints one JSON line per blocking depth: forward / adjoint ms, shot-timesteps/s, algorithmic GB/s
 (12·Npad B per forward shot-step, 16·Npad B per adjoint shot-step).
@@ -27,6 +28,7 @@ ap.add_argument("--nx", type=int, default=3000)
 ap.add_argument("--nt", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--T", type=str, default="2,3,4", help="blocking depths to time")
+ap.add_argument("--narrow", action="store_true", help="64-column chunked regions (round-3 layout)")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
 a = ap.parse_args()
@@ -35,7 +37,7 @@ ctx = dict(n_grid=a.nx, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=1
 fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
 v = v_normalize(torch.from_numpy(make_model("curvefault", a.nz, a.nx, batch=1))).to(dev)
 plan = fwi._plan(a.nz, a.nx, dev)
-plan.set_variant(fwd_gen_coeffs=not a.no_gen)
+plan.set_variant(fwd_gen_coeffs=not a.no_gen, wide_chunked=not a.narrow)
 sz = plan.sizes(1)
 npad = sz.Hp * sz.Wp
 dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
@@ -61,7 +63,7 @@ for T in [int(t) for t in a.T.split(",")]:
     plan.status()
     f, d = min(fw), min(ad)
     shot_steps = a.ns * a.nt
-    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
                       "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
                       "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
                       "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
