@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-sample-reps", type=int, default=12,
                    help="repetitions of the CPU sample gradient (~10 s of host work at the defaults)")
     p.add_argument("--no-red", action="store_true", help="skip the configs[2] RED-DiffEq loop timing")
+    p.add_argument("--no-configs4", action="store_true", help="skip the configs[4] per-rank RED iteration")
     return p.parse_args()
 
 
@@ -188,6 +189,89 @@ def rank_workload_rate(dev, a, nsl, family):
     return {"workload": f"configs[3] per-rank share: CurveFault-B, {nsl} of {nsl * 8} shots, nt={nt}, one GPU, "
                         "no all-reduce", "ms_per_step": round(dt * 1e3, 4),
             "shot_timesteps_per_s": round(nsl * nt / dt, 1), "kernels": fwi._plan(70, 70, dev).launch_info(1)}
+
+
+def configs4_rank_workload(dev, a, nsl=16, ns_total=128, nz=500, nx=3000, iters=3):
+    """One rank's share of configs[4] on this GPU: a Marmousi-size 500 x 3000 model (740 x 3240 padded),
+    16 of the 128 shots (the 8-way sharding's per-GPU share), nt = 1000, one RED-DiffEq iteration of the
+    drop-in InversionEngine (HIP forward + adjoint on the chunked wide-region kernels, the 2-D tiled patch
+    regulariser as ONE bf16 U-Net call over every tile, Adam + clamp + metrics).  Random-init U-Net
+    (reference architecture), synthetic model; the other ranks' observed shots are zeros (never read on
+    this rank).  Also the forward / adjoint alone (HIP events) against their algorithmic bytes, and the
+    peak HBM allocated."""
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.models.diffusion import GaussianDiffusion, Unet
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import prepare_initial_model, s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.ssim import SSIM
+    from red_diffeq.utils.synthetic import make_model
+    torch.manual_seed(8888)
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
+    nt = a.nt
+    ctx = dict(n_grid=nx, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=nx, ns=ns_total)
+    fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none, shots=(0, nsl))
+    vt = torch.from_numpy(make_model("curvefault", nz, nx, seed=8888, batch=1))
+    with torch.no_grad():
+        y_loc = fwi(v_normalize(vt).to(dev))
+    y = torch.zeros(1, ns_total, y_loc.shape[2], y_loc.shape[3], device=dev)
+    y[:, :nsl] = y_loc
+    del y_loc
+    mu = torch.nn.functional.pad(prepare_initial_model(vt, "smoothed", sigma=10.0), (1, 1, 1, 1))
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1)
+    diff = GaussianDiffusion(net, image_size=72, timesteps=1000, sampling_timesteps=250,
+                             objective="pred_noise").to(dev)
+    net.set_precision("bf16")
+    eng = InversionEngine(diff, SSIM(), regularization="diffusion", sigma_x0=1e-4, show_progress=False)
+
+    def run(ts):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.optimize(mu, vt, y, fwi, ts=ts, lr=0.03, reg_lambda=0.75, regularization="diffusion")
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(1)                        # plans, buffers and graph captures outside the timing
+    t_w = run(1)
+    t_all = run(1 + iters)
+    ms = (t_all - t_w) / iters * 1e3
+    fwi.check()
+    # the time loops alone, HIP events on the stream the kernels are launched on
+    plan = fwi._plan(nz, nx, dev)
+    sz = plan.sizes(1)
+    npad = sz.Hp * sz.Wp
+    v_in = v_normalize(vt).to(dev)
+    dseis = torch.randn(1, nsl, sz.nrec, plan.ng, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fw, ad = [], []
+    for _ in range(2):
+        coeffs, vstat = plan.coeffs(v_in, 0)
+        ev[0].record()
+        seis, hist = plan.forward(coeffs, 1, keep_history=True)
+        ev[1].record()
+        plan.adjoint(coeffs, hist, dseis, 1)
+        ev[2].record()
+        torch.cuda.synchronize()
+        del hist, seis
+        fw.append(ev[0].elapsed_time(ev[1]))
+        ad.append(ev[1].elapsed_time(ev[2]))
+    plan.status()
+    f, d = min(fw), min(ad)
+    shot_steps = nsl * nt
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9
+    info = plan.launch_info(1)
+    del eng, diff, net, fwi, plan, y, dseis
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[4] per-rank share: {nz}x{nx} model ({sz.Hp}x{sz.Wp} padded), {nsl} of {ns_total} "
+                        f"shots, nt={nt}, one RED-DiffEq iteration (fwd+adj + 2-D tiled bf16 U-Net regulariser + "
+                        "Adam + metrics), one GPU, no all-reduce",
+            "ms_per_iter": round(ms, 2), "shot_timesteps_per_s": round(shot_steps / (ms * 1e-3), 1),
+            "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+            "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
+            "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
+            "fwd_frac_alg": round(12 * npad * shot_steps / f / 1e6 / HBM_PEAK_GBS, 4),
+            "adj_frac_alg": round(16 * npad * shot_steps / d / 1e6 / HBM_PEAK_GBS, 4),
+            "peak_hbm_allocated_GB": round(peak_gb, 1), "kernels": info}
 
 
 def launch_ranks(a):
@@ -463,6 +547,8 @@ def main():
                         "configuration), random-init U-Net", "ms_per_iter": p_ms,
             "reference_ms_per_iter": 2250.0, "reference_hw": "RTX 3090 (BASELINE.md §1)",
             "speedup_vs_reference": round(2250.0 / p_ms, 1)}
+    if world == 1 and a.ns is None and not a.no_configs4:
+        out["configs4_rank_workload"] = configs4_rank_workload(dev, a)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, vtrue[:1], a.cpu_sample_shots, a.cpu_sample_reps)
     if rank == 0:

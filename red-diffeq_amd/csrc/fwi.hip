@@ -329,6 +329,7 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
 template <int NW>
 __device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
@@ -547,6 +548,7 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
 
 struct AdjTBArgs {
     TBGeo g;
+    CoefGen cg;                          // model + sponge amplitude (wide kernels regenerate alpha / kappa)
     const float *coeffs;                 // K3 fields: alpha, temp1, temp2, kappa at 0..3 x cstride
     const float *in_l1, *in_l2;          // L_{k0+1}, L_{k0+2}
     float *out_l1, *out_l2;              // L_{k0-nsteps+1}, L_{k0-nsteps+2}
@@ -912,37 +914,52 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
     }
 }
 
-// Adjoint on wide regions, the oracle's exact operation order (k_adj_tb's per-cell arithmetic):
+// Adjoint on wide regions (k_adj_tb's per-cell arithmetic):
 //   L_k = T1 L_{k+1} - T2 L_{k+2} + (c2 N1(A L_{k+1}) + c3 N2(A L_{k+1})) [+ R^T dseis[k-1]]
 //   gA_s += L_k (2c1 P_{k-1} + c2 S1(P_{k-1}) + c3 S2(P_{k-1})),  gk += (K P_{k-1})(L_{k+1} - L_k)
 //   gbeta[s] += L_k(src) w[k-1]           (own cells; gA loaded and stored once per launch)
-template <int T, int NW, int R, bool PAIR>
+// EXACT: the oracle's fp32 operation order (bitwise gA / gbeta).  Else the same stencils with FMA
+// contraction (fp32-level tolerance: rdq_fwi_set_variant without RDQ_VARIANT_ADJ_EXACT, nbc >= 20).
+// Every gk term is summed in fp64 in both.  alpha and kappa are
+// regenerated from the model in registers (gen_coef, bit-identical to K3's fields): the 16 shots of a
+// tile then read the L2-resident 6 MB model instead of two padded fields each.  Loads are issued in
+// the order the first step uses them (alpha's model values and L_{k+1} first).
+template <int T, int NW, int R, bool PAIR, bool EXACT>
 __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
 {
     __shared__ f32x2 xq[2][NW][4][64];
     __shared__ f32x2 xp[2][NW][4][64];
     TW_REGION_INIT()
-    const float *AL = a.coeffs + (size_t)b * g.slice;
     f32x2 A[R], KP[R], L0[R], L1[R], GA[R];   // temp1 / temp2 re-derived per step (bit-identical)
     unsigned pmask = 0, smask = 0, rmask = 0;            // wave-uniform row masks
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2}, k2 = {2.0f, 2.0f}, k1 = {1.0f, 1.0f};
+    f32x2 Pn[R];
     {
-        const __amdgpu_buffer_rsrc_t RA = rsrc_of(AL, sbytes), RK = rsrc_of(AL + 3 * g.cstride, sbytes);
         const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(a.in_l1 + so, sbytes), RL2 = rsrc_of(a.in_l2 + so, sbytes);
         const __amdgpu_buffer_rsrc_t RG = rsrc_of(a.gA + so, sbytes);
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, sbytes);
+        int gz[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int gz = wrapn(uz0 + r, g.Hp);
-            A[r] = ld2<PAIR>(RA, v0, v1, rofs[r] * 4);
-            KP[r] = ld2<PAIR>(RK, v0, v1, rofs[r] * 4);
-            L1[r] = ld2<PAIR>(RL1, v0, v1, rofs[r] * 4);   // L_{k+1}
-            L0[r] = ld2<PAIR>(RL2, v0, v1, rofs[r] * 4);   // L_{k+2}
-            GA[r] = (rin & (1u << r)) ? ld2<PAIR>(RG, vi0, vi1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+            gz[r] = wrapn(uz0 + r, g.Hp);
             const int rr = w * R + r;
             if (rr >= H - 2 && rr < RH - H + 2) pmask |= 1u << r;
-            if (gz == g.isz) smask |= 1u << r;
-            if (gz == g.igz) rmask |= 1u << r;
+            if (gz[r] == g.isz) smask |= 1u << r;
+            if (gz[r] == g.igz) rmask |= 1u << r;
         }
+        Coef c0[R], c1[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) { c0[r] = gen_coef(a.cg, b, gz[r], gx0); c1[r] = gen_coef(a.cg, b, gz[r], gx1); }
+#pragma unroll
+        for (int r = 0; r < R; ++r) L1[r] = ld2<PAIR>(RL1, v0, v1, rofs[r] * 4);   // L_{k+1}
+#pragma unroll
+        for (int r = 0; r < R; ++r) L0[r] = ld2<PAIR>(RL2, v0, v1, rofs[r] * 4);   // L_{k+2}
+#pragma unroll
+        for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, v0, v1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < R; ++r) GA[r] = (rin & (1u << r)) ? ld2<PAIR>(RG, vi0, vi1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < R; ++r) { A[r] = f32x2{c0[r].al, c1[r].al}; KP[r] = f32x2{c0[r].kp, c1[r].kp}; }
     }
     const int isx = g.isx[s];
     const bool sc0 = xin0 && gx0 == isx, sc1 = xin1 && gx1 == isx;   // the source cell is an own cell
@@ -950,14 +967,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(a.dseis + (size_t)bs * g.nrec * g.dstride);
     const bool gbl = (smask & rin) && (sc0 || sc1);
     float gbacc = gbl ? a.gbeta[bs] : 0.0f;
-    double ksum = 0.0;
-    // history P_{k-1} on the rows whose stencil the interior needs, prefetched one step ahead
-    f32x2 Pn[R];
-    {
-        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, sbytes);
-#pragma unroll
-        for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, v0, v1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
-    }
+    double ksum = 0.0;                   // every gk term in fp64
 #pragma unroll
     for (int t = 0; t < T; ++t) {       // exactly T steps (the host launches a shorter tail as its own T)
         __builtin_amdgcn_sched_barrier(0);  // no step's work moved into another (live ranges: no spills)
@@ -967,16 +977,16 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
         f32x2 P[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) P[r] = Pn[r];
-        if (t + 1 < T) {
+        if (t + 1 < T) {   // history P_{k-2} of the next step, on the rows the interior's stencil needs
             const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(k - 1) * g.level + so, sbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) if (pmask & (1u << r)) Pn[r] = ld2<PAIR>(HR, v0, v1, rofs[r] * 4);
         }
         // this step's receiver residuals, loaded before the stencil so their latency hides under it
-        const bool rstep = rmask && ((k - 1) % g.st) == 0;   // wave-uniform
+        const int ri = rmask ? rec_index(k - 1, g.st) : -1;   // wave-uniform
         f32x2 dsv = {-0.0f, -0.0f};
-        if (rstep) {
-            const int ro = ((k - 1) / g.st) * g.dstride;
+        if (ri >= 0) {
+            const int ro = ri * g.dstride;
             const float d0 = bload(DSR, rcv0 >= 0 ? (ro + rcv0) * 4 : OOB, 0);
             const float d1 = bload(DSR, rcv1 >= 0 ? (ro + rcv1) * 4 : OOB, 0);
             dsv = f32x2{rcv0 >= 0 ? d0 : -0.0f, rcv1 >= 0 ? d1 : -0.0f};
@@ -995,13 +1005,19 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
             const HTaps x = htaps(q[r]);
             f32x2 n1 = qm1 + qp1; n1 = n1 + x.l1; n1 = n1 + x.r1;
             f32x2 n2 = qm2 + qp2; n2 = n2 + x.l2; n2 = n2 + x.r2;
-            f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;
-            f32x2 t1 = kC1X2 * A[r]; t1 = t1 + k2; t1 = t1 - KP[r];      // pde.py:69
-            const f32x2 t2 = k1 - KP[r];                                  // pde.py:70
-            f32x2 l = t1 * cur[r]; const f32x2 l2 = t2 * prv[r]; l = l - l2; l = l + nb;
-            prv[r] = l;
+            if constexpr (EXACT) {
+                f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;
+                f32x2 t1 = kC1X2 * A[r]; t1 = t1 + k2; t1 = t1 - KP[r];      // pde.py:69
+                const f32x2 t2 = k1 - KP[r];                                  // pde.py:70
+                f32x2 l = t1 * cur[r]; const f32x2 l2 = t2 * prv[r]; l = l - l2; l = l + nb;
+                prv[r] = l;
+            } else {
+                const f32x2 nb = fma2(kC3, n2, kC2 * n1);
+                const f32x2 t1 = fma2(kC1X2, A[r], k2) - KP[r], t2 = k1 - KP[r];
+                prv[r] = fma2(t1, cur[r], fma2(-t2, prv[r], nb));
+            }
         }
-        if (rstep) {                            // adjoint of the receiver sampling
+        if (ri >= 0) {                          // adjoint of the receiver sampling
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (rmask & (1u << r)) prv[r] = prv[r] + dsv;      // -0 on lanes without a receiver
@@ -1015,14 +1031,23 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
             const HTaps x = htaps(pc);
             f32x2 s1 = pm1 + pp1; s1 = s1 + x.l1; s1 = s1 + x.r1;
             f32x2 s2 = pm2 + pp2; s2 = s2 + x.l2; s2 = s2 + x.r2;
-            f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;
-            f32x2 d = kC1X2 * pc; d = d + lap;
             const f32x2 l = prv[r];
-            const f32x2 c = l * d;
-            GA[r] = GA[r] + c;
-            f32x2 kk = KP[r] * pc; const f32x2 dl = cur[r] - l; kk = kk * dl;   // fp32 term, fp64 sum
-            ksum += xin0 ? (double)kk.x : 0.0;
-            ksum += xin1 ? (double)kk.y : 0.0;
+            const f32x2 dl = cur[r] - l;
+            if constexpr (EXACT) {
+                f32x2 lap = kC2 * s1; const f32x2 lq = kC3 * s2; lap = lap + lq;
+                f32x2 d = kC1X2 * pc; d = d + lap;
+                const f32x2 c = l * d;
+                GA[r] = GA[r] + c;
+                f32x2 kk = KP[r] * pc; kk = kk * dl;                      // fp32 term, fp64 sum
+                ksum += xin0 ? (double)kk.x : 0.0;
+                ksum += xin1 ? (double)kk.y : 0.0;
+            } else {
+                const f32x2 d = fma2(kC1X2, pc, fma2(kC3, s2, kC2 * s1));
+                GA[r] = fma2(l, d, GA[r]);
+                const f32x2 kk = (KP[r] * pc) * dl;                    // fp32 term, fp64 sum (the total
+                ksum += (double)(xin0 ? kk.x : 0.0f);                   //  cancels: fp32 partials lost
+                ksum += (double)(xin1 ? kk.y : 0.0f);                   //  1.3e-4 of it at OpenFWI)
+            }
             if ((smask & (1u << r)) && (sc0 || sc1)) { const float gb = (sc0 ? l.x : l.y) * a.w[t]; gbacc = gbacc + gb; }
         }
     }
@@ -1039,17 +1064,19 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
             }
     }
     if (gbl) a.gbeta[bs] = gbacc;
-    // deterministic workgroup reduction of the sponge-coefficient partial sum (LDS of the exchange)
+    // deterministic workgroup reduction of the sponge-coefficient partial sum: a fixed xor tree per
+    // wave, then the NW wave sums in wave order (LDS of the exchange)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ksum += __shfl_xor(ksum, o, 64);
     double *red = reinterpret_cast<double *>(&xq[0][0][0][0]);
     __syncthreads();
-    const int tid = threadIdx.x;
-    red[tid] = ksum;
+    if (lane == 0) red[w] = ksum;
     __syncthreads();
-    for (int w2 = 32 * NW; w2 > 0; w2 >>= 1) {
-        if (tid < w2) red[tid] += red[tid + w2];
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = red[0];
+        for (int i = 1; i < NW; ++i) tot += red[i];
+        a.gk_part[(size_t)bs * a.nblk + ti.tile] += tot;
     }
-    if (tid == 0) a.gk_part[(size_t)bs * a.nblk + ti.tile] += red[0];
 }
 #undef TW_VERT
 #undef TW_REGION_INIT
@@ -1579,7 +1606,6 @@ __device__ __forceinline__ float bload_nt(__amdgpu_buffer_rsrc_t r, int voff, in
 {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, CP_NT));
 }
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // P_{k-1}, rows uz0-2 .. uz0+9 of one step: slab rows 0..7 as row pairs PC[i] = {i, i+4}, the
 // stencil's halo rows as PH = {-2, -1, 8, 9}.  HR = the epoch's history descriptor, SOFF = the
@@ -2569,20 +2595,24 @@ void launch_fwd_w(int T, bool gen, bool pair, dim3 grid, hipStream_t st, const F
     default: launch_fwd_w_T<4>(gen, pair, grid, st, a); break;
     }
 }
-template <int TT>
+template <int TT, bool EX>
 void launch_adj_w_T(bool pair, dim3 grid, hipStream_t st, const AdjTBArgs &a)
 {
     const dim3 blk(64 * TW_ADJ_NW);
-    if (pair) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, true>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, false>), grid, blk, 0, st, a);
+    if (pair) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, true, EX>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_adj_tw<TT, TW_ADJ_NW, TW_ADJ_R, false, EX>), grid, blk, 0, st, a);
 }
-void launch_adj_w(int T, bool pair, dim3 grid, hipStream_t st, const AdjTBArgs &a)
+void launch_adj_w(int T, bool pair, bool exact, dim3 grid, hipStream_t st, const AdjTBArgs &a)
 {
-    switch (T) {
-    case 1: launch_adj_w_T<1>(pair, grid, st, a); break;
-    case 2: launch_adj_w_T<2>(pair, grid, st, a); break;
-    case 3: launch_adj_w_T<3>(pair, grid, st, a); break;
-    default: launch_adj_w_T<4>(pair, grid, st, a); break;
+    switch (T * 2 + (exact ? 1 : 0)) {
+    case 2: launch_adj_w_T<1, false>(pair, grid, st, a); break;
+    case 3: launch_adj_w_T<1, true>(pair, grid, st, a); break;
+    case 4: launch_adj_w_T<2, false>(pair, grid, st, a); break;
+    case 5: launch_adj_w_T<2, true>(pair, grid, st, a); break;
+    case 6: launch_adj_w_T<3, false>(pair, grid, st, a); break;
+    case 7: launch_adj_w_T<3, true>(pair, grid, st, a); break;
+    case 8: launch_adj_w_T<4, false>(pair, grid, st, a); break;
+    default: launch_adj_w_T<4, true>(pair, grid, st, a); break;
     }
 }
 
@@ -2936,6 +2966,7 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * ns * nblk_alloc * sizeof(double), st));
     RDQ_CHECK(hipMemsetAsync(gbeta, 0, (size_t)B * ns * sizeof(float), st));
     a.coeffs = coeffs; a.hist = hist; a.dseis = dseis; a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
+    a.cg = coef_gen(p, B, coeffs);
     a.nblk = nblk_alloc;
     RDQ_TRY(fork_chains(p, st, S));
     for (int c = 0; c < S; ++c) {
@@ -2955,7 +2986,9 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
             a.in_l2 = ring + (size_t)(2 * pin + 1) * L;
             a.out_l1 = ring + (size_t)(2 * pout) * L;
             a.out_l2 = ring + (size_t)(2 * pout + 1) * L;
-            if (p->wide) launch_adj_w(a.nsteps, (p->Wp & 1) == 0, grid, cs, a);   // (tail: T' < T)
+            // (tail: T' < T); FMA form only where the persistent adjoint uses it too (nbc >= 20: a thin
+            // sponge's standing modes amplify the contraction's rounding, 1.5e-5 at nbc = 4)
+            if (p->wide) launch_adj_w(a.nsteps, (p->Wp & 1) == 0, !p->adj_fma, grid, cs, a);
             else launch_adj(T, grid, cs, a);
         }
     }

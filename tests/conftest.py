@@ -18,6 +18,21 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP kernels)")
 
 
+def record_margin(test, case, measured, bar):
+    """One parity test's measured value against its bar, appended as a JSON line to
+    $RDQ_EVIDENCE_DIR/margins.jsonl (GPU evidence runs: profiles/r*/margins.jsonl), so every bar can
+    be read next to what the kernels actually achieve.  No-op without the variable."""
+    import json
+    d = os.environ.get("RDQ_EVIDENCE_DIR")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    rec = {"test": test, "case": str(case), "measured": float(measured), "bar": float(bar),
+           "ratio": float(measured) / float(bar) if bar else None}
+    with open(os.path.join(d, "margins.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
 def load_golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, ctx_of, load_golden, vnorm
+from conftest import GOLDEN, ctx_of, load_golden, record_margin, vnorm
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -522,3 +522,99 @@ def test_marmousi_scale_grid_vs_oracle(cuda):
         assert bits_equal(gA[:, 0] + gA[:, 1], oA), T
         assert bits_equal(gb.view(B, -1).cpu().numpy(), ob), T
         np.testing.assert_allclose(gk.view(B, -1).sum(1).cpu().numpy(), oK, rtol=1e-7)
+
+
+def _chunked_run(plan, v, B, dseis, wide, exact, T):
+    """Chunked forward + adjoint: (seis, per-shot gA [B, ns, Hp, Wp], gbeta [B, ns], gk sum [B])."""
+    plan.set_persistent(False)
+    plan.set_variant(adj_exact=exact, wide_chunked=wide)
+    plan.set_tuning(T, T, 1)
+    assert not plan.launch_info(B)["adj_persistent"]
+    coeffs, vstat = plan.coeffs(v, 0)
+    seis, hist = plan.forward(coeffs, B, keep_history=True)
+    gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+    g = plan.finalize(coeffs, vstat, gA, gk, gb, B, 0)
+    plan.status()
+    sz = plan.sizes(B)
+    return (seis.cpu().numpy(), gA.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy(),
+            gb.view(B, -1).cpu().numpy(), gk.view(B, -1).sum(1).cpu().numpy(), g.cpu().numpy())
+
+
+def _shot_sum(gA):
+    acc = gA[:, 0].copy()                      # shots in order, fp32 (the K4 / oracle order)
+    for s in range(1, gA.shape[1]):
+        acc = acc + gA[:, s]
+    return acc
+
+
+@pytest.mark.parametrize("nx,nbc,T", [(71, 10, 4), (71, 10, 3), (84, 10, 4), (40, 4, 2)])
+def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T):
+    """The chunked kernels on 128-column regions (two columns per lane; k_fwd_tw / k_adj_tw) on an odd
+    padded width (Wp = 91: a lane's column pair wraps across the domain edge, 4-byte accesses), an
+    even one (Wp = 104: 8-byte pairs) and a thin sponge (nbc = 4): forward bit-exact and exact-order
+    gA / gbeta bit-exact vs the oracle and equal, shot by shot, to the 64-column kernels; nt = 162 is
+    not a multiple of T, so the tail launch runs its own depth.  The FMA variant (the default) within
+    fp32 tolerance."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=nx, nt=162, dx=10.0, dt=0.001, nbc=nbc, f=15.0, sz=10, gz=10, ng=nx, ns=3)
+    vn = vnorm(make_model("curvefault", 40, nx, seed=31, batch=2))
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vn).to(cuda)
+    plan = fwi._plan(40, nx, v.device)
+    B = 2
+    sz = plan.sizes(B)
+    assert sz.Wp == nx + 2 * nbc
+    rng = np.random.default_rng(11)
+    dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
+    dseis = torch.from_numpy(dseis_np).to(cuda)
+    wide = _chunked_run(plan, v, B, dseis, True, True, T)
+    narrow = _chunked_run(plan, v, B, dseis, False, True, T)
+    f = O.OracleFWI(dict(ctx), B)
+    so, c = f.forward(vn, keep_history=True)
+    oA, oK, ob = f.adjoint(c, dseis_np)
+    assert bits_equal(wide[0], so) and bits_equal(narrow[0], so)
+    assert bits_equal(wide[1], narrow[1])
+    assert bits_equal(_shot_sum(wide[1]), oA)
+    assert bits_equal(wide[2], ob) and bits_equal(narrow[2], ob)
+    np.testing.assert_allclose(wide[3], oK, rtol=1e-7)
+    np.testing.assert_allclose(narrow[3], wide[3], rtol=1e-12)
+    fma = _chunked_run(plan, v, B, dseis, True, False, T)
+    assert bits_equal(fma[0], so)
+    gA, oA = fma[1].astype(np.float64).sum(1), oA.astype(np.float64)   # (nbc = 4 grows to 1e25: fp64 norms)
+    assert np.linalg.norm(gA - oA) / np.linalg.norm(oA) < 2e-6
+    np.testing.assert_allclose(fma[2], ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
+    np.testing.assert_allclose(fma[3], oK, rtol=2e-5)
+
+
+@pytest.mark.parametrize("name,kw", FWD)
+def test_wide_chunked_fma_adjoint_vs_oracle(cuda, name, kw):
+    """The default chunked adjoint (FMA contraction) on every forward fixture: gA within 2e-6 rel-L2 of
+    the oracle's, gbeta within 2e-5, and the velocity gradient (K4) within 5e-5 rel-L2 of the oracle's
+    (the bar the exact path meets against the reference's autograd; measured 1.6e-5 at OpenFWI, the
+    persistent default's recurrence form 1.0e-5).
+    The sponge sum gk = sum K P (L_{k+1} - L_k) is a difference of nearly equal adjoint levels, so
+    the contraction's rounding shows there most (1.3e-4 relative at OpenFWI, ns = 5, nt = 400); it
+    enters the gradient at one cell (the first argmin of the velocity).
+    Thin-sponge fixtures (nbc < 20) run the exact order."""
+    z = load_golden(name)
+    ctx = ctx_of(z)
+    fwi = make_fwi(ctx, **kw)
+    vn = vnorm(z["v"])
+    v = torch.from_numpy(vn).to(cuda)
+    B = v.shape[0]
+    plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(3)
+    dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
+    got = _chunked_run(plan, v, B, torch.from_numpy(dseis_np).to(cuda), True, False, 4)
+    f = O.OracleFWI(ctx, B, **kw)
+    _, c = f.forward(vn, keep_history=True)
+    oA, oK, ob = f.adjoint(c, dseis_np)
+    gA, oA = got[1].astype(np.float64).sum(1), oA.astype(np.float64)
+    assert np.linalg.norm(gA - oA) / np.linalg.norm(oA) < 2e-6
+    np.testing.assert_allclose(got[2], ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
+    np.testing.assert_allclose(got[3], oK, rtol=3e-4)
+    go = f.finalize(c, oA.astype(np.float32), oK, ob)
+    rel = np.linalg.norm(got[4] - go) / np.linalg.norm(go)
+    record_margin("wide_chunked_fma_dLdv_rel_l2", name, rel, 5e-5)
+    assert rel < 5e-5
