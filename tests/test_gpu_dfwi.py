@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ctx_of, load_golden
+from conftest import ctx_of, load_golden, record_margin
 
 pytestmark = pytest.mark.gpu
 
@@ -45,15 +45,21 @@ def test_diffusionfwi_vs_reference(cuda, tag, kw):
     mu, hist = bench.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
                               torch.from_numpy(z["y"]).to(cuda), fwi, ts=3, diffusion_ts=4, lr=0.03, **kw)
     h = hist[0]
+    # bars ~10x the measured deviation (profiles/r4/margins.jsonl), except the grad_smooth run's data
+    # misfit: its smoothed restart-Adam steps move near-zero-gradient cells by +-lr on fp32-level
+    # signs (tools/dfwi_sensitivity.py: 5.5e-3 from an eps-hat perturbation of 1e-7; measured 5.7e-3)
+    bars = {"base": dict(obs=3e-4, ssim=3e-4, mae=3e-4, rmse=3e-4, mean=1e-5),
+            "smooth": dict(obs=1e-2, ssim=4e-4, mae=4e-4, rmse=4e-4, mean=1e-3)}[tag]
     for k in ("obs", "ssim", "mae", "rmse"):
         key = "obs_losses" if k == "obs" else k
-        np.testing.assert_allclose(np.array(h[key]), z[tag + "_" + k], rtol=1e-2, err_msg=k)
+        got, ref = np.array(h[key], np.float64), z[tag + "_" + k].astype(np.float64)
+        record_margin("diffusionfwi_metric_rel", f"{tag}:{k}", float(np.max(np.abs(got - ref) / np.abs(ref))), bars[k])
+        np.testing.assert_allclose(got, ref, rtol=bars[k], err_msg=k)
     d = np.abs(mu.cpu().numpy() - z[tag + "_mu"])
+    record_margin("diffusionfwi_mean_abs_model_dev", tag, float(d.mean()), bars["mean"])
+    assert d.mean() < bars["mean"], (d.mean(), d.max())
     if tag == "base":
-        assert d.mean() < 2e-3 and (d > 1e-2).mean() <= 0.02 and d.max() <= 3 * 0.03, \
-            (d.mean(), (d > 1e-2).sum(), d.max())
-    else:
-        assert d.mean() < 2e-3, (d.mean(), d.max())
+        assert (d > 1e-2).mean() <= 0.02 and d.max() <= 3 * 0.03, ((d > 1e-2).sum(), d.max())
 
 
 def test_ilvr_fwi_vs_reference(cuda):
@@ -73,5 +79,8 @@ def test_ilvr_fwi_vs_reference(cuda):
     h = hist[0]
     for k in ("obs", "ssim", "mae", "rmse"):
         key = "obs_losses" if k == "obs" else k
-        np.testing.assert_allclose(np.array(h[key]), z[k], rtol=2e-3, err_msg=k)
-    assert np.abs(mu.cpu().numpy() - z["mu"]).max() < 2e-3
+        got, ref = np.array(h[key], np.float64), z[k].astype(np.float64)
+        record_margin("ilvr_metric_rel", k, float(np.max(np.abs(got - ref) / np.abs(ref))), 8e-4)
+        np.testing.assert_allclose(got, ref, rtol=8e-4, err_msg=k)        # measured <= 7.7e-5
+    record_margin("ilvr_max_abs_model_dev", "", float(np.abs(mu.cpu().numpy() - z["mu"]).max()), 4e-5)
+    assert np.abs(mu.cpu().numpy() - z["mu"]).max() < 4e-5                 # measured 4.1e-6

@@ -85,6 +85,7 @@ def test_gradient_vs_reference_autograd(cuda, name):
     np.testing.assert_allclose(loss.detach().cpu().numpy(), z["loss"], rtol=2e-6)
     g = vn.grad.cpu().numpy()
     ref = z["grad"]
+    record_margin("grad_vs_reference_autograd_rel_l2", name, np.linalg.norm(g - ref) / np.linalg.norm(ref), 5e-5)
     assert np.linalg.norm(g - ref) / np.linalg.norm(ref) < 5e-5
     # and against the oracle on identical inputs: tighter (only fp64 summation order differs)
     f = O.OracleFWI(ctx_of(z), vn.shape[0])
@@ -93,21 +94,25 @@ def test_gradient_vs_reference_autograd(cuda, name):
     go = f.finalize(c, *f.adjoint(c, ds))
     # default persistent adjoint contracts into FMAs (RDQ_VARIANT_ADJ_EXACT off): fp32-level only
     err = np.linalg.norm(g - go) / np.linalg.norm(go)
+    record_margin("grad_vs_oracle_rel_l2", name, err, 5e-6)
     assert err < 5e-6, err
 
 
-@pytest.mark.parametrize("dt,f", [(0.001, 15.0), (0.0005, 15.0), (0.00025, 15.0), (0.001, 7.5)])
-def test_recurrence_adjoint_at_small_dt(cuda, dt, f):
+@pytest.mark.parametrize("dt,f,nbc", [(0.001, 15.0, 120), (0.0005, 15.0, 120), (0.00025, 15.0, 120), (0.001, 7.5, 120),
+                                      (0.001, 15.0, 20), (0.001, 15.0, 40)])
+def test_recurrence_adjoint_at_small_dt(cuda, dt, f, nbc):
     """The default persistent adjoint rebuilds lap'(P_{k-1}) from three history levels and divides by
     A = (v dt / dx)^2, so rounding in P grows like eps / (omega dt)^2 as dt or f shrinks.  Every
     reference config runs dt = 0.001, f = 15 Hz; this pins the error at 2x and 4x smaller dt and at
     half the frequency against the oracle, next to the exact-order adjoint (rdq_fwi_set_variant
     flag 2) on the same inputs.  Bars (rel-L2 of dL/dv vs the oracle, sign residuals): exact order
     1e-6 (measured 0), recurrence 2e-5 at the reference's dt and f (measured 1.0e-5), 1e-4 below them
-    (measured 2.3e-5 at dt / 2, 3.9e-5 at dt / 4, 4.6e-6 at f / 2; profiles/r3/small_dt_adjoint.jsonl)."""
+    (measured 2.3e-5 at dt / 2, 3.9e-5 at dt / 4, 4.6e-6 at f / 2; profiles/r3/small_dt_adjoint.jsonl).
+    Sponge widths at and above the recurrence cut-off (RDQ_RECURRENCE_MIN_NBC = 20): nbc = 20
+    and 40 at the reference's dt / f, same 2e-5 bar."""
     z = load_golden("grad_openfwi_ns1")
     ctx = ctx_of(z)
-    ctx["dt"], ctx["f"] = dt, f
+    ctx["dt"], ctx["f"], ctx["nbc"] = dt, f, nbc
     nt = int(ctx["nt"])
     vn0 = vnorm(z["v_init"])
     fo = O.OracleFWI(ctx, vn0.shape[0])
@@ -125,14 +130,16 @@ def test_recurrence_adjoint_at_small_dt(cuda, dt, f):
         plan.status()
         assert plan.launch_info(1)["adj_persistent"]
         errs[exact] = float(np.linalg.norm(vn.grad.cpu().numpy() - go) / np.linalg.norm(go))
-    rec = {"dt": dt, "f": f, "nt": nt, "grad_rel_l2_recurrence": errs[False], "grad_rel_l2_exact": errs[True]}
+    rec = {"dt": dt, "f": f, "nbc": nbc, "nt": nt, "grad_rel_l2_recurrence": errs[False], "grad_rel_l2_exact": errs[True]}
+    bar = 2e-5 if (dt, f) == (0.001, 15.0) else 1e-4
+    record_margin("recurrence_adjoint_dLdv_rel_l2", f"dt={dt},f={f},nbc={nbc}", errs[False], bar)
     d = os.environ.get("RDQ_EVIDENCE_DIR")
     if d:
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "small_dt_adjoint.jsonl"), "a") as fh:
             fh.write(json.dumps(rec) + "\n")
     assert errs[True] < 1e-6, rec
-    assert errs[False] < (2e-5 if (dt, f) == (0.001, 15.0) else 1e-4), rec
+    assert errs[False] < bar, rec
 
 
 @pytest.mark.parametrize("fwd_rows,adj_rows", [(6, 6), (8, 8), (12, 12), (24, 8)])
@@ -478,6 +485,8 @@ def test_inversion_loop_vs_reference(cuda, name):
     d = np.abs(mu - z["mu"])
     rm = float(np.sqrt(np.mean(d ** 2)))
     print(f"{name}: velocity-model RMSE vs the reference {rm:.3e} (floor {floor:.3e})")
+    record_margin("loop_model_rmse_vs_ref", name, rm, max(1e-4, 2.0 * floor))
+    record_margin("loop_rmse_history_max_dev", name, float(np.abs(np.array(h["rmse"]) - z["rmse"]).max()), 1e-4)
     assert rm <= max(1e-4, 2.0 * floor), (rm, floor)
     assert float(np.median(d)) < 1e-5, float(np.median(d))
     for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):

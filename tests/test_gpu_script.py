@@ -152,3 +152,53 @@ def test_checkpoint_round_trip_dim64(cuda, tmp_path):
         ref = torch.from_numpy(z[key]).to(cuda)
         err = (got - ref).abs().max().item()
         assert err <= 2e-4 * ref.abs().max().item(), (key, err)
+
+
+@pytest.mark.parametrize("name,n_models,nz,nx,family", [
+    ("default", 2, 70, 70, "FV"),                # regularization none, batch_size 1 -> two batches
+    ("openfwi_red-diffeq", 25, 70, 70, "CF"),    # RED-DiffEq, batch_size 25: 25 models x 5 shots, B = 25 U-Net
+    ("marmousi_red-diffeq", 1, 70, 190, "Marmousi"),   # RED-DiffEq on 70 x 190: patched regulariser
+])
+def test_reference_configs_run_unchanged_through_cli(cuda, tmp_path, monkeypatch, name, n_models, nz, nx, family):
+    """The reference's own configs (configs/default.yaml, configs/openfwi/red-diffeq.yaml,
+    configs/marmousi/red-diffeq.yaml; parsed values in tests/golden/configs/*.json, written back out
+    as YAML) through scripts/run_inversion.py's command line, main(["--config", ..., "--ts", "2"]),
+    unchanged: their relative data / checkpoint / results paths resolve under a scratch directory
+    holding a tiny synthetic dataset in the OpenFWI layout (the checkpoint is absent: random U-Net).
+    Every model of every batch writes <idx>_results.npz with the reference's keys
+    (reference run_inversion.py:180-216, 332-415)."""
+    import json
+    import yaml
+    from red_diffeq.solvers.pde import FWIForward
+    from red_diffeq.utils.data_trans import s_normalize_none, v_denormalize, v_normalize
+    from red_diffeq.utils.synthetic import make_model
+    cfg = json.load(open(os.path.join(ROOT, "tests", "golden", "configs", name + ".json")))["config"]
+    monkeypatch.chdir(tmp_path)
+    with open("config.yaml", "w") as f:
+        yaml.safe_dump(cfg, f)
+    seis_dir, vel_dir = cfg["data"]["seismic_data_dir"], cfg["data"]["velocity_data_dir"]
+    os.makedirs(seis_dir)
+    os.makedirs(vel_dir)
+    vel = make_model({"FV": "flatvel", "CF": "curvefault"}.get(family, "curvefault"), nz, nx, seed=5, batch=n_models)
+    fwi = FWIForward(dict(cfg["pde"]), cuda, normalize=True, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
+    with torch.no_grad():
+        seis = fwi(v_normalize(torch.from_numpy(vel)).to(cuda)).cpu().numpy()
+    assert seis.shape == (n_models, cfg["pde"]["ns"], cfg["pde"]["nt"], cfg["pde"]["ng"])
+    np.save(os.path.join(seis_dir, family + ".npy"), seis)
+    np.save(os.path.join(vel_dir, family + ".npy"), vel)
+    del fwi
+    _script().main(["--config", "config.yaml", "--ts", "2"])
+    runs = sorted((tmp_path / cfg["experiment"]["results_dir"]).glob(f"*/{cfg['experiment']['name']}/*"))
+    assert len(runs) == 1, runs
+    assert (runs[0] / "config.yaml").exists()
+    files = sorted((runs[0] / family).glob("*_results.npz"), key=lambda p: int(p.name.split("_")[0]))
+    assert [f.name for f in files] == [f"{i}_results.npz" for i in range(n_models)]
+    for f in (files[0], files[-1]):
+        z = np.load(f)
+        assert set(z.files) == {"result", "initial_velocity", "ground_truth", "total_losses", "obs_losses",
+                                "reg_losses", "ssim", "mae", "rmse"}
+        assert z["result"].shape == (nz, nx) and z["obs_losses"].shape == (2,)
+        assert np.isfinite(z["result"]).all() and np.abs(z["result"]).max() <= 1.0
+        assert np.isfinite(z["total_losses"]).all() and z["obs_losses"][1] < z["obs_losses"][0]
+        idx = int(f.name.split("_")[0])
+        np.testing.assert_array_equal(z["ground_truth"], vel[idx, 0])

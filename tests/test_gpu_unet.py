@@ -7,6 +7,7 @@ per-op max-abs <= 2e-5 x scale; whole U-Net <= 2e-4 relative to the output range
 The reference fixtures are "parity unpinned" at Attend (denoising-diffusion-pytorch 2.1.1 is not
 installed; its flash=False math is restated)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -14,14 +15,17 @@ import torch
 import torch.nn as nn
 
 import unet_torch_ref as R
-from conftest import load_golden
+from conftest import load_golden, record_margin
 
 pytestmark = pytest.mark.gpu
 
 
-def close(a, b, rel=2e-5):
+def close(a, b, rel=1e-5, what=""):
+    """max |a - b| <= rel x max |b|; the measured ratio is recorded next to the bar (record_margin)."""
     scale = max(b.abs().max().item(), 1e-6)
     err = (a - b).abs().max().item()
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    record_margin(test, what, err / scale, rel)
     assert err <= rel * scale, (err, scale)
 
 
@@ -117,7 +121,7 @@ def test_conv_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post):
         ref = R.group_norm_affine_silu(R.conv2d(xin, conv), norm, sc[:, :, None, None].chunk(2, dim=1) if ss else None)
         if post:
             ref = ref + pr
-    close(got, ref, rel=5e-5)
+    close(got, ref, rel=1e-5)
     assert int(O._TICKET_POOL[x.device]["pool"].abs().sum()) == 0
 
 
@@ -163,7 +167,7 @@ def test_conv_rms_fused(cuda, C, cout, H, B):
     with torch.no_grad():
         got = ops.rms_conv(x, nm, conv)
         ref = R.conv2d(R.rmsnorm(x, g), conv)
-    close(got, ref, rel=5e-5)
+    close(got, ref, rel=1e-5)
 
 
 @pytest.mark.parametrize("C,H,ss", [(64, 72, True), (16, 9, False), (128, 18, True)])
@@ -199,7 +203,7 @@ def test_rmsnorm_linear_sinusoidal(cuda):
     emb = math.log(10000) / (half - 1)
     f = torch.exp(torch.arange(half, device=cuda) * -emb)
     ref = torch.cat(((t[:, None] * f).sin(), (t[:, None] * f).cos()), -1)
-    close(ops.sinusoidal(t, 64), ref, rel=1e-4)
+    close(ops.sinusoidal(t, 64), ref, rel=2e-5)
 
 
 def test_time_mlp_and_scale_shifts(cuda):
@@ -216,7 +220,7 @@ def test_time_mlp_and_scale_shifts(cuda):
         f = torch.exp(torch.arange(half, device=cuda) * -(math.log(10000) / (half - 1)))
         emb = torch.cat(((t[:, None] * f).sin(), (t[:, None] * f).cos()), -1)
         ref = net.time_mlp[3](F.gelu(net.time_mlp[1](emb)))
-        close(te, ref, rel=1e-4)
+        close(te, ref, rel=2e-5)
         blocks = net._resnet_blocks()
         ss = ops.resnet_scale_shifts(te, blocks)
         assert len(ss) == len(blocks) == 19
@@ -256,7 +260,7 @@ def test_linear_attention(cuda, C, H, B):
         m.norm.g.mul_(1 + 0.2 * torch.randn_like(m.norm.g))
         m.to_out[1].g.mul_(1 + 0.2 * torch.randn_like(m.to_out[1].g))
     x = torch.randn(B, C, H, H, device=cuda)
-    close(ops.linear_attention(x, m), R.linear_attention(x, m) + x, rel=5e-5)
+    close(ops.linear_attention(x, m), R.linear_attention(x, m) + x, rel=1e-5)
 
 
 # 9 x 9 (the U-Net's level), 8 x 8 and 16 x 16, B = 1 and 2
@@ -267,7 +271,7 @@ def test_full_attention(cuda, C, H, B):
     torch.manual_seed(5)
     m = Attention(C).to(cuda)
     x = torch.randn(B, C, H, H, device=cuda)
-    close(ops.full_attention(x, m), R.full_attention(x, m) + x, rel=5e-5)
+    close(ops.full_attention(x, m), R.full_attention(x, m) + x, rel=1e-5)
 
 
 def _load_unet(cuda):
@@ -286,8 +290,9 @@ def test_unet_dim8_vs_reference_fixture(cuda):
         out = net(x, t)
         ref_torch = R.unet_forward(net, x, t)
     ref = torch.from_numpy(z["out"]).to(cuda)
-    close(out, ref, rel=2e-4)                  # vs the reference implementation (CPU)
-    close(out, ref_torch, rel=1e-4)            # vs plain PyTorch fp32 on the same GPU
+    # bars <= 20x what the kernels measure (9.6e-7 / 1.05e-6 of the output range, profiles/r4/margins.jsonl)
+    close(out, ref, rel=2e-5, what="vs reference fixture")      # vs the reference implementation (CPU)
+    close(out, ref_torch, rel=2e-5, what="vs torch fp32")       # vs plain PyTorch fp32 on the same GPU
 
 
 @pytest.mark.parametrize("tag", ["sq", "sqw", "patch"])
@@ -305,9 +310,10 @@ def test_red_regulariser_vs_reference(cuda, tag):
     fn = red.get_reg_loss_patched if tag == "patch" else red.get_reg_loss
     reg, gpm, tt = fn(mu, t=t, noise=noise)
     reg.sum().backward()
-    close(reg.detach(), torch.from_numpy(zr[tag + "_reg"]).to(cuda), rel=1e-3)
-    close(gpm.detach(), torch.from_numpy(zr[tag + "_gpm"]).to(cuda), rel=1e-3)
-    close(mu.grad, torch.from_numpy(zr[tag + "_grad"]).to(cuda), rel=2e-4)
+    # measured <= 1.3e-6 of each output's range (profiles/r4/margins.jsonl)
+    close(reg.detach(), torch.from_numpy(zr[tag + "_reg"]).to(cuda), rel=2e-5, what="reg")
+    close(gpm.detach(), torch.from_numpy(zr[tag + "_gpm"]).to(cuda), rel=2e-5, what="gpm")
+    close(mu.grad, torch.from_numpy(zr[tag + "_grad"]).to(cuda), rel=2e-5, what="grad")
 
 
 def _bf(t):
@@ -512,8 +518,8 @@ def test_post_process_and_p_sample_deterministic_vs_reference(cuda):
     with torch.no_grad():
         for t in (0, 37, 640):
             mean, var, logvar, xs = diff.p_mean_variance(x, torch.full((2,), t, dtype=torch.long, device=cuda))
-            close(mean, torch.from_numpy(z[f"pmv{t}_mean"]).to(cuda), rel=1e-4)
-            close(xs, torch.from_numpy(z[f"pmv{t}_xs"]).to(cuda), rel=1e-4)
+            close(mean, torch.from_numpy(z[f"pmv{t}_mean"]).to(cuda), rel=2e-5)
+            close(xs, torch.from_numpy(z[f"pmv{t}_xs"]).to(cuda), rel=2e-5)
             assert np.allclose(var.reshape(-1).cpu().numpy(), z[f"pmv{t}_var"], rtol=1e-6)
             assert np.allclose(logvar.reshape(-1).cpu().numpy(), z[f"pmv{t}_logvar"], rtol=1e-6)
             m2, xs2 = diff.p_sample_deterministic(x, t)
@@ -531,4 +537,4 @@ def test_post_process_and_p_sample_deterministic_vs_reference(cuda):
     finally:
         torch.randn_like = orig
     assert calls == [(2, 1, 72, 72)]
-    close(den, torch.from_numpy(z["denoised"]).to(cuda), rel=1e-4)
+    close(den, torch.from_numpy(z["denoised"]).to(cuda), rel=2e-5)
