@@ -81,12 +81,14 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
  *   RDQ_VARIANT_FWD_GEN    the chunked forward regenerates alpha/temp1/temp2 from the model in
  *                          registers instead of loading the three K3 fields (identical results;
  *                          14% faster on the configs[4] grid);
- *   RDQ_VARIANT_ADJ_EXACT  the persistent adjoint keeps the oracle's exact fp32 operation order (gA
- *                          bit-identical to oracle/fwi_oracle.c) instead of rebuilding the gradient's
- *                          stencil term from the forward's time recurrence with FMA contraction
- *                          (faster; dL/dv within ~1e-5 rel-L2).  Plans whose sponge is thinner than 20
- *                          cells (nbc < 20) always run the exact order: there the recurrence's
- *                          cancellation is not fp32-accurate (5e-3 at nbc = 4);
+ *   RDQ_VARIANT_ADJ_EXACT  the adjoint keeps the oracle's exact fp32 operation order (gA
+ *                          bit-identical to oracle/fwi_oracle.c) instead of, in the persistent
+ *                          kernels, rebuilding the gradient's stencil term from the forward's time
+ *                          recurrence with FMA contraction (dL/dv within ~1e-5 rel-L2) and, in the
+ *                          wide chunked kernels, contracting the stencils into FMAs (dL/dv within
+ *                          ~2e-5).  Plans whose sponge is thinner than 20 cells (nbc < 20) always run
+ *                          the exact order: there the recurrence's cancellation is not fp32-accurate
+ *                          (5e-3 at nbc = 4) and standing modes amplify any contraction;
  *   RDQ_VARIANT_NO_XCD_LOCAL the persistent kernels publish every neighbour hand-off write-through
  *                          (sc1) instead of keeping whole slices on one XCD (read from HW_REG_XCC_ID)
  *                          with L2-resident hand-offs (identical results; slower);
