@@ -1,6 +1,7 @@
-"""Per-shape timing of the U-Net's fp32 convolutions at B = 1 (dim 64, 72x72): each shape's op
-captured 20x back to back in a hipGraph, replayed, device time per call and TFLOP/s.
-python tools/conv_micro.py [--only NAME] [--reps R] [--B B]"""
+"""Per-shape timing of the U-Net's convolutions (dim 64, 72x72): each shape's op captured back to
+back in a hipGraph, replayed, device time per call and TFLOP/s against the fp32 matrix peak, or with
+--bf16 (the configs[4] batch: --B 344) against the bf16 dense peak.
+python tools/conv_micro.py [--only NAME] [--reps R] [--B B ...] [--bf16] [--inner N]"""
 import argparse
 import json
 import os
@@ -26,7 +27,7 @@ SHAPES = {
 }
 
 
-def run(name, B, reps, inner=20):
+def run(name, B, reps, inner=20, bf16=False):
     cin1, cin2, cout, k, H, mode = SHAPES[name]
     g = torch.Generator(device="cuda").manual_seed(0)
     hs = H // 2 if mode == 1 else H
@@ -34,7 +35,7 @@ def run(name, B, reps, inner=20):
     x2 = torch.randn(B, cin2, H, H, device="cuda", generator=g) if cin2 else None
     w = torch.randn(cout, cin1 + cin2, k, k, device="cuda", generator=g) * 0.05
     b = torch.randn(cout, device="cuda", generator=g)
-    f = lambda: torch.ops.red_diffeq.conv2d_mfma(x, x2, w, b, None, k // 2, mode, False)  # noqa: E731
+    f = lambda: torch.ops.red_diffeq.conv2d_mfma(x, x2, w, b, None, k // 2, mode, bf16)  # noqa: E731
     for _ in range(3):
         f()
     torch.cuda.synchronize()
@@ -52,8 +53,9 @@ def run(name, B, reps, inner=20):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (reps * inner)
     flop = 2.0 * B * H * H * cout * (cin1 + cin2) * k * k
-    return {"shape": name, "B": B, "us": round(us, 2), "tflops": round(flop / us / 1e6, 1),
-            "mfma_frac": round(flop / us / 1e6 / 157.3, 3)}
+    peak = 2500.0 if bf16 else 157.3
+    return {"shape": name, "B": B, "bf16": bf16, "us": round(us, 2), "tflops": round(flop / us / 1e6, 1),
+            "mfma_frac": round(flop / us / 1e6 / peak, 3)}
 
 
 if __name__ == "__main__":
@@ -61,8 +63,10 @@ if __name__ == "__main__":
     ap.add_argument("--only", default=None)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--B", type=int, nargs="+", default=[1])
+    ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--inner", type=int, default=20)
     a = ap.parse_args()
     names = [a.only] if a.only else list(SHAPES)
     for B in a.B:
         for n in names:
-            print(json.dumps(run(n, B, a.reps)), flush=True)
+            print(json.dumps(run(n, B, a.reps, a.inner, a.bf16)), flush=True)
