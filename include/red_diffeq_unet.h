@@ -195,6 +195,19 @@ int rdq_linear_attention_block(int32_t B, int32_t heads, int32_t dh, int32_t n, 
                                const float *b_out, const float *g_out, const float *res, float *y, void *ws,
                                hipStream_t stream);
 
+/* LinearAttention.forward(x) + x with bf16 operands and fp32 accumulation (the configs[4] batched U-Net;
+ * reference diffusion.py:182-195 and the residual at 286 / 297): RMSNorm(x) (g_in), qkv = to_qkv,
+ * softmax(q) over d, softmax(k) over the memory + pixel tokens, context, to_out conv (+ b_out) and
+ * RMSNorm (g_out), + x, in two launches that never materialise qkv or the hidden tensor.
+ * heads = 4, dim_head = 32; dim 64 / 128; x, y (B, dim, n) fp32, y != x; mem_kv (2, 4, 32, nmem);
+ * wqkv / wout: rdq_conv2d_bf16_pack's packs of the (384, dim, 1, 1) / (dim, 128, 1, 1) weights;
+ * ws: rdq_linear_attention_bf16_ws_bytes (per chunk partial contexts). */
+size_t rdq_linear_attention_bf16_ws_bytes(int32_t B, int32_t dim, int32_t n);
+int rdq_linear_attention_bf16(int32_t B, int32_t dim, int32_t n, int32_t nmem, float scale, const float *x,
+                              const float *g_in, const void *wqkv, const float *mem_kv, const void *wout,
+                              const float *b_out, const float *g_out, float *y, void *ws, size_t ws_bytes,
+                              hipStream_t stream);
+
 /* Attention core with Attend(flash=False) (diffusion.py:209-217): softmax(q k^T dh^-1/2) v over
  * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32; K/V of one
  * head staged in LDS (n + nmem <= ~1500). */

@@ -236,7 +236,8 @@ __device__ __forceinline__ float dpp_shl1(float v)   // lane i <- lane i+1 (x+1)
 
 struct TBGeo {
     int B, ns, Hp, Wp, ld, isz, igz, ng, nrec, st;
-    int s_off, ns_grp;                   // this launch covers shots [s_off, s_off + ns_grp)
+    int s_off, ns_grp;                   // chunked launch: shots [s_off, s_off + ns_grp) of all B models
+    int sl_off, nsl;                     // persistent launch: flat slices [sl_off, sl_off + nsl), slice = b * ns + s
     int tiles_x, ntiles;                 // tile grid of this launch's blocking depth
     size_t cstride, slice, level;        // level = B*ns*slice (one time level of all slices)
     const int *isx, *rcv_start, *rcv_list;
@@ -1185,7 +1186,7 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
         }
         int sl = -1, tile = 0, local = 0;
         if (ok) {
-            const int Tt = g.ntiles, S = g.B * g.ns_grp;
+            const int Tt = g.ntiles, S = g.nsl;
             int placed = 0, take[8];
             for (int i = 0; i < 8; ++i) {
                 take[i] = xcd_mode ? min((int)n[i] / Tt, S - placed) : 0;
@@ -1227,9 +1228,9 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
     const PtTile ti = pt_assign(g, a.status, a.xcd_mode);                                           \
     if (!ti.valid) return;                                                                          \
     const bool gl2 = ti.local;                     /* uniform: XCD-local slice, L2 hand-offs */      \
-    const int b = __builtin_amdgcn_readfirstlane(ti.sl / g.ns_grp);                                 \
-    const int s = __builtin_amdgcn_readfirstlane(g.s_off + (ti.sl - b * g.ns_grp));                 \
-    const int bs = b * g.ns + s;                                                                    \
+    const int bs = __builtin_amdgcn_readfirstlane(g.sl_off + ti.sl);                                \
+    const int b = __builtin_amdgcn_readfirstlane(bs / g.ns);                                        \
+    const int s = __builtin_amdgcn_readfirstlane(bs - b * g.ns);                                    \
     const int tx = __builtin_amdgcn_readfirstlane(ti.tx), ty = __builtin_amdgcn_readfirstlane(ti.ty); \
     const int tile = __builtin_amdgcn_readfirstlane(ti.tile);                                       \
     const int ux = tx * IW - H + lane;                                                              \
@@ -2477,6 +2478,7 @@ TBGeo tb_geo(const rdq_fwi_plan *p, int B)
     g.isx = p->d_isx; g.rcv_start = p->d_rcv_start; g.rcv_list = p->d_rcv_list;
     g.rlane = p->d_rlane; g.dstride = p->rmulti ? p->ncolr : p->g.ng;
     g.s_off = 0; g.ns_grp = p->g.ns;
+    g.sl_off = 0; g.nsl = B * p->g.ns;
     return g;
 }
 
@@ -2693,26 +2695,27 @@ int gk_blocks(const rdq_fwi_plan *p)
     return n;
 }
 
-// Shots per persistent launch: every slice of one launch must be resident at once, so a survey
-// larger than the chip (e.g. 32 OpenFWI shots = 4 x 224 workgroups) runs as ceil(ns / per) launches
-// over consecutive shot groups of near-equal size; 0 = not even one shot of all B models fits.
-int pt_shots_per_launch(const rdq_fwi_plan *p, int B, int T, int NW, int cap)
+// Slices (model x shot) per persistent launch: every slice of one launch must be resident at once,
+// so a batch larger than the chip (e.g. 32 OpenFWI shots = 4 x 224 workgroups, or the reference's
+// OpenFWI config of 25 models x 5 shots = 125 slices) runs as ceil(B ns / per) launches over
+// consecutive runs of the flat slice index b * ns + s, of near-equal size; 0 = not even one slice fits.
+int pt_slices_per_launch(const rdq_fwi_plan *p, int B, int T, int NW, int cap)
 {
     if (cap <= 0) return 0;
-    const unsigned per = (unsigned)cap / (pt_tiles_padded(p, T, NW) * (unsigned)B);
+    const unsigned per = (unsigned)cap / pt_tiles_padded(p, T, NW);
     if (per < 1) return 0;
-    const int groups = (p->g.ns + (int)per - 1) / (int)per;
-    return (p->g.ns + groups - 1) / groups;
+    const int total = B * p->g.ns, groups = (total + (int)per - 1) / (int)per;
+    return (total + groups - 1) / groups;
 }
 
-// grid of a persistent launch covering `nsg` shots of B models.  A slice is XCD-local (L2 hand-offs,
+// grid of a persistent launch covering S slices.  A slice is XCD-local (L2 hand-offs,
 // pt_assign) only if one XCD received all its Tt workgroups; blocks are dealt round-robin over the
 // 8 XCDs, so a launch of S slices gets that for every slice only with >= 8 Tt ceil(S / 8) blocks.
 // Launches of fewer than 8 slices (e.g. the reference's 5-shot survey: 5 x 32 = 160 blocks, 20 per
 // XCD) are padded up to it when the chip holds that many; the surplus blocks find no slice and exit.
-unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
+unsigned pt_grid(const rdq_fwi_plan *p, int T, int NW, int nsl, bool adj)
 {
-    const unsigned S = (unsigned)B * (unsigned)nsg;
+    const unsigned S = (unsigned)nsl;
     unsigned grid = pt_tiles_padded(p, T, NW) * S;
     if (p->xcd_mode) {
         const int ih = region_rows(NW) - 4 * T;
@@ -2729,8 +2732,8 @@ unsigned pt_grid(const rdq_fwi_plan *p, int B, int T, int NW, int nsg, bool adj)
 }
 
 // region height (waves) of the persistent kernel for this call, 0 = not resident -> chunked.
-// Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).  `per` = shots
-// per launch (the survey runs as ceil(ns / per) launches).
+// Taller regions first: one workgroup per CU and less halo (64 x 96 vs 64 x 64).  `per` = slices
+// per launch (the batch runs as ceil(B ns / per) launches).
 // Small surveys first: a launch of at most PT_SMALL_WG workgroups in 64 x 64 regions of 16 waves x
 // 4 rows runs each step with 2/3 of the 96-row kernels' per-wave work on CUs the 96-row launch leaves
 // idle (profiles/r3/pt64_ab.txt, configs[1] geometry: 3 shots = 168 workgroups, forward 1.30 -> 1.14
@@ -2742,16 +2745,16 @@ int persistent_nw(rdq_fwi_plan *p, int B, bool adj, int *per = nullptr)
     const int T = adj ? p->adj_T : p->fwd_T;
     const int want = p->persist == -1 ? 1 : p->persist;   // 1 = auto, 8 / 12 / 16 = forced
     if (want == 1 || want == 16) {
-        const int k = pt_shots_per_launch(p, B, T, 16, capacity_nw(p, 16, adj, T));
-        const bool small = k >= p->g.ns && pt_tiles_padded(p, T, 16) * (unsigned)(B * p->g.ns) <= PT_SMALL_WG;
+        const int k = pt_slices_per_launch(p, B, T, 16, capacity_nw(p, 16, adj, T));
+        const bool small = k >= B * p->g.ns && pt_tiles_padded(p, T, 16) * (unsigned)(B * p->g.ns) <= PT_SMALL_WG;
         if (k > 0 && (want == 16 || small)) { if (per) *per = k; return 16; }
     }
     if (want == 1 || want == 12) {
-        const int k = pt_shots_per_launch(p, B, T, 12, capacity_nw(p, 12, adj, T));
+        const int k = pt_slices_per_launch(p, B, T, 12, capacity_nw(p, 12, adj, T));
         if (k > 0) { if (per) *per = k; return 12; }
     }
     if (want == 1 || want == 8) {
-        const int k = pt_shots_per_launch(p, B, T, 8, capacity_nw(p, 8, adj, T));
+        const int k = pt_slices_per_launch(p, B, T, 8, capacity_nw(p, 8, adj, T));
         if (k > 0) { if (per) *per = k; return 8; }
     }
     return 0;
@@ -2861,12 +2864,12 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof; a.xcd_mode = p->xcd_mode;
-    // consecutive shot groups, one resident launch each (granules live at per-slice offsets, so
+    // consecutive slice groups, one resident launch each (granules live at per-slice offsets, so
     // one zeroing serves every group)
-    for (int s0 = 0; s0 < p->g.ns; s0 += per) {
-        a.g.s_off = s0;
-        a.g.ns_grp = std::min(per, p->g.ns - s0);
-        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, false));
+    for (int s0 = 0; s0 < B * p->g.ns; s0 += per) {
+        a.g.sl_off = s0;
+        a.g.nsl = std::min(per, B * p->g.ns - s0);
+        const dim3 grid(pt_grid(p, T, NW, a.g.nsl, false));
         if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         launch_fwd_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
@@ -2895,10 +2898,10 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + PROF_WORDS : nullptr;
     a.xcd_mode = p->xcd_mode;
-    for (int s0 = 0; s0 < p->g.ns; s0 += per) {
-        a.g.s_off = s0;
-        a.g.ns_grp = std::min(per, p->g.ns - s0);
-        const dim3 grid(pt_grid(p, B, T, NW, a.g.ns_grp, true));
+    for (int s0 = 0; s0 < B * p->g.ns; s0 += per) {
+        a.g.sl_off = s0;
+        a.g.nsl = std::min(per, B * p->g.ns - s0);
+        const dim3 grid(pt_grid(p, T, NW, a.g.nsl, true));
         if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
         launch_adj_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
@@ -3216,7 +3219,7 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     out[1] = persistent_nw(p, B, true, &pera);
     out[2] = p->fwd_T;
     out[3] = p->adj_T;
-    const int ns = p->g.ns, nt = p->g.nt;
+    const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
     out[4] = out[0] ? (ns + perf - 1) / perf : (nt + p->fwd_T - 1) / p->fwd_T;
     out[5] = out[1] ? (ns + pera - 1) / pera : (nt + p->adj_T - 1) / p->adj_T;
     return 0;

@@ -2439,6 +2439,343 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
     }
 }
 
+// ------------------------------------------------- linear attention, bf16, whole block fused
+// LinearAttention.forward(x) + x (reference diffusion.py:182-195 and the residual at 286 / 297) for the
+// batched bf16 U-Net (configs[4]: hundreds of 72 x 72 tiles).  The unfused form writes and re-reads
+// qkv (384 channels, 6x the block's input) and the hidden tensor; here two launches read the input
+// twice and write the output once:
+//   k_lab_kv   per (sample, pixel chunk): RMSNorm(x) -> bf16 -> [k | v] = W_kv xn on
+//              v_mfma_f32_32x32x16_bf16, k softmax over pixels folded into a running context
+//              (flash style: per-channel running maximum, the context and the denominator rescaled
+//              when it rises) -> per chunk (m, den, ctx^T) of every head
+//   k_lab_out  per (sample, pixel chunk): the chunk partials and the memory tokens combined into the
+//              normalised context (x scale), RMSNorm(x) -> q = W_q xn, softmax over d, hidden = ctx^T q,
+//              y = W_out hidden + b, RMSNorm(y) * g * sqrt(dim) + x
+// Wave h owns head h in every head-local stage.  The MFMA layouts are chosen so that no per-pixel or
+// per-channel reduction crosses more than the lane pair (l, l ^ 32): k and v are formed TRANSPOSED
+// (rows = pixels, columns = channels: a lane holds one channel over 16 pixels), so the softmax
+// maximum over pixels is lane-local, and the context product ctx^T[e][d] = sum_n v[e][n] p[d][n]
+// takes both operands straight from those registers (the reduction index n enumerated in the same
+// register order for both); q is formed with pixels as columns (a lane holds 16 of one pixel's 32 d),
+// so the softmax over d is lane-local plus one swap, and hidden = ctx^T q takes q from registers.
+// Operands are bf16 (activations rounded as staged, as the bf16 convs do, and the softmax weights
+// and context), every accumulation fp32.
+constexpr int LB_PX = 64, LB_DH = 32, LB_HEADS = 4, LB_HID = LB_HEADS * LB_DH;
+constexpr int LB_PART = LB_HEADS * (2 * LB_DH + LB_DH * LB_DH);   // floats per (sample, chunk)
+
+struct LabArgs {
+    const float *x, *g_in, *mem, *b_out, *g_out;
+    const __bf16 *wqkv;              // [3 * 128][D]  (q, k, v rows)
+    const __bf16 *wout;              // [D][128]
+    float *part, *y;
+    int n, nch, nsub, nmem;
+    float scale;
+};
+
+// D layout of v_mfma_f32_32x32x16_bf16: register r of lane l holds row (r & 3) + 8 (r >> 2) + 4 (l >> 5)
+__device__ __forceinline__ int lb_row(int r, int g) { return (r & 3) + 8 * (r >> 2) + 4 * g; }
+
+// RMSNorm(x) of pixels [p0, p0 + 64) of sample b, rounded to bf16, into Xs[px][c], in two halves so
+// the next tile's loads are in flight during this tile's MFMAs: lb_load (thread: pixel lane, channel
+// octets wave + 4 j; pixels past n read pixel n - 1, their results are masked) and lb_store (the
+// norm over the four waves' partial sums, then the scaled bf16 octets).  lb_store's barrier also
+// orders its Xs writes after every wave's reads of the previous tile.
+template <int D>
+__device__ __forceinline__ void lb_load(const LabArgs &a, int b, int p0, float (&v)[D / 32][8])
+{
+    // buffer loads: one lane offset for every channel, the channel's plane offset in an SGPR
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int voff = min(p0 + lane, a.n - 1) * 4;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(a.x + (size_t)b * D * a.n), (short)0, D * a.n * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < D / 32; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[j][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    rx, voff, (8 * (w + 4 * j) + i) * a.n * 4, 0));
+}
+
+template <int D>
+__device__ __forceinline__ void lb_store(const LabArgs &a, const float (&v)[D / 32][8], __bf16 (*Xs)[D + 8],
+                                         float (*red)[LB_PX])
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float ss = 0.0f;
+#pragma unroll
+    for (int j = 0; j < D / 32; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss = fmaf(v[j][i], v[j][i], ss);
+    red[w][lane] = ss;
+    __syncthreads();
+    const float tot = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    const float k = sqrtf((float)D) / fmaxf(sqrtf(tot), 1e-12f);
+#pragma unroll
+    for (int j = 0; j < D / 32; ++j) {
+        const int c0 = 8 * (w + 4 * j);
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (__bf16)(v[j][i] * k * a.g_in[c0 + i]);
+        *reinterpret_cast<bf16x8 *>(&Xs[lane][c0]) = o;
+    }
+}
+
+// Occupancy sets the rate of these streaming kernels (each workgroup has one tile's loads in flight
+// during the previous tile's MFMAs): register budgets of 3 (dim 64) / 2 (dim 128) workgroups per CU.
+template <int D> struct LbOcc { static constexpr int N = D == 64 ? 3 : 2; };
+
+template <int D>
+__global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
+{
+    constexpr int KS = D / 16;                       // k-steps over the input channels
+    constexpr bool WREG = D <= 64;                   // W_kv fragments held in registers (else L1 / L2)
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[LB_PX][D + 8];
+    __shared__ float red[4][LB_PX];
+    const int ch = blockIdx.x, b = blockIdx.y;
+    const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, g = lane >> 5, cl = lane & 31;
+    // B fragments: column = channel cl of head h (k rows 128 + 32 h, v rows 256 + 32 h), k = c
+    const __bf16 *wk = a.wqkv + (size_t)(LB_HID + h * LB_DH + cl) * D + 8 * g;
+    const __bf16 *wv = a.wqkv + (size_t)(2 * LB_HID + h * LB_DH + cl) * D + 8 * g;
+    bf16x8 fk[WREG ? KS : 1], fv[WREG ? KS : 1];
+    if constexpr (WREG) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            fk[s] = *reinterpret_cast<const bf16x8 *>(wk + 16 * s);
+            fv[s] = *reinterpret_cast<const bf16x8 *>(wv + 16 * s);
+        }
+    }
+    f32x16 ctx = {};
+    float mrun = -INFINITY, den = 0.0f;
+    const int sub0 = ch * a.nsub, sub1 = min(sub0 + a.nsub, (a.n + LB_PX - 1) / LB_PX);
+    float xv[D / 32][8];
+    if (sub0 < sub1) lb_load<D>(a, b, sub0 * LB_PX, xv);
+    for (int sb = sub0; sb < sub1; ++sb) {
+        const int p0 = sb * LB_PX;
+        lb_store<D>(a, xv, Xs, red);
+        __syncthreads();
+        if (sb + 1 < sub1) lb_load<D>(a, b, p0 + LB_PX, xv);
+        // one 32-pixel block at a time: k^T and v^T (rows = pixels, column = channel cl), the online
+        // softmax over the pixels of channel d = cl (this lane and lane ^ 32), the context update
+#pragma unroll 1
+        for (int pb = 0; pb < 2; ++pb) {
+            f32x16 kt = {}, vt = {};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const bf16x8 bk = WREG ? fk[s] : *reinterpret_cast<const bf16x8 *>(wk + 16 * s);
+                const bf16x8 bv = WREG ? fv[s] : *reinterpret_cast<const bf16x8 *>(wv + 16 * s);
+                const bf16x8 av = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
+                kt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bk, kt, 0, 0, 0);
+                vt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, vt, 0, 0, 0);
+            }
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool ok = p0 + pb * 32 + lb_row(r, g) < a.n;
+                kt[r] = ok ? kt[r] : -INFINITY;
+                tmax = fmaxf(tmax, kt[r]);
+            }
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+            const float mnew = fmaxf(mrun, tmax);
+            const float f = mrun == -INFINITY ? 0.0f : expf(mrun - mnew);
+            mrun = mnew;
+            float ps = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = kt[r] == -INFINITY ? 0.0f : expf(kt[r] - mnew);
+                kt[r] = e;
+                ps += e;
+            }
+            den = den * f + ps;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ctx[r] *= f;
+            // ctx^T[e][d] += sum_n v[e][n] p[d][n]: k index j of lane group g <-> pixel lb_row(8 s + j, g)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 av, bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    av[j] = (__bf16)vt[8 * s + j];
+                    bp[j] = (__bf16)kt[8 * s + j];
+                }
+                ctx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bp, ctx, 0, 0, 0);
+            }
+        }
+    }
+    den += __shfl_xor(den, 32);
+    float *o = a.part + ((size_t)b * a.nch + ch) * LB_PART + h * (2 * LB_DH + LB_DH * LB_DH);
+    if (g == 0) {
+        o[cl] = mrun;
+        o[LB_DH + cl] = den;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[2 * LB_DH + lb_row(r, g) * LB_DH + cl] = ctx[r];
+}
+
+template <int D>
+__global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
+{
+    constexpr int KS = D / 16, NOB = D / 64;         // o blocks per wave (two waves per pixel block)
+    constexpr bool WREG = D <= 64, WOREG = false;    // W_q / W_out fragments in registers (else L1 / L2)
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[LB_PX][D + 8];
+    __shared__ __attribute__((aligned(16))) __bf16 Hs[LB_PX][LB_HID + 8];
+    __shared__ float red[4][LB_PX];
+    __shared__ float red2[4][32];
+    __shared__ float Cs[LB_HEADS][LB_DH][LB_DH + 1];
+    const int ch = blockIdx.x, b = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = w, g = lane >> 5, cl = lane & 31;
+    // ---- the normalised context of head h (x scale): chunks combined in order, then the memory tokens
+    {
+        const int d = cl;
+        const float *mk = a.mem + ((size_t)(0 * LB_HEADS + h) * LB_DH + d) * a.nmem;
+        float M = -INFINITY;
+        for (int j = 0; j < a.nmem; ++j) M = fmaxf(M, mk[j]);
+        const float *pb0 = a.part + (size_t)b * a.nch * LB_PART + h * (2 * LB_DH + LB_DH * LB_DH);
+        for (int c = 0; c < a.nch; ++c) M = fmaxf(M, pb0[(size_t)c * LB_PART + d]);
+        float den = 0.0f, acc[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        for (int c = 0; c < a.nch; ++c) {
+            const float *pc = pb0 + (size_t)c * LB_PART;
+            const float mc = pc[d];
+            const float f = mc == -INFINITY ? 0.0f : expf(mc - M);
+            den += f * pc[LB_DH + d];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += f * pc[2 * LB_DH + lb_row(r, g) * LB_DH + d];
+        }
+        const float *mv = a.mem + (size_t)(1 * LB_HEADS + h) * LB_DH * a.nmem;
+        for (int j = 0; j < a.nmem; ++j) {
+            const float e = expf(mk[j] - M);
+            den += e;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += e * mv[(size_t)lb_row(r, g) * a.nmem + j];
+        }
+        // lanes d and d + 32 both formed den (same terms): acc rows e split between them
+        const float k = a.scale / den;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Cs[h][d][lb_row(r, g)] = acc[r] * k;
+    }
+    __syncthreads();
+    // A fragments of hidden = ctx^T q: row e = cl, k index j of group g <-> d = lb_row(8 s + j, g)
+    bf16x8 fc[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fc[s][j] = (__bf16)Cs[h][lb_row(8 * s + j, g)][cl];
+    // q rows of head h (A operand, row d = cl) and the wave's W_out rows (A operand, row o)
+    const __bf16 *wq = a.wqkv + (size_t)(h * LB_DH + cl) * D + 8 * g;
+    bf16x8 fq[WREG ? KS : 1];
+    if constexpr (WREG) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) fq[s] = *reinterpret_cast<const bf16x8 *>(wq + 16 * s);
+    }
+    const int pbw = __builtin_amdgcn_readfirstlane(w & 1), obw = __builtin_amdgcn_readfirstlane(w >> 1);   // y tiles:
+                                                     // pixel block pbw, o blocks obw + 2 j
+    const __bf16 *wo = a.wout + (size_t)(obw * 32 + cl) * LB_HID + 8 * g;
+    bf16x8 fo[WOREG ? NOB : 1][8];
+    if constexpr (WOREG) {
+#pragma unroll
+        for (int j = 0; j < NOB; ++j)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) fo[j][s] = *reinterpret_cast<const bf16x8 *>(wo + (size_t)j * 64 * LB_HID + 16 * s);
+    }
+    const float gs = sqrtf((float)D);
+    const int sub0 = ch * a.nsub, sub1 = min(sub0 + a.nsub, (a.n + LB_PX - 1) / LB_PX);
+    float xv[D / 32][8];
+    if (sub0 < sub1) lb_load<D>(a, b, sub0 * LB_PX, xv);
+    for (int sb = sub0; sb < sub1; ++sb) {
+        const int p0 = sb * LB_PX;
+        lb_store<D>(a, xv, Xs, red);                 // (its barrier: Hs / red2 of the previous tile consumed)
+        __syncthreads();
+        if (sb + 1 < sub1) lb_load<D>(a, b, p0 + LB_PX, xv);
+        // q[d][px] of head h, softmax over d (this lane's 16 d and lane ^ 32's), then hidden
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {
+            f32x16 q = {};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const bf16x8 aw = WREG ? fq[s] : *reinterpret_cast<const bf16x8 *>(wq + 16 * s);
+                const bf16x8 bx = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
+                q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bx, q, 0, 0, 0);
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, q[r]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            float sm = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { q[r] = expf(q[r] - mx); sm += q[r]; }
+            sm += __shfl_xor(sm, 32);
+            const float inv = 1.0f / sm;
+            f32x16 hid = {};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 bq;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bq[j] = (__bf16)(q[8 * s + j] * inv);
+                hid = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fc[s], bq, hid, 0, 0, 0);
+            }
+            // hidden[e][px] -> Hs[px][32 h + e]: rows 4 q4 .. 4 q4 + 3 are four consecutive e
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                __attribute__((ext_vector_type(4))) __bf16 o4;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o4[i] = (__bf16)hid[4 * q4 + i];
+                *reinterpret_cast<decltype(o4) *>(&Hs[pb * 32 + cl][h * LB_DH + lb_row(4 * q4, g)]) = o4;
+            }
+        }
+        __syncthreads();
+        // y[o][px] = W_out hidden + b for pixel block pbw, o blocks obw + 2 j; the residual in flight
+        const int px = p0 + pbw * 32 + cl;
+        // residual loads / output stores through buffer resources of sample b: lane offset (pixel, row
+        // group 4 g), the row's plane in an SGPR; pixels past n store to an offset past the buffer
+        const int vo = (min(px, a.n - 1) + 4 * g * a.n) * 4;
+        const int vs = px < a.n ? (px + 4 * g * a.n) * 4 : (int)0x80000000u;
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(a.x + (size_t)b * D * a.n), (short)0, D * a.n * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y + (size_t)b * D * a.n, (short)0,
+                                                                            D * a.n * 4, 0x00020000);
+        float rv[NOB][16];
+#pragma unroll
+        for (int j = 0; j < NOB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                rv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    rx, vo, ((obw + 2 * j) * 32 + (r & 3) + 8 * (r >> 2)) * a.n * 4, 0));
+        f32x16 y[NOB];
+        float ss = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NOB; ++j) {
+            y[j] = f32x16{};
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 aw = WOREG ? fo[j][s]
+                                        : *reinterpret_cast<const bf16x8 *>(wo + (size_t)j * 64 * LB_HID + 16 * s);
+                const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(&Hs[pbw * 32 + cl][16 * s + 8 * g]);
+                y[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bh, y[j], 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float t = y[j][r] + (a.b_out ? a.b_out[(obw + 2 * j) * 32 + lb_row(r, g)] : 0.0f);
+                y[j][r] = t;
+                ss = fmaf(t, t, ss);
+            }
+        }
+        ss += __shfl_xor(ss, 32);
+        if (g == 0) red2[w][cl] = ss;
+        __syncthreads();
+        const float tot = red2[pbw][cl] + red2[pbw + 2][cl];
+        const float k = gs / fmaxf(sqrtf(tot), 1e-12f);
+#pragma unroll
+        for (int j = 0; j < NOB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = (obw + 2 * j) * 32 + lb_row(r, g);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y[j][r] * k * a.g_out[o] + rv[j][r]),
+                                                      ry, vs, ((obw + 2 * j) * 32 + (r & 3) + 8 * (r >> 2)) * a.n * 4, 0);
+            }
+    }
+}
+
 // the halo-staged kernel takes 3x3 / pad 1 convs (plain, with a concatenated skip, or on a nearest-
 // upsampled input) whose tile grid fills the chip; everything else stays on the per-tap kernel
 bool conv3_ok(const rdq_conv_desc *d)
@@ -3177,6 +3514,52 @@ int rdq_linear_attention_block(int32_t B, int32_t heads, int32_t dh, int32_t n, 
     if (dim == 64) launch_la_out_proj<64>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
     else if (dim == 128) launch_la_out_proj<128>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
     else launch_la_out_proj<256>(B, heads, n, fold, scale, qkv, pstat, src, w_out, b_out, g_out, res, y, st);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+// rdq_linear_attention_bf16: pixel chunks of nsub 64-pixel tiles, about 2048 workgroups per launch
+static void lab_split(int B, int n, int *nsub, int *nch)
+{
+    const int tiles = (n + LB_PX - 1) / LB_PX;
+    int s = (int)std::min<int64_t>(16, std::max<int64_t>(2, ((int64_t)tiles * B + 2047) / 2048));
+    s = std::min(s, tiles);
+    *nsub = s;
+    *nch = (tiles + s - 1) / s;
+}
+
+size_t rdq_linear_attention_bf16_ws_bytes(int32_t B, int32_t dim, int32_t n)
+{
+    if (B < 1 || n < 1 || (dim != 64 && dim != 128)) return 0;
+    int nsub, nch;
+    lab_split(B, n, &nsub, &nch);
+    return (size_t)B * nch * LB_PART * sizeof(float);
+}
+
+int rdq_linear_attention_bf16(int32_t B, int32_t dim, int32_t n, int32_t nmem, float scale, const float *x,
+                              const float *g_in, const void *wqkv, const float *mem_kv, const void *wout,
+                              const float *b_out, const float *g_out, float *y, void *ws, size_t ws_bytes,
+                              hipStream_t st)
+{
+    if (B < 1 || n < 1 || nmem < 0 || (dim != 64 && dim != 128) || !x || !g_in || !wqkv ||
+        (nmem > 0 && !mem_kv) || !wout || !g_out || !y || !ws || y == x)
+        return RDQ_E_INVALID;
+    if ((int64_t)B * dim * n >= ((int64_t)1 << 31) || ws_bytes < rdq_linear_attention_bf16_ws_bytes(B, dim, n))
+        return RDQ_E_INVALID;
+    LabArgs a{};
+    a.x = x; a.g_in = g_in; a.mem = mem_kv; a.b_out = b_out; a.g_out = g_out;
+    a.wqkv = static_cast<const __bf16 *>(wqkv); a.wout = static_cast<const __bf16 *>(wout);
+    a.part = static_cast<float *>(ws); a.y = y;
+    a.n = n; a.nmem = nmem; a.scale = scale;
+    lab_split(B, n, &a.nsub, &a.nch);
+    const dim3 grid(a.nch, B);
+    if (dim == 64) {
+        hipLaunchKernelGGL(k_lab_kv<64>, grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_lab_out<64>, grid, dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(k_lab_kv<128>, grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_lab_out<128>, grid, dim3(256), 0, st, a);
+    }
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

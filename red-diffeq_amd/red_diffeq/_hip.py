@@ -126,6 +126,10 @@ SIGNATURES = {
     "rdq_linear_attention_block": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_float, c_void_p,
                                              c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                              c_void_p, c_void_p]),
+    "rdq_linear_attention_bf16_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_linear_attention_bf16": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                            c_void_p]),
     "rdq_full_attention": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "rdq_red_q_sample": (c_int32, [c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

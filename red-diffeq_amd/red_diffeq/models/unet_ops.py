@@ -180,8 +180,12 @@ def rms_conv(x, norm, conv):
 
 def linear_attention(x, m):
     """LinearAttention.forward(x) + x (diffusion.py:182-195 and the residual at 286/297)."""
-    qkv = rms_conv(x, m.norm, m.to_qkv)
     conv = m.to_out[0]
+    if _PREC["mode"] == "bf16" and ops.linear_attn_bf16_fusable(x, m.to_qkv.weight, conv.weight, m.heads):
+        # the whole block in two launches, qkv and the hidden tensor never written (rdq_linear_attention_bf16)
+        return torch.ops.red_diffeq.linear_attn_bf16(x, m.norm.g, m.to_qkv.weight, m.mem_kv, conv.weight, conv.bias,
+                                                     m.to_out[1].g, m.heads, float(m.scale))
+    qkv = rms_conv(x, m.norm, m.to_qkv)
     if _PREC["mode"] == "fp32" and ops.linear_attn_block_fusable(qkv.shape[1], m.heads, conv.weight.shape[0]):
         # context -> (combine, softmax(q) x context, to_out conv, RMSNorm, + x) in one launch (fp32 only: at
         # the configs[4] tile batch under bf16 it measured 1.32 ms per 72 x 72 block against 0.45 + the bf16

@@ -779,6 +779,45 @@ def _(qkv, mem_kv, heads, scale, w_out, b_out, g_out, residual):
     return qkv.new_empty(B, w_out.shape[0], H, W)
 
 
+def linear_attn_bf16_fusable(x, w_qkv, w_out, heads):
+    """rdq_linear_attention_bf16 applies: 4 heads of 32, dim 64 / 128 (the U-Net's 72 / 36 / 18 levels), 1x1 projections."""
+    return (heads == 4 and x.dim() == 4 and x.shape[1] in (64, 128) and tuple(w_qkv.shape) == (384, x.shape[1], 1, 1)
+            and tuple(w_out.shape) == (x.shape[1], 128, 1, 1))
+
+
+@torch.library.custom_op(f"{LIB}::linear_attn_bf16", mutates_args=())
+def linear_attn_bf16(x: Tensor, g_in: Tensor, w_qkv: Tensor, mem_kv: Tensor, w_out: Tensor, b_out: Optional[Tensor],
+                     g_out: Tensor, heads: int, scale: float) -> Tensor:
+    """LinearAttention.forward(x) + x (diffusion.py:182-195, residual 286/297) with bf16 operands and fp32
+    accumulation, two launches (rdq_linear_attention_bf16): the configs[4] batched U-Net."""
+    _hip.require_device(x)
+    if not linear_attn_bf16_fusable(x, w_qkv, w_out, heads):
+        raise ValueError("linear_attn_bf16: shape not supported (see linear_attn_bf16_fusable)")
+    x = x.contiguous()
+    B, D, H, W = x.shape
+    L = _hip.lib()
+    st = _hip.stream_of(x)
+    dq, _ = _conv_desc(x, None, w_qkv, 0, 0)
+    h = torch.empty(B, 128, H, W, device="meta")
+    do, _ = _conv_desc(h, None, w_out, 0, 0)
+    wq = _bf16_pack(w_qkv, dq, st)
+    wo = _bf16_pack(w_out, do, st)
+    nws = int(L.rdq_linear_attention_bf16_ws_bytes(B, D, H * W))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _hip.check(L.rdq_linear_attention_bf16(B, D, H * W, mem_kv.shape[-1], float(scale), _hip.ptr(x),
+                                           _hip.ptr(g_in.contiguous()), _hip.ptr(wq), _hip.ptr(mem_kv.contiguous()),
+                                           _hip.ptr(wo), _hip.ptr(b_out) if b_out is not None else None,
+                                           _hip.ptr(g_out.contiguous()), _hip.ptr(y), _hip.ptr(ws), nws, st),
+               "rdq_linear_attention_bf16")
+    return y
+
+
+@linear_attn_bf16.register_fake
+def _(x, g_in, w_qkv, mem_kv, w_out, b_out, g_out, heads, scale):
+    return torch.empty_like(x)
+
+
 @torch.library.custom_op(f"{LIB}::attn", mutates_args=())
 def attn(qkv: Tensor, mem_kv: Tensor, heads: int) -> Tensor:
     """Attention core with Attend(flash=False) (diffusion.py:209-218): softmax(q k^T d^-1/2) v over
@@ -997,6 +1036,6 @@ for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (co
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
                    (linear_silu_multi, "linear_silu_multi"),
-                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (linear_attn_block, "linear_attn_block"), (attn, "attn"),
+                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (linear_attn_block, "linear_attn_block"), (linear_attn_bf16, "linear_attn_bf16"), (attn, "attn"),
                    (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
     _forward_only(_op, _name)

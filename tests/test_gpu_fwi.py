@@ -343,6 +343,42 @@ def test_persistent_shot_groups_openfwi_ns20(cuda):
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-6
 
 
+@pytest.mark.parametrize("B,ns", [(3, 5), (25, 5)])
+def test_persistent_slice_groups_span_models(cuda, B, ns):
+    """Model batches larger than one resident launch (the reference's OpenFWI config runs 25 models
+    x 5 shots = 125 slices, 8 fit at once) run as persistent launches over consecutive runs of the
+    flat slice index b * ns + s, groups crossing model boundaries: seismograms and exact-order
+    adjoint accumulators bit-exact vs the chunked kernels."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=70, nt=160, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns)
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vnorm(make_model("curvefault", 70, 70, seed=5, batch=B))).to(cuda)
+    plan = fwi._plan(70, 70, v.device)
+    plan.set_tuning(4, 4, 1)
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(11)
+    dseis = torch.from_numpy(rng.standard_normal((B, ns, sz.nrec, plan.ng)).astype(np.float32)).to(cuda)
+    plan.set_variant(adj_exact=True)
+    out = {}
+    for persist in (True, False):
+        plan.set_persistent(persist)
+        info = plan.launch_info(B)
+        assert info["fwd_persistent"] == persist and info["adj_persistent"] == persist
+        if persist:
+            assert info["fwd_launches"] > 1 and info["adj_launches"] > 1   # groups cross model boundaries
+        coeffs, vstat = plan.coeffs(v, 0)
+        seis, hist = plan.forward(coeffs, B, keep_history=True)
+        gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+        plan.status()
+        out[persist] = (seis.cpu().numpy(), gA.cpu().numpy(), gb.cpu().numpy(), gk.view(B, -1).sum(1).cpu().numpy())
+        del hist
+    for a, b in zip(out[True], out[False]):
+        if a.dtype == np.float32:
+            assert bits_equal(a, b)
+        else:
+            np.testing.assert_allclose(a, b, rtol=1e-12)
+
+
 @pytest.mark.parametrize("ns,B", [(8, 1), (3, 2), (20, 1)])
 def test_persistent_xcd_local_equals_write_through(cuda, ns, B):
     """XCD-local slices (pt_assign: L2-resident granule hand-offs between the tiles of a slice on

@@ -263,6 +263,38 @@ def test_linear_attention(cuda, C, H, B):
     close(ops.linear_attention(x, m), R.linear_attention(x, m) + x, rel=1e-5)
 
 
+# the configs[4] batched U-Net's levels (72 / 36 / 18) and ragged pixel counts (10 x 10 = 100, 18 x 18 = 324)
+@pytest.mark.parametrize("C,H,B", [(64, 72, 3), (64, 72, 40), (64, 36, 5), (128, 36, 2), (128, 18, 7), (64, 10, 3)])
+def test_linear_attention_bf16_fused(cuda, C, H, B):
+    """LinearAttention.forward(x) + x in the two-launch bf16 form (rdq_linear_attention_bf16: bf16
+    operands, fp32 accumulation) vs the fp32 torch restatement; new behaviour (configs[4] mixed
+    precision), so the bar is a bf16-level tolerance on the attention output (the residual excluded),
+    recorded next to the unfused bf16 path's deviation on the same inputs."""
+    from red_diffeq.models.diffusion import LinearAttention
+    from red_diffeq.models import unet_ops as ops
+    from red_diffeq import ops as O
+    torch.manual_seed(40 + C + H)
+    m = LinearAttention(C).to(cuda)
+    with torch.no_grad():
+        m.norm.g.mul_(1 + 0.2 * torch.randn_like(m.norm.g))
+        m.to_out[1].g.mul_(1 + 0.2 * torch.randn_like(m.to_out[1].g))
+        m.to_out[0].bias.normal_(0, 0.1)
+    x = torch.randn(B, C, H, H, device=cuda)
+    assert O.linear_attn_bf16_fusable(x, m.to_qkv.weight, m.to_out[0].weight, m.heads)
+    with torch.no_grad():
+        ref = R.linear_attention(x.double(), m.double()).float()
+        m.float()
+        with ops.precision("bf16"):
+            got = ops.linear_attention(x, m) - x
+            qkv = ops.conv2d(ops.rmsnorm(x, m.norm.g), m.to_qkv)
+            unf = ops.rmsnorm(ops.conv2d(torch.ops.red_diffeq.linear_attn(qkv, m.mem_kv, m.heads, float(m.scale)),
+                                         m.to_out[0]), m.to_out[1].g)
+    scale = ref.abs().max().item()
+    record_margin("linear_attention_bf16_unfused_max_rel", f"C={C},H={H},B={B}",
+                  (unf - ref).abs().max().item() / scale, 3e-2)
+    close(got, ref, rel=3e-2, what="fused bf16 vs fp64")
+
+
 # 9 x 9 (the U-Net's level), 8 x 8 and 16 x 16, B = 1 and 2
 @pytest.mark.parametrize("C,H,B", [(256, 9, 2), (512, 9, 1), (256, 8, 1), (128, 16, 1)])
 def test_full_attention(cuda, C, H, B):
@@ -438,6 +470,7 @@ def test_unet_bf16_close_to_fp32(cuda):
         again = net(x, t)
     assert torch.equal(again, ref)
     rel = float((got - ref).norm() / ref.norm())
+    record_margin("unet_bf16_vs_fp32_rel_l2", "dim64 B6", rel, 2e-2)
     assert rel < 2e-2, rel
 
 
