@@ -559,7 +559,7 @@ struct AdjTBArgs {
     double *gk_part;                     // [B*ns][nblk]
     float *gbeta;                        // [B*ns]
     int k0, nsteps, nblk;
-    float w[TB_MAXT];                    // w[k0-1-t]
+    float w[8];                          // w[k0-1-t] (wide kernels: up to TW_ADJ_MAXT steps)
 };
 
 // Adjoint with the same register-region blocking, walking k = k0, k0-1, ...:
@@ -2450,6 +2450,7 @@ struct rdq_fwi_plan {
     int fwd_rw = 6, adj_rw = 6;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave;
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
+    int adj_Tw = 6;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT; profiles/r4/configs4_chunked_ab)
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
@@ -2569,6 +2570,7 @@ void launch_adj(int T, dim3 grid, hipStream_t st, const Args &a)
 // wide chunked regions: forward 16 waves x 8 rows (128 x 128), adjoint 16 waves x 4 rows (128 x 64:
 // its seven two-column fields per row fill the 128 VGPRs of a 1024-thread workgroup)
 constexpr int TW_FWD_NW = 16, TW_FWD_R = 8, TW_ADJ_NW = 16, TW_ADJ_R = 4;
+constexpr int TW_ADJ_MAXT = 6;          // deepest wide adjoint (k_adj_tw instantiations 1 .. 6)
 int tw_tiles_x(int Wp, int T) { return (Wp + (TW_W - 4 * T) - 1) / (TW_W - 4 * T); }
 int tw_tiles_y(int Hp, int T, bool adj)
 {
@@ -2614,7 +2616,11 @@ void launch_adj_w(int T, bool pair, bool exact, dim3 grid, hipStream_t st, const
     case 6: launch_adj_w_T<3, false>(pair, grid, st, a); break;
     case 7: launch_adj_w_T<3, true>(pair, grid, st, a); break;
     case 8: launch_adj_w_T<4, false>(pair, grid, st, a); break;
-    default: launch_adj_w_T<4, true>(pair, grid, st, a); break;
+    case 9: launch_adj_w_T<4, true>(pair, grid, st, a); break;
+    case 10: launch_adj_w_T<5, false>(pair, grid, st, a); break;
+    case 11: launch_adj_w_T<5, true>(pair, grid, st, a); break;
+    case 12: launch_adj_w_T<6, false>(pair, grid, st, a); break;
+    default: launch_adj_w_T<6, true>(pair, grid, st, a); break;
     }
 }
 
@@ -2684,6 +2690,8 @@ unsigned pt_tiles_padded(const rdq_fwi_plan *p, int T, int NW)
 int gk_blocks(const rdq_fwi_plan *p)
 {
     int n = 0;
+    for (int T = 1; T <= TW_ADJ_MAXT; ++T)                                       // wide chunked (128 x 64)
+        n = std::max(n, tw_tiles_x(p->Wp, T) * tw_tiles_y(p->Hp, T, true));
     for (int T = 1; T <= TB_MAXT; ++T) {
         n = std::max(n, tiles_x(p->Wp, T) * tiles_y(p->Hp, T));                  // narrow chunked (64 x 64)
         n = std::max(n, tw_tiles_x(p->Wp, T) * tw_tiles_y(p->Hp, T, true));      // wide chunked (128 x 64)
@@ -2962,7 +2970,7 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     AdjTBArgs a{};
     a.g = tb_geo(p, B);
     const size_t L = a.g.level;
-    const int T = p->adj_T, S = chain_count(p), ns = p->g.ns;
+    const int T = p->wide ? p->adj_Tw : p->adj_T, S = chain_count(p), ns = p->g.ns;
     const int nblk_alloc = gk_blocks(p);
     RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
     RDQ_CHECK(hipMemsetAsync(gA, 0, L * sizeof(float), st));
@@ -2983,7 +2991,7 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
-            for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
+            for (int t = 0; t < 8; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
             const int pin = i & 1, pout = pin ^ 1;
             a.in_l1 = ring + (size_t)(2 * pin) * L;
             a.in_l2 = ring + (size_t)(2 * pin + 1) * L;
@@ -3218,10 +3226,11 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     out[0] = persistent_nw(p, B, false, &perf);
     out[1] = persistent_nw(p, B, true, &pera);
     out[2] = p->fwd_T;
-    out[3] = p->adj_T;
+    const int adjT = !out[1] && p->wide ? p->adj_Tw : p->adj_T;   // chunked adjoint: the wide kernels' depth
+    out[3] = adjT;
     const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
     out[4] = out[0] ? (ns + perf - 1) / perf : (nt + p->fwd_T - 1) / p->fwd_T;
-    out[5] = out[1] ? (ns + pera - 1) / pera : (nt + p->adj_T - 1) / p->adj_T;
+    out[5] = out[1] ? (ns + pera - 1) / pera : (nt + adjT - 1) / adjT;
     return 0;
 }
 

@@ -819,8 +819,9 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
 // the same pass on statistics accumulated by the producing conv (k_conv_cc, a.gnp): wave 0 of each
 // workgroup sums its (sample, group)'s per-tile partials — lane l takes tiles l, l+64, ... of the
 // sample in order, then a fixed xor tree — and the pass adds an optional residual after the SiLU
-// (ResnetBlock's identity shortcut, diffusion.py:168)
-template <bool SMALL>
+// (ResnetBlock's identity shortcut, diffusion.py:168).  V float4 per thread (large batches: V = 4, so
+// the per-workgroup statistics reduction is paid once per 4096 elements instead of 1024)
+template <bool SMALL, int V = 1>
 __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const float *__restrict__ x,
                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
                                                     const float *__restrict__ ss, const double *__restrict__ gnp,
@@ -834,11 +835,15 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     // this thread's elements, residual and channel constants are loaded first (independent of the
     // statistics), so the statistics reduction below overlaps their latency
     const bool vec = (HW & 3) == 0;
-    const int i4 = (ch * 256 + (int)threadIdx.x) * 4;
-    float4 v = {0.0f, 0.0f, 0.0f, 0.0f}, r = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (!SMALL && vec && i4 < HW) {
-        v = *reinterpret_cast<const float4 *>(x + base + i4);
-        if (post) r = *reinterpret_cast<const float4 *>(post + base + i4);
+    float4 v[V], r[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int i4 = ((ch * V + k) * 256 + (int)threadIdx.x) * 4;
+        v[k] = r[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (!SMALL && vec && i4 < HW) {
+            v[k] = *reinterpret_cast<const float4 *>(x + base + i4);
+            if (post) r[k] = *reinterpret_cast<const float4 *>(post + base + i4);
+        }
     }
     const float ga = gamma[c], be = beta[c];
     const bool sso = ss != nullptr;
@@ -882,17 +887,22 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
         return;
     }
     if (vec) {
-        if (i4 < HW) {
-            v.x = gn_silu1(v.x, mean, rstd, ga, be, sso, sc1, sh);
-            v.y = gn_silu1(v.y, mean, rstd, ga, be, sso, sc1, sh);
-            v.z = gn_silu1(v.z, mean, rstd, ga, be, sso, sc1, sh);
-            v.w = gn_silu1(v.w, mean, rstd, ga, be, sso, sc1, sh);
-            if (post) { v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w; }
-            *reinterpret_cast<float4 *>(y + base + i4) = v;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const int i4 = ((ch * V + k) * 256 + (int)threadIdx.x) * 4;
+            if (i4 < HW) {
+                float4 u = v[k];
+                u.x = gn_silu1(u.x, mean, rstd, ga, be, sso, sc1, sh);
+                u.y = gn_silu1(u.y, mean, rstd, ga, be, sso, sc1, sh);
+                u.z = gn_silu1(u.z, mean, rstd, ga, be, sso, sc1, sh);
+                u.w = gn_silu1(u.w, mean, rstd, ga, be, sso, sc1, sh);
+                if (post) { u.x += r[k].x; u.y += r[k].y; u.z += r[k].z; u.w += r[k].w; }
+                *reinterpret_cast<float4 *>(y + base + i4) = u;
+            }
         }
     } else {
-        const int e1 = min(HW, (ch + 1) * 1024);
-        for (int i = ch * 1024 + (int)threadIdx.x; i < e1; i += 256) {
+        const int e1 = min(HW, (ch + 1) * 1024 * V);
+        for (int i = ch * 1024 * V + (int)threadIdx.x; i < e1; i += 256) {
             float u = gn_silu1(x[base + i], mean, rstd, ga, be, sso, sc1, sh);
             if (post) u += post[base + i];
             y[base + i] = u;
@@ -2270,10 +2280,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 #pragma unroll
         for (int k = 0; k < C3_NI; ++k) hstore(0, k, hpack(v[k], ok[k]));
     }
-    // weight ring: three taps in registers, fetched two taps before their stash
+    // weight ring: three taps in registers; tap s is fetched at tap s - 3 into the slot tap s - 3 left
+    // (stashed at the end of tap s - 4) and stashed at the end of tap s - 1: two taps of latency
     bf16x8 wr[3];
     wr[0] = wload(0, 0);
     wr[1] = wload(0, 1);
+    wr[2] = wload(0, 2);
     wstash(0, wr[0]);
     __syncthreads();
 
@@ -2289,7 +2301,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int s = cc * 9 + t;
-            wr[(t + 2) % 3] = wload(min(cc + (t + 2) / 9, a.cch - 1), (t + 2) % 9);
+            wr[t % 3] = wload(min(cc + (t + 3) / 9, a.cch - 1), (t + 3) % 9);
             if constexpr (PF) {
 #pragma unroll
                 for (int k = 0; k < C3_NI; ++k)
@@ -2828,9 +2840,11 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 }  // namespace
 
 // the small-image form is its own instantiation (the per-channel form's code is unchanged by it)
+// (gn4: gn_grid chose 4096-element chunks: the k_gn_apply_t<false, 4> instantiation)
 #define LAUNCH_GN_T(GRID, ST, ...)                                                                     \
     do {                                                                                               \
         if (nch < 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<true>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
+        else if (gn4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false, 4>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
         else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false>), GRID, dim3(256), 0, ST, __VA_ARGS__);      \
     } while (0)
 #define LAUNCH_GN(GRID, ST, ...)                                                                       \
@@ -2842,16 +2856,20 @@ bool conv_desc_ok(const rdq_conv_desc *d)
 // GroupNorm pass grid: one workgroup per (channel, 1024-element chunk) of a group, or for images of
 // <= 512 pixels in grids of more than 8192 workgroups -nch = 1024 / HW whole channels per workgroup
 // (9 x 9 at B = 344 had 176 K workgroups of 81 elements each: 138 -> 10 us per pass; at B = 1 the
-// per-channel form is faster); returns the x extent, *nch the kernels' chunk argument
-static int gn_grid(int B, int C, int G, int HW, int *nch)
+// per-channel form is faster); returns the x extent, *nch the kernels' chunk argument.  With gn4
+// (callers of k_gn_apply_t only) batched sizes of >= 16 M elements take 4096-element chunks
+static int gn_grid(int B, int C, int G, int HW, int *nch, bool *gn4 = nullptr)
 {
     const int cpg = C / G;
+    if (gn4) *gn4 = false;
     if (HW <= 512 && (int64_t)C * B > 8192) {
         const int cpb = 1024 / HW;
         *nch = -cpb;
         return (cpg + cpb - 1) / cpb;
     }
-    *nch = (HW + 1023) / 1024;
+    const int chunk = gn4 && (int64_t)B * C * HW >= (1 << 24) ? 4096 : 1024;
+    if (gn4) *gn4 = chunk == 4096;
+    *nch = (HW + chunk - 1) / chunk;
     return cpg * *nch;
 }
 
@@ -3005,7 +3023,8 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     }
     const int C = d->cout, HW = c.HW;
     int nch = 0;
-    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    bool gn4 = false;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, gnp, eps, post_residual, y);
     RDQ_CHECK(hipGetLastError());
@@ -3078,7 +3097,8 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
     hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
     const int C = d->cout, HW = c.HW;
     int nch = 0;
-    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    bool gn4 = false;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
                        scale_shift, c.gnp, eps, nullptr, y);
     RDQ_CHECK(hipGetLastError());
@@ -3117,7 +3137,8 @@ int rdq_conv2d_gn_silu_lsm(const rdq_conv_desc *d, const float *x, const float *
                            nlsm, per_b);
     const int C = d->cout, HW = c.HW;
     int nch = 0;
-    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    bool gn4 = false;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
                        ss_index >= 0 ? ly[ss_index] : nullptr, c.gnp, eps, post_residual, y);
     RDQ_CHECK(hipGetLastError());
@@ -3338,7 +3359,8 @@ int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float 
     if (!y || !gamma || !beta || !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st)) return RDQ_E_INVALID;
     const int C = d->cout, HW = c.HW;
     int nch = 0;
-    const int gxa = gn_grid(d->B, C, G, HW, &nch);
+    bool gn4 = false;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
                        scale_shift, c.gnp, eps, post_residual, y, C3_BM);
     RDQ_CHECK(hipGetLastError());

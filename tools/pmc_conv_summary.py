@@ -1,11 +1,12 @@
 """MFMA utilisation of the U-Net conv kernels from one rocprofv3 --pmc pass (tools/gpu_conv_pmc.sh):
 per dispatch of k_conv_cc, SQ_VALU_MFMA_BUSY_CYCLES (summed over the SIMDs) against the dispatch's
 duration x clock x 1024 SIMDs, plus the wave-level busy / wait fractions.
-python tools/pmc_conv_summary.py <pass dir> <label> [clock GHz]"""
+python tools/pmc_conv_summary.py <pass dir> <label> [clock GHz]   (PMC_KERNEL: kernel name filter)"""
 import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 d, label = sys.argv[1], sys.argv[2]
@@ -13,7 +14,7 @@ ghz = float(sys.argv[3]) if len(sys.argv) > 3 else 2.4
 per = collections.defaultdict(dict)
 for f in glob.glob(d + "/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "k_conv_cc" not in r["Kernel_Name"]:
+        if os.environ.get("PMC_KERNEL", "k_conv_cc") not in r["Kernel_Name"]:
             continue
         k = r["Dispatch_Id"]
         per[k][r["Counter_Name"]] = float(r["Counter_Value"])
