@@ -138,6 +138,18 @@ size_t rdq_conv2d_bf16_gn_ws_bytes(const rdq_conv_desc *d, int32_t G);
 int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                             int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
                             const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
+/* The same Block for a ResnetBlock's block1, whose output feeds only block2's conv (diffusion.py:166-167):
+ * y8 = bf16(SiLU(GroupNorm(conv3x3(cat(x, x2)))...)) stored as channel octets [B][cout / 8][H*W][8]
+ * (cout % 8 == 0) -- the rounding block2's bf16 conv applies to its operands anyway, so the pair is
+ * bit-identical to rdq_conv2d_bf16_gn_silu twice; ws: rdq_conv2d_bf16_gn_ws_bytes. */
+int rdq_conv2d_bf16_gn_silu8(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp,
+                             const float *bias, int32_t G, float eps, const float *gamma, const float *beta,
+                             const float *scale_shift, void *y8, void *ws, size_t ws_bytes, hipStream_t stream);
+/* block2 of that pair: rdq_conv2d_bf16_gn_silu on the octet input x8 (d: plain mode, cin2 = 0,
+ * cin1 % 32 == 0). */
+int rdq_conv2d_bf16_gn_silu_x8(const rdq_conv_desc *d, const void *x8, const void *wp, const float *bias, int32_t G,
+                               float eps, const float *gamma, const float *beta, const float *scale_shift,
+                               const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
 /* rdq_conv2d_gn_silu_out's tail (final_res_block's block2 + final_conv, diffusion.py:299-301) on the bf16
  * halo-staged conv: yf = conv1x1(Block_bf16(x) [+ post_residual], wf) + bf; ws: rdq_conv2d_bf16_gn_ws_bytes. */

@@ -32,6 +32,7 @@ namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 
 // ------------------------------------------------------------------------------------ conv2d
 // Implicit GEMM on the fp32 matrix cores: D[cout][pixel] = W[cout][k] x A[k][pixel], k = (ci, ky, kx).
@@ -907,6 +908,72 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
             if (post) u += post[base + i];
             y[base + i] = u;
         }
+    }
+}
+
+// k_gn_apply_t's pass for a Block whose output feeds ONLY the next 3x3 bf16 conv (ResnetBlock's block1,
+// diffusion.py:166-167): the same per-element arithmetic (statistics from the conv's per-tile
+// partials, GN -> scale / shift -> SiLU), rounded to bf16 and stored as channel octets
+// [B][C / 8][HW][8], the layout k_conv3_bf16<.., IN8> gathers with one 16-byte load per pixel.  The
+// consumer rounds its operands to bf16 anyway, so its result is bit-identical to the fp32 path's
+// while this pass writes half the bytes and the conv reads half.  Workgroup: 256 pixels of one
+// (sample, group), every octet of the group.
+__global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const float *__restrict__ x,
+                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                   const float *__restrict__ ss, const double *__restrict__ gnp,
+                                                   float eps, __bf16 *__restrict__ y, int bm)
+{
+    const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
+    const int p = blockIdx.x * 256 + (int)threadIdx.x;
+    __shared__ float st2[2];
+    if (threadIdx.x < 64) {                     // (sample, group) statistics: k_gn_apply_t's reduction
+        const int lane = threadIdx.x;
+        const int mlo = (int)(((int64_t)b * HW) / bm), mhi = (int)(((int64_t)(b + 1) * HW - 1) / bm);
+        double s = 0.0, q = 0.0;
+        for (int mt = mlo + lane; mt <= mhi; mt += 64) {
+            const int slot = (int)(((int64_t)mt * bm) / HW) == b ? 0 : 1;
+            const double *pp = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
+            s += pp[0];
+            q += pp[1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            q += __shfl_xor(q, o, 64);
+        }
+        if (lane == 0) {
+            const double n = (double)cpg * HW, mean = s / n;
+            double var = q / n - mean * mean;
+            var = var < 0.0 ? 0.0 : var;
+            st2[0] = (float)mean;
+            st2[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+    }
+    // this thread's first octet in flight behind the statistics
+    const int pc = min(p, HW - 1);
+    const float *xb = x + ((size_t)b * C + g * cpg) * HW + pc;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = xb[(size_t)j * HW];
+    __syncthreads();
+    const float mean = st2[0], rstd = st2[1];
+    const bool sso = ss != nullptr;
+    for (int o = 0; o < cpg / 8; ++o) {
+        float nx[8];
+        if (o + 1 < cpg / 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nx[j] = xb[(size_t)(8 * (o + 1) + j) * HW];
+        }
+        bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = g * cpg + 8 * o + j;
+            const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
+            h[j] = (__bf16)gn_silu1(v[j], mean, rstd, gamma[c], beta[c], sso, sc1, sh);
+        }
+        if (p < HW) *reinterpret_cast<bf16x8 *>(y + (((size_t)b * (C >> 3) + (g * cpg >> 3) + o) * HW + p) * 8) = h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = nx[j];
     }
 }
 
@@ -1979,7 +2046,6 @@ void launch_conv_ig(dim3 grid, hipStream_t st, const IgArgs &a)
 // stores 32 consecutive pixels of one output channel) x 32*NB output channels (the A operand).
 // mfma_f32_32x32x16_bf16 lane maps: A[row l&31][k 8(l>>5)+j], B[k 8(l>>5)+j][col l&31],
 // D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31] (cdna_hip_programming.md §3).
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 constexpr int BF_BM = 128, BF_BK = 32, BF_LD = BF_BK + 8;   // LDS rows of 80 B
 
 struct BfArgs {
@@ -2184,13 +2250,14 @@ constexpr int C3_ROWS = C3_BM + 2 * C3_WMAX + 2;  // 402 <= 64 * C3_NI
 struct C3Args {
     rdq_conv_desc d;
     const float *x, *x2, *bias, *res;
+    const __bf16 *x8;                // IN8: the input as bf16 octets [B][cin / 8][H W][8] (cin2 = 0)
     const __bf16 *w;                 // [cout][9][cinp]
     float *y;
     double *gnp;                     // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
     int cinp, K, M, HW, R, cch, plane, G;
 };
 
-template <int MODE>
+template <int MODE, bool IN8 = false>
 __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 {
     __shared__ __attribute__((aligned(16))) __bf16 Hs[2][C3_ROWS][BF_LD];     // 2 x 31.4 KiB
@@ -2218,6 +2285,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
     // one item's 8 channels of chunk cc: unconditional loads at 32-bit offsets from a wave-uniform
     // base (offset 0 where the item is empty), so the compiler never waits per load; the zeroing
     // happens when the item is rounded
+    // IN8: the item's 8 channels are one 16-byte load of the packed bf16 input (already rounded)
+    auto hload8 = [&](int k, int cc, bf16x8 &v) -> bool {
+        const unsigned s = it_src[k];
+        const bool ok = s != ~0u;
+        const unsigned o = ok ? (((s >> 20) * (unsigned)(d.cin1 >> 3) + (unsigned)(cc * 4 + wv)) * (unsigned)a.plane +
+                                 (s & 0xfffff)) * 8u
+                              : 0u;
+        v = *reinterpret_cast<const bf16x8 *>(a.x8 + o);
+        return ok;
+    };
     auto hload = [&](int k, int cc, float (&v)[8]) -> bool {
         const unsigned s = it_src[k];
         const int c = cc * BF_BK + 8 * wv;
@@ -2272,7 +2349,14 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) acc[c][mb] = f32x16{};
 
-    {   // chunk 0's halo
+    if constexpr (IN8) {   // chunk 0's halo
+        bf16x8 v[C3_NI];
+        bool ok[C3_NI];
+#pragma unroll
+        for (int k = 0; k < C3_NI; ++k) ok[k] = hload8(k, 0, v[k]);
+#pragma unroll
+        for (int k = 0; k < C3_NI; ++k) hstore(0, k, ok[k] ? v[k] : bf16x8{});
+    } else {
         float v[C3_NI][8];
         bool ok[C3_NI];
 #pragma unroll
@@ -2295,7 +2379,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
         // halo item k of the next chunk: issued at tap IT[k], rounded and stored four taps later
         // (at most six items in flight: slot k % 6)
         constexpr int IT[C3_NI] = {0, 0, 1, 1, 2, 3, 4};
-        float hv[6][8];
+        float hv[IN8 ? 1 : 6][8];
+        bf16x8 hv8[IN8 ? 6 : 1];
         bool hok[6];
         const int hb = cc & 1;
 #pragma unroll
@@ -2305,10 +2390,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
             if constexpr (PF) {
 #pragma unroll
                 for (int k = 0; k < C3_NI; ++k)
-                    if (IT[k] + 4 == t) hstore(hb ^ 1, k, hpack(hv[k % 6], hok[k % 6]));
+                    if (IT[k] + 4 == t) {
+                        if constexpr (IN8) hstore(hb ^ 1, k, hok[k % 6] ? hv8[k % 6] : bf16x8{});
+                        else hstore(hb ^ 1, k, hpack(hv[k % 6], hok[k % 6]));
+                    }
 #pragma unroll
                 for (int k = 0; k < C3_NI; ++k)
-                    if (IT[k] == t) hok[k % 6] = hload(k, cc + 1, hv[k % 6]);
+                    if (IT[k] == t) {
+                        if constexpr (IN8) hok[k % 6] = hload8(k, cc + 1, hv8[k % 6]);
+                        else hok[k % 6] = hload(k, cc + 1, hv[k % 6]);
+                    }
             }
             const int toff = (t / 3) * d.W + t % 3;
             const __bf16 *wsb = &Ws[s & 1][0][0];
@@ -3325,10 +3416,14 @@ int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float 
 
 // conv3x3_bf16 + GroupNorm statistics in its epilogue (as rdq_conv2d_bf16_gn_silu), conv output in ws
 static bool bf16_gn_conv(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
-                         int32_t G, void *ws, size_t ws_bytes, C3Args &c, hipStream_t st)
+                         int32_t G, void *ws, size_t ws_bytes, C3Args &c, hipStream_t st, const void *x8 = nullptr)
 {
     const size_t need = rdq_conv2d_bf16_gn_ws_bytes(d, G);
-    if (!need || !x || !wp || !ws || ws_bytes < need || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+    if (!need || !(x || x8) || !wp || !ws || ws_bytes < need || (d->cin2 > 0 && !x2 && d->in_mode == RDQ_IN_PLAIN))
+        return false;
+    // packed bf16 octet input: plain mode, one input tensor, channel count a multiple of the 32-deep chunk
+    if (x8 && (d->in_mode != RDQ_IN_PLAIN || d->cin2 != 0 || d->cin1 % BF_BK ||
+               (int64_t)d->B * d->cin1 * d->H * d->W >= ((int64_t)1 << 32)))
         return false;
     const size_t M = (size_t)d->B * d->H * d->W;
     float *h = static_cast<float *>(ws);
@@ -3343,12 +3438,47 @@ static bool bf16_gn_conv(const rdq_conv_desc *d, const float *x, const float *x2
     c.R = C3_BM + 2 * d->W + 2;
     c.cch = c.cinp / BF_BK;
     c.plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? c.HW / 4 : c.HW;
+    c.x8 = static_cast<const __bf16 *>(x8);
     const dim3 grid((c.M + C3_BM - 1) / C3_BM, d->cout / C3_BN);
-    if (d->in_mode == RDQ_IN_UPSAMPLE2)
+    if (x8)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_PLAIN, true>), grid, dim3(256), 0, st, c);
+    else if (d->in_mode == RDQ_IN_UPSAMPLE2)
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_bf16<RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
     return true;
+}
+
+int rdq_conv2d_bf16_gn_silu8(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp,
+                             const float *bias, int32_t G, float eps, const float *gamma, const float *beta,
+                             const float *scale_shift, void *y8, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    C3Args c;
+    if (!y8 || !gamma || !beta || d->cout % 8 || (int64_t)d->B * d->cout * d->H * d->W >= ((int64_t)1 << 32) ||
+        !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st))
+        return RDQ_E_INVALID;
+    const int HW = c.HW;
+    hipLaunchKernelGGL(k_gn_apply8, dim3((HW + 255) / 256, d->B * G), dim3(256), 0, st, d->cout, HW, G, c.y, gamma,
+                       beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+int rdq_conv2d_bf16_gn_silu_x8(const rdq_conv_desc *d, const void *x8, const void *wp, const float *bias, int32_t G,
+                               float eps, const float *gamma, const float *beta, const float *scale_shift,
+                               const float *post_residual, float *y, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    C3Args c;
+    if (!y || !gamma || !beta || !x8 || !bf16_gn_conv(d, nullptr, nullptr, wp, bias, G, ws, ws_bytes, c, st, x8))
+        return RDQ_E_INVALID;
+    const int C = d->cout, HW = c.HW;
+    int nch = 0;
+    bool gn4 = false;
+    const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
+    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
+                       scale_shift, c.gnp, eps, post_residual, y, C3_BM);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
 }
 
 int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,

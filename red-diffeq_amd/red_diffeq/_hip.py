@@ -106,6 +106,12 @@ SIGNATURES = {
     "rdq_conv2d_bf16_gn_silu": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                           c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_size_t, c_void_p]),
+    "rdq_conv2d_bf16_gn_silu8": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                           c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p]),
+    "rdq_conv2d_bf16_gn_silu_x8": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_int32, c_float,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                             c_void_p]),
     "rdq_conv2d_bf16_gn_silu_out": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -123,8 +123,14 @@ class ResnetBlock(nn.Module):
                                                      self.res_conv)
             if pair is not None:
                 return self.block2(pair[0], post=pair[1])
-            h = self.block2(self.block1(x, scale_shift=scale_shift, skip=skip))
+            h = ops.block_pair(x, skip, self.block1, self.block2, scale_shift)   # bf16: one hand-off in bf16
+            if h is None:
+                h = self.block2(self.block1(x, scale_shift=scale_shift, skip=skip))
             return ops.conv2d(x, self.res_conv, x2=skip, residual=h)    # h + res_conv(x), fused
+        if skip is None:
+            h = ops.block_pair(x, None, self.block1, self.block2, scale_shift, post=x)
+            if h is not None:
+                return h
         h = self.block1(x, scale_shift=scale_shift, skip=skip)
         if skip is not None:
             x = torch.cat((x, skip), dim=1)

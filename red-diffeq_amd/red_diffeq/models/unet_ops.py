@@ -150,6 +150,28 @@ def conv_group_norm_silu(x, conv, norm, scale_shift=None, skip=None, post=None):
     return h + post if post is not None else h
 
 
+def block_pair(x, skip, block1, block2, scale_shift=None, post=None):
+    """block2(block1(cat(x, skip), scale_shift)) [+ post] (ResnetBlock, diffusion.py:160-168) in the bf16
+    form that hands block1's output to block2 as bf16 channel octets (conv2d_bf16_block_pair: bit-identical
+    to the two Block calls); None where that form does not apply (fp32, or shapes outside the fused conv)."""
+    if _PREC["mode"] != "bf16":
+        return None
+    c1, c2 = block1.proj, block2.proj
+    if any((cv.padding[0] if isinstance(cv.padding, tuple) else int(cv.padding)) != 1 for cv in (c1, c2)):
+        return None
+    G = block1.norm.num_groups
+    if block2.norm.num_groups != G or c1.weight.shape[0] % 32:
+        return None
+    hmeta = torch.empty((x.shape[0], c1.weight.shape[0], x.shape[2], x.shape[3]), device="meta")
+    if not (ops.conv_gn_bf16_fusable(x, skip, c1.weight, 1, PLAIN, G) and
+            ops.conv_gn_bf16_fusable(hmeta, None, c2.weight, 1, PLAIN, G)):
+        return None
+    return torch.ops.red_diffeq.conv2d_bf16_block_pair(x, skip, c1.weight, c1.bias, block1.norm.weight, block1.norm.bias,
+                                                       scale_shift, float(block1.norm.eps), c2.weight, c2.bias,
+                                                       block2.norm.weight, block2.norm.bias, float(block2.norm.eps), G,
+                                                       post)
+
+
 def conv_group_norm_silu_shortcut(x, conv, norm, scale_shift, skip, res_conv):
     """(Block.forward(cat(x, skip)), res_conv(cat(x, skip))) of a ResnetBlock with a 1x1 shortcut: both
     convs in one launch (rdq_conv2d_gn_silu_sc) where that form applies (fp32), else None."""
@@ -220,6 +242,6 @@ def red_epilogue(diff, xt, t, eps_hat, eps):
                                         diff.sqrt_recipm1_alphas_cumprod)
 
 
-HIP_OPS = {"head", "first_block_and_scale_shifts", "last_block_and_out", "conv2d", "conv_group_norm_silu", "conv_group_norm_silu_shortcut", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
+HIP_OPS = {"head", "first_block_and_scale_shifts", "last_block_and_out", "conv2d", "conv_group_norm_silu", "conv_group_norm_silu_shortcut", "block_pair", "linear", "time_mlp", "resnet_scale_shifts", "sinusoidal", "group_norm_affine_silu", "rmsnorm", "linear_attention",
            "full_attention", "red_q_sample", "red_q_sample_into", "red_epilogue"}
 del math

@@ -445,6 +445,46 @@ def _(x, x2, weight, bias, pad, mode, gamma, beta, scale_shift, groups, eps, pos
     return x.new_empty(shape)
 
 
+@torch.library.custom_op(f"{LIB}::conv2d_bf16_block_pair", mutates_args=())
+def conv2d_bf16_block_pair(x: Tensor, x2: Optional[Tensor], w1: Tensor, b1: Optional[Tensor], gamma1: Tensor, beta1: Tensor,
+                           scale_shift: Optional[Tensor], eps1: float, w2: Tensor, b2: Optional[Tensor], gamma2: Tensor,
+                           beta2: Tensor, eps2: float, groups: int, post: Optional[Tensor]) -> Tensor:
+    """ResnetBlock's block2(block1(cat(x, x2), scale_shift)) [+ post] on the bf16 halo-staged conv
+    (diffusion.py:160-168): block1's normalised output is written as bf16 channel octets, the rounding
+    block2's conv applies to its operands anyway (rdq_conv2d_bf16_gn_silu8 / _x8): bit-identical to two
+    conv2d_bf16_gn_silu calls, half the bytes between them."""
+    _hip.require_device(x)
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    d1, shape1 = _conv_desc(x, x2, w1, 1, 0)
+    d2, shape2 = _conv_desc(torch.empty(shape1, device="meta"), None, w2, 1, 0)
+    L = _hip.lib()
+    n1 = int(L.rdq_conv2d_bf16_gn_ws_bytes(ctypes.byref(d1), int(groups)))
+    n2 = int(L.rdq_conv2d_bf16_gn_ws_bytes(ctypes.byref(d2), int(groups)))
+    if n1 == 0 or n2 == 0 or not bf16_eligible(w1) or not bf16_eligible(w2) or shape1[1] % 32:
+        raise ValueError("conv2d_bf16_block_pair: shapes not supported (see unet_ops.block_pair)")
+    st = _hip.stream_of(x)
+    wp1, wp2 = _bf16_pack(w1, d1, st), _bf16_pack(w2, d2, st)
+    ws = torch.empty(max(n1, n2), dtype=torch.uint8, device=x.device)
+    B, C1, H, W = shape1
+    h8 = torch.empty((B, C1 // 8, H, W, 8), device=x.device, dtype=torch.bfloat16)
+    y = torch.empty(shape2, device=x.device, dtype=torch.float32)
+    ss = scale_shift.contiguous() if scale_shift is not None else None
+    pr = post.contiguous() if post is not None else None
+    _hip.check(L.rdq_conv2d_bf16_gn_silu8(ctypes.byref(d1), _hip.ptr(x), _hip.ptr(x2), _hip.ptr(wp1), _hip.ptr(b1),
+                                          int(groups), float(eps1), _hip.ptr(gamma1), _hip.ptr(beta1), _hip.ptr(ss),
+                                          _hip.ptr(h8), _hip.ptr(ws), n1, st), "rdq_conv2d_bf16_gn_silu8")
+    _hip.check(L.rdq_conv2d_bf16_gn_silu_x8(ctypes.byref(d2), _hip.ptr(h8), _hip.ptr(wp2), _hip.ptr(b2), int(groups),
+                                            float(eps2), _hip.ptr(gamma2), _hip.ptr(beta2), None, _hip.ptr(pr),
+                                            _hip.ptr(y), _hip.ptr(ws), n2, st), "rdq_conv2d_bf16_gn_silu_x8")
+    return y
+
+
+@conv2d_bf16_block_pair.register_fake
+def _(x, x2, w1, b1, gamma1, beta1, scale_shift, eps1, w2, b2, gamma2, beta2, eps2, groups, post):
+    return x.new_empty((x.shape[0], w2.shape[0], x.shape[2], x.shape[3]))
+
+
 @torch.library.custom_op(f"{LIB}::conv2d_bf16_gn_silu_out", mutates_args=())
 def conv2d_bf16_gn_silu_out(x: Tensor, weight: Tensor, bias: Optional[Tensor], pad: int, gamma: Tensor, beta: Tensor,
                             scale_shift: Optional[Tensor], groups: int, eps: float, post: Optional[Tensor],
@@ -1032,6 +1072,7 @@ def _forward_only(op, name):
 
 for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (conv2d_gn_silu, "conv2d_gn_silu"), (conv2d_gn_silu_sc, "conv2d_gn_silu_sc"),
                    (conv2d_bf16_gn_silu, "conv2d_bf16_gn_silu"), (conv2d_bf16_gn_silu_out, "conv2d_bf16_gn_silu_out"),
+                   (conv2d_bf16_block_pair, "conv2d_bf16_block_pair"),
                    (conv2d_gn_silu_lsm, "conv2d_gn_silu_lsm"), (conv2d_gn_silu_out, "conv2d_gn_silu_out"), (unet_head, "unet_head"),
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),

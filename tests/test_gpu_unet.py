@@ -454,6 +454,35 @@ def test_conv_bf16_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post, mode):
     close(got, ref, rel=1e-5)
 
 
+# (batches large enough for the halo-staged conv: >= 512 tiles of 256 pixels x 64 channels)
+@pytest.mark.parametrize("cin1,cin2,cout,H,B,ss,post", [(64, 0, 64, 72, 26, True, True), (64, 64, 64, 72, 27, True, False),
+                                                       (128, 0, 128, 36, 64, False, True), (128, 128, 256, 18, 120, True, False)])
+def test_bf16_block_pair_bitexact(cuda, cin1, cin2, cout, H, B, ss, post):
+    """ResnetBlock's block1 -> block2 with block1's output handed over as bf16 channel octets
+    (conv2d_bf16_block_pair) vs the two Block calls in fp32 storage: bit-identical (block2's conv rounds
+    its operands to bf16 either way)."""
+    torch.manual_seed(21)
+    c1 = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    c2 = nn.Conv2d(cout, cout, 3, padding=1).to(cuda)
+    n1, n2 = nn.GroupNorm(8, cout).to(cuda), nn.GroupNorm(8, cout).to(cuda)
+    with torch.no_grad():
+        for n in (n1, n2):
+            n.weight.normal_(1, 0.2)
+            n.bias.normal_(0, 0.2)
+    x = torch.randn(B, cin1, H, H, device=cuda)
+    x2 = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    sc = torch.randn(B, 2 * cout, device=cuda) * 0.3 if ss else None
+    pr = torch.randn(B, cout, H, H, device=cuda) if post else None
+    with torch.no_grad():
+        got = torch.ops.red_diffeq.conv2d_bf16_block_pair(x, x2, c1.weight, c1.bias, n1.weight, n1.bias, sc, 1e-5,
+                                                          c2.weight, c2.bias, n2.weight, n2.bias, 1e-5, 8, pr)
+        h = torch.ops.red_diffeq.conv2d_bf16_gn_silu(x, x2, c1.weight, c1.bias, 1, 0, n1.weight, n1.bias, sc, 8, 1e-5,
+                                                     None)
+        ref = torch.ops.red_diffeq.conv2d_bf16_gn_silu(h, None, c2.weight, c2.bias, 1, 0, n2.weight, n2.bias, None, 8,
+                                                       1e-5, pr)
+    assert torch.equal(got, ref), (got - ref).abs().max().item()
+
+
 def test_unet_bf16_close_to_fp32(cuda):
     """Whole U-Net (reference architecture, dim 64) with bf16 convolutions vs fp32: new behaviour
     (configs[4]), no reference counterpart; the deviation is bounded, not bitwise."""
