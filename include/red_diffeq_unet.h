@@ -111,6 +111,12 @@ int rdq_unet_head(const rdq_conv_desc *d, const float *x, const float *w, const 
                   float theta, const int64_t *t, const float *w1, const float *b1, int32_t hid, const float *w2,
                   const float *b2, int32_t out, float *temb, hipStream_t stream);
 
+/* Unet.init_conv (Conv2d(1, 64, 7, padding=3), fp32) as a direct conv: one thread per output pixel and
+ * all 64 channels (the batched bf16 U-Net's stem; the fp32 reference path keeps rdq_conv2d / the fused
+ * head).  d: cin1 = 1, cin2 = 0, 7 x 7, pad 3, cout 64, plain mode, 64 <= W <= 72; RDQ_E_INVALID otherwise. */
+int rdq_conv2d_stem(const rdq_conv_desc *d, const float *x, const float *w, const float *bias, float *y,
+                    hipStream_t stream);
+
 /* Mixed-precision conv2d (same input modes and epilogue): bf16 operands, fp32 accumulation on
  * v_mfma_f32_32x32x16_bf16.  The weights are packed once by rdq_conv2d_bf16_pack into
  * wp[cout][kh*kw][cinp] bf16 (round-to-nearest-even, cinp = cin1+cin2 rounded up to 32, zero-padded;

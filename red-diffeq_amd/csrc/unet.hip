@@ -2542,6 +2542,54 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
     }
 }
 
+// ------------------------------------------------------ stem conv (7 x 7, one input channel)
+// Unet.init_conv = Conv2d(1, 64, 7, padding=3) of the batched bf16 U-Net (an fp32 conv there: its K =
+// 49 is below the bf16 path's floor).  The implicit GEMM spends its time gathering 49 taps of one
+// channel per K step; here a thread owns one output pixel and all 64 channels: its 7 x 7 window from
+// an LDS copy of the tile's input rows, the weights from LDS as broadcast reads (four channels per
+// ds_read_b128), 3136 FMAs, 64 coalesced stores.  Workgroup: 256 consecutive pixels of one sample.
+constexpr int ST_K = 7, ST_C = 64, ST_ROWS = 12;   // input rows a 256-pixel tile reads (W >= 64)
+__global__ __launch_bounds__(256) void k_stem7(int H, int W, const float *__restrict__ x, const float *__restrict__ w,
+                                               const float *__restrict__ bias, float *__restrict__ y)
+{
+    __shared__ float xs[ST_ROWS][C3_WMAX + ST_K - 1];
+    __shared__ __attribute__((aligned(16))) float ws_[ST_K * ST_K][ST_C];   // [tap][channel]: broadcast reads
+    const int b = blockIdx.y, HW = H * W, p0 = blockIdx.x * 256, p = p0 + (int)threadIdx.x;
+    for (int i = threadIdx.x; i < ST_K * ST_K * ST_C; i += 256) {
+        const int c = i / (ST_K * ST_K), t = i - c * ST_K * ST_K;
+        ws_[t][c] = w[i];
+    }
+    const int r0 = p0 / W - ST_K / 2;                  // first input row of the window set
+    const float *xb = x + (size_t)b * HW;
+    for (int i = threadIdx.x; i < ST_ROWS * (W + ST_K - 1); i += 256) {
+        const int rr = i / (W + ST_K - 1), cc = i - rr * (W + ST_K - 1);
+        const int ih = r0 + rr, iw = cc - ST_K / 2;
+        xs[rr][cc] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xb[ih * W + iw] : 0.0f;
+    }
+    __syncthreads();
+    if (p >= HW) return;
+    const int oh = p / W, ow = p - oh * W, lr = oh - ST_K / 2 - r0;   // local row of the window top
+    float acc[ST_C];
+#pragma unroll
+    for (int c = 0; c < ST_C; ++c) acc[c] = bias ? bias[c] : 0.0f;
+#pragma unroll
+    for (int ky = 0; ky < ST_K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < ST_K; ++kx) {
+            const float v = xs[lr + ky][ow + kx];
+            const f32x4 *wt = reinterpret_cast<const f32x4 *>(&ws_[ky * ST_K + kx][0]);
+#pragma unroll
+            for (int c4 = 0; c4 < ST_C / 4; ++c4) {
+                const f32x4 w4 = wt[c4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[4 * c4 + q] = fmaf(v, w4[q], acc[4 * c4 + q]);
+            }
+        }
+    float *yb = y + (size_t)b * ST_C * HW + p;
+#pragma unroll
+    for (int c = 0; c < ST_C; ++c) yb[(size_t)c * HW] = acc[c];
+}
+
 // ------------------------------------------------- linear attention, bf16, whole block fused
 // LinearAttention.forward(x) + x (reference diffusion.py:182-195 and the residual at 286 / 297) for the
 // batched bf16 U-Net (configs[4]: hundreds of 72 x 72 tiles).  The unfused form writes and re-reads
@@ -3353,6 +3401,17 @@ int rdq_unet_set_option(int32_t option, int32_t value)
     const int old = g_bf16_per_tap;
     g_bf16_per_tap = value != 0;
     return old;
+}
+
+int rdq_conv2d_stem(const rdq_conv_desc *d, const float *x, const float *w, const float *bias, float *y, hipStream_t st)
+{
+    if (!conv_desc_ok(d) || !x || !w || !y || d->cin1 != 1 || d->cin2 != 0 || d->kh != ST_K || d->kw != ST_K ||
+        d->pad != ST_K / 2 || d->cout != ST_C || d->in_mode != RDQ_IN_PLAIN || d->W < 64 || d->W > C3_WMAX ||
+        (int64_t)d->B * ST_C * d->H * d->W >= ((int64_t)1 << 31))
+        return RDQ_E_INVALID;
+    hipLaunchKernelGGL(k_stem7, dim3((d->H * d->W + 255) / 256, d->B), dim3(256), 0, st, d->H, d->W, x, w, bias, y);
+    RDQ_CHECK(hipGetLastError());
+    return 0;
 }
 
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,

@@ -97,6 +97,7 @@ SIGNATURES = {
     "rdq_unet_head": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_float,
                                 c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_wpack_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "rdq_conv2d_stem": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_pack": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_unet_set_option": (c_int32, [c_int32, c_int32]),

@@ -264,6 +264,12 @@ def conv2d_mfma(x: Tensor, x2: Optional[Tensor], weight: Tensor, bias: Optional[
     res = residual.contiguous() if residual is not None else None
     L = _hip.lib()
     st = _hip.stream_of(x)
+    if bf16 and tuple(weight.shape) == (64, 1, 7, 7) and pad == 3 and mode == 0 and x2 is None and residual is None \
+            and 64 <= x.shape[3] <= 72:
+        # the batched bf16 U-Net's stem (an fp32 conv: K = 49 is below the bf16 floor) as a direct conv
+        _hip.check(L.rdq_conv2d_stem(ctypes.byref(d), _hip.ptr(x), _hip.ptr(weight.contiguous()), _hip.ptr(bias),
+                                     _hip.ptr(y), st), "rdq_conv2d_stem")
+        return y
     if bf16 and bf16_eligible(weight):
         wp = _bf16_pack(weight, d, st)
         nws = int(L.rdq_conv2d_bf16_ws_bytes(ctypes.byref(d)))

@@ -483,6 +483,19 @@ def test_bf16_block_pair_bitexact(cuda, cin1, cin2, cout, H, B, ss, post):
     assert torch.equal(got, ref), (got - ref).abs().max().item()
 
 
+@pytest.mark.parametrize("B,H,W", [(3, 72, 72), (2, 64, 64), (1, 40, 70)])
+def test_stem_direct_conv(cuda, B, H, W):
+    """Unet.init_conv (Conv2d(1, 64, 7, padding=3)) under the bf16 precision: the direct fp32 conv
+    (rdq_conv2d_stem: a thread per pixel, all 64 channels) vs the torch fp32 conv."""
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(23)
+    conv = nn.Conv2d(1, 64, 7, padding=3).to(cuda)
+    x = torch.randn(B, 1, H, W, device=cuda)
+    with torch.no_grad(), ops.precision("bf16"):
+        got = ops.conv2d(x, conv)
+    close(got, torch.nn.functional.conv2d(x, conv.weight, conv.bias, padding=3), rel=1e-5)
+
+
 def test_unet_bf16_close_to_fp32(cuda):
     """Whole U-Net (reference architecture, dim 64) with bf16 convolutions vs fp32: new behaviour
     (configs[4]), no reference counterpart; the deviation is bounded, not bitwise."""
