@@ -1429,6 +1429,95 @@ __global__ __launch_bounds__(256) void k_linear_silu_multi_b(int in, int B, cons
     }
 }
 
+// Large batches, in = 256 (the dim-64 U-Net's time embedding): the same per-sample arithmetic as
+// wave_dot -- lane k's partial p[k] = sum over u of w[k + 64u] x[k + 64u] as an FMA chain in u, then the
+// shfl_down tree over k (pairs 32 apart first, then 16, ..., 1) -- evaluated with one SAMPLE per
+// lane instead of one sample per wave: the tree is evaluated depth-first in registers
+// (wdot_tree), so no cross-lane instruction is needed.  Each sample's result is bit for bit
+// k_linear_silu_multi's.  Workgroup: 64 samples (SiLU'd into LDS, rows padded to 257 floats:
+// conflict-free column reads) x 4 waves x WDR rows; the rows' weights in LDS as [row][k][u]
+// (one broadcast read per leaf).
+constexpr int WDR = 8;
+// wave_dot's shfl_down tree as a recursion: F(o, l) = F(2o, l) + F(2o, l + o), F(64, l) = lane l's
+// partial (an FMA chain over u of w[l + 64u] x[l + 64u]); the sample's result is F(1, 0).  Every index
+// is a template constant; one row at a time (independent rows let the scheduler interleave whole
+// trees and spill).
+template <int O, int LX>
+__device__ __forceinline__ float wdot_tree(const float *__restrict__ xrow, const float *__restrict__ wrow, float dep)
+{
+    if constexpr (O == 64) {
+        // the leaf's LDS offset passes through an asm that consumes the previous leaf group's value:
+        // its reads are issued after that group (the scheduler would otherwise lift all 64 leaves')
+        int ox = LX;
+        asm volatile("" : "+v"(ox) : "v"(dep));
+        const f32x4 w4 = *reinterpret_cast<const f32x4 *>(wrow + 4 * ox);    // [k][u]: one broadcast read
+        float sacc = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sacc = fmaf(w4[u], xrow[ox + 64 * u], sacc);
+        return sacc;
+    } else {
+        const float a = wdot_tree<2 * O, LX>(xrow, wrow, dep);
+        // groups of four leaves issue their reads together; each group waits for the previous one
+        const float b = wdot_tree<2 * O, LX + O>(xrow, wrow, O < 16 ? a : dep);
+        return a + b;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wdot_silu_b(int B, const float *__restrict__ x, LinMulti L)
+{
+    __shared__ float xs[64][257];
+    __shared__ __attribute__((aligned(16))) float wt[4][WDR][64][4];   // [wave][row][k][u]
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b0 = blockIdx.y * 64, nb = min(64, B - b0), gend = L.start[L.n];
+    // staging with 16 loads in flight per thread (a load per iteration would be a latency chain)
+    const int g0 = (blockIdx.x * 4 + wv) * WDR;
+    const float *wr[WDR];
+#pragma unroll
+    for (int r = 0; r < WDR; ++r) {
+        const int go = min(g0 + r, gend - 1);
+        int j = 0;
+        while (go >= L.start[j + 1]) ++j;
+        wr[r] = L.w[j] + (size_t)(go - L.start[j]) * 256;
+    }
+    {
+        float wv4[WDR][4];
+#pragma unroll
+        for (int r = 0; r < WDR; ++r)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wv4[r][u] = wr[r][lane + 64 * u];
+#pragma unroll
+        for (int r = 0; r < WDR; ++r)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wt[wv][r][lane][u] = wv4[r][u];
+    }
+#pragma unroll 1
+    for (int it = 0; it < 64; it += 16) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int idx = (it + q) * 256 + tid, bb = idx >> 8;
+            v[q] = x[(size_t)(b0 + min(bb, nb - 1)) * 256 + (idx & 255)];
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int idx = (it + q) * 256 + tid;
+            xs[idx >> 8][idx & 255] = v[q] / (1.0f + expf(-v[q]));
+        }
+    }
+    __syncthreads();
+    const int b = b0 + lane;
+#pragma unroll 1
+    for (int r = 0; r < WDR; ++r) {
+        const int go = g0 + r;
+        if (go >= gend) break;                      // wave-uniform
+        const float res = wdot_tree<1, 0>(xs[lane], &wt[wv][r][0][0], 0.0f);
+        int j = 0;
+        while (go >= L.start[j + 1]) ++j;
+        const int o = go - L.start[j];
+        if (lane < nb) L.y[j][(size_t)b * L.out[j] + o] = res + (L.b[j] ? L.b[j][o] : 0.0f);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_linear_silu_multi(int in, const float *__restrict__ x, LinMulti L)
 {
     const int go = blockIdx.x * 4 + (threadIdx.x >> 6), b = blockIdx.y, lane = threadIdx.x & 63;
@@ -3665,7 +3754,10 @@ int rdq_linear_silu_multi(int32_t B, int32_t in, const float *x, int32_t n, cons
         L.out[j] = out[j];
         L.start[j + 1] = L.start[j] + out[j];
     }
-    if (B > LSB / 2 && in <= 256)
+    if (B >= 64 && in == 256)
+        hipLaunchKernelGGL(k_wdot_silu_b, dim3((L.start[n] + 4 * WDR - 1) / (4 * WDR), (B + 63) / 64), dim3(256), 0, st, B,
+                           x, L);
+    else if (B > LSB / 2 && in <= 256)
         hipLaunchKernelGGL(k_linear_silu_multi_b, dim3((L.start[n] + 4 * LSR - 1) / (4 * LSR), (B + LSB - 1) / LSB),
                            dim3(256), LSB * in * sizeof(float), st, in, B, x, L);
     else

@@ -228,19 +228,20 @@ def test_time_mlp_and_scale_shifts(cuda):
             close(s, b.mlp[1](F.silu(te)))
 
 
-def test_time_mlp_and_scale_shifts_batched(cuda):
-    """The large-batch kernels (B > 16: the configs[4] tile batch) give every sample exactly what the
-    per-sample launch gives it."""
+@pytest.mark.parametrize("B", [45, 130])
+def test_time_mlp_and_scale_shifts_batched(cuda, B):
+    """The large-batch kernels (B > 16: k_time_mlp_b / k_linear_silu_multi_b; B >= 64: the
+    sample-per-lane k_wdot_silu_b) give every sample exactly what the per-sample launch gives it."""
     from red_diffeq.models.diffusion import Unet
     from red_diffeq.models import unet_ops as ops
     torch.manual_seed(8)
     net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
-    t = torch.randint(0, 1000, (45,), device=cuda)
+    t = torch.randint(0, 1000, (B,), device=cuda)
     blocks = net._resnet_blocks()
     with torch.no_grad():
         te = ops.time_mlp(t, net.time_mlp)
         ss = ops.resnet_scale_shifts(te, blocks)
-        for i in (0, 7, 8, 31, 32, 44):
+        for i in sorted(i for i in {0, 7, 8, 31, 32, 44, 63, 64, B - 1} if i < B):
             assert torch.equal(te[i:i + 1], ops.time_mlp(t[i:i + 1], net.time_mlp))
             for a, b in zip(ss, ops.resnet_scale_shifts(te[i:i + 1], blocks)):
                 assert torch.equal(a[i:i + 1], b)
