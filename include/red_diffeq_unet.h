@@ -225,6 +225,14 @@ int rdq_linear_attention_bf16(int32_t B, int32_t dim, int32_t n, int32_t nmem, f
                               const float *g_in, const void *wqkv, const float *mem_kv, const void *wout,
                               const float *b_out, const float *g_out, float *y, void *ws, size_t ws_bytes,
                               hipStream_t stream);
+/* The same two-launch LinearAttention block in fp32 (the reference's arithmetic: v_mfma_f32_32x32x2_f32,
+ * fp32 staging): wqkv / wout are the module's own fp32 weights (384, dim) / (dim, 128); dim 64 / 128;
+ * ws: rdq_linear_attention_f32_ws_bytes. */
+size_t rdq_linear_attention_f32_ws_bytes(int32_t B, int32_t dim, int32_t n);
+int rdq_linear_attention_f32(int32_t B, int32_t dim, int32_t n, int32_t nmem, float scale, const float *x,
+                             const float *g_in, const float *wqkv, const float *mem_kv, const float *wout,
+                             const float *b_out, const float *g_out, float *y, void *ws, size_t ws_bytes,
+                             hipStream_t stream);
 
 /* Attention core with Attend(flash=False) (diffusion.py:209-217): softmax(q k^T dh^-1/2) v over
  * nmem memory keys + n pixels; mem_kv (2, heads, nmem, dh); out (B, heads*dh, n).  dh = 32; K/V of one

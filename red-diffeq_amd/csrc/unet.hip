@@ -2707,6 +2707,7 @@ struct LabArgs {
     const float *x, *g_in, *mem, *b_out, *g_out;
     const __bf16 *wqkv;              // [3 * 128][D]  (q, k, v rows)
     const __bf16 *wout;              // [D][128]
+    const float *wqkv32, *wout32;    // the fp32 form (F): the module's own weights, same layouts
     float *part, *y;
     int n, nch, nsub, nmem;
     float scale;
@@ -2736,9 +2737,15 @@ __device__ __forceinline__ void lb_load(const LabArgs &a, int b, int p0, float (
                                                     rx, voff, (8 * (w + 4 * j) + i) * a.n * 4, 0));
 }
 
-template <int D>
-__device__ __forceinline__ void lb_store(const LabArgs &a, const float (&v)[D / 32][8], __bf16 (*Xs)[D + 8],
-                                         float (*red)[LB_PX])
+// staged operand rows: bf16 [px][D + 8] (16-byte fragment reads), or fp32 [px][D + 1] (F: one float
+// per lane and k-step, odd pitch: conflict-free)
+template <int D, bool F> struct LbX {
+    using T = typename std::conditional<F, float, __bf16>::type;
+    static constexpr int P = F ? D + 1 : D + 8;
+};
+template <int D, bool F>
+__device__ __forceinline__ void lb_store(const LabArgs &a, const float (&v)[D / 32][8],
+                                         typename LbX<D, F>::T (*Xs)[LbX<D, F>::P], float (*red)[LB_PX])
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float ss = 0.0f;
@@ -2753,29 +2760,40 @@ __device__ __forceinline__ void lb_store(const LabArgs &a, const float (&v)[D / 
 #pragma unroll
     for (int j = 0; j < D / 32; ++j) {
         const int c0 = 8 * (w + 4 * j);
-        bf16x8 o;
+        if constexpr (F) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (__bf16)(v[j][i] * k * a.g_in[c0 + i]);
-        *reinterpret_cast<bf16x8 *>(&Xs[lane][c0]) = o;
+            for (int i = 0; i < 8; ++i) Xs[lane][c0 + i] = v[j][i] * k * a.g_in[c0 + i];
+        } else {
+            bf16x8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (__bf16)(v[j][i] * k * a.g_in[c0 + i]);
+            *reinterpret_cast<bf16x8 *>(&Xs[lane][c0]) = o;
+        }
     }
 }
 
 // Occupancy sets the rate of these streaming kernels (each workgroup has one tile's loads in flight
 // during the previous tile's MFMAs): register budgets of 3 (dim 64) / 2 (dim 128) workgroups per CU.
-template <int D> struct LbOcc { static constexpr int N = D == 64 ? 3 : 2; };
+template <int D, bool F = false> struct LbOcc {      // (F: fp32 staging, LDS-bound)
+    static constexpr int N = F ? (D == 64 ? 2 : 1) : (D == 64 ? 3 : 2);
+};
 
-template <int D>
-__global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
+// F: the fp32 form (the reference's arithmetic, small batches): the same structure on
+// v_mfma_f32_32x32x2_f32 (k index of lane group g = g: one float per lane and k-step), fp32 staging
+template <int D, bool F = false>
+__global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_kv(LabArgs a)
 {
     constexpr int KS = D / 16;                       // k-steps over the input channels
-    constexpr bool WREG = D <= 64;                   // W_kv fragments held in registers (else L1 / L2)
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[LB_PX][D + 8];
+    constexpr bool WREG = D <= 64 && !F;             // W_kv fragments held in registers (else L1 / L2)
+    __shared__ __attribute__((aligned(16))) typename LbX<D, F>::T Xs[LB_PX][LbX<D, F>::P];
     __shared__ float red[4][LB_PX];
     const int ch = blockIdx.x, b = blockIdx.y;
     const int lane = threadIdx.x & 63, h = threadIdx.x >> 6, g = lane >> 5, cl = lane & 31;
     // B fragments: column = channel cl of head h (k rows 128 + 32 h, v rows 256 + 32 h), k = c
     const __bf16 *wk = a.wqkv + (size_t)(LB_HID + h * LB_DH + cl) * D + 8 * g;
     const __bf16 *wv = a.wqkv + (size_t)(2 * LB_HID + h * LB_DH + cl) * D + 8 * g;
+    const float *wk32 = a.wqkv32 + (size_t)(LB_HID + h * LB_DH + cl) * D + g;
+    const float *wv32 = a.wqkv32 + (size_t)(2 * LB_HID + h * LB_DH + cl) * D + g;
     bf16x8 fk[WREG ? KS : 1], fv[WREG ? KS : 1];
     if constexpr (WREG) {
 #pragma unroll
@@ -2791,7 +2809,7 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
     if (sub0 < sub1) lb_load<D>(a, b, sub0 * LB_PX, xv);
     for (int sb = sub0; sb < sub1; ++sb) {
         const int p0 = sb * LB_PX;
-        lb_store<D>(a, xv, Xs, red);
+        lb_store<D, F>(a, xv, Xs, red);
         __syncthreads();
         if (sb + 1 < sub1) lb_load<D>(a, b, p0 + LB_PX, xv);
         // one 32-pixel block at a time: k^T and v^T (rows = pixels, column = channel cl), the online
@@ -2799,13 +2817,22 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
 #pragma unroll 1
         for (int pb = 0; pb < 2; ++pb) {
             f32x16 kt = {}, vt = {};
+            if constexpr (F) {
+#pragma unroll 8
+                for (int s = 0; s < D / 2; ++s) {
+                    const float av = Xs[pb * 32 + cl][2 * s + g];
+                    kt = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wk32[2 * s], kt, 0, 0, 0);
+                    vt = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wv32[2 * s], vt, 0, 0, 0);
+                }
+            } else {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const bf16x8 bk = WREG ? fk[s] : *reinterpret_cast<const bf16x8 *>(wk + 16 * s);
-                const bf16x8 bv = WREG ? fv[s] : *reinterpret_cast<const bf16x8 *>(wv + 16 * s);
-                const bf16x8 av = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
-                kt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bk, kt, 0, 0, 0);
-                vt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, vt, 0, 0, 0);
+                for (int s = 0; s < KS; ++s) {
+                    const bf16x8 bk = WREG ? fk[s] : *reinterpret_cast<const bf16x8 *>(wk + 16 * s);
+                    const bf16x8 bv = WREG ? fv[s] : *reinterpret_cast<const bf16x8 *>(wv + 16 * s);
+                    const bf16x8 av = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
+                    kt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bk, kt, 0, 0, 0);
+                    vt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, vt, 0, 0, 0);
+                }
             }
             float tmax = -INFINITY;
 #pragma unroll
@@ -2829,15 +2856,21 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
 #pragma unroll
             for (int r = 0; r < 16; ++r) ctx[r] *= f;
             // ctx^T[e][d] += sum_n v[e][n] p[d][n]: k index j of lane group g <-> pixel lb_row(8 s + j, g)
+            // (F: k index g of step r <-> pixel lb_row(r, g))
+            if constexpr (F) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                bf16x8 av, bp;
+                for (int r = 0; r < 16; ++r) ctx = __builtin_amdgcn_mfma_f32_32x32x2f32(vt[r], kt[r], ctx, 0, 0, 0);
+            } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    av[j] = (__bf16)vt[8 * s + j];
-                    bp[j] = (__bf16)kt[8 * s + j];
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 av, bp;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        av[j] = (__bf16)vt[8 * s + j];
+                        bp[j] = (__bf16)kt[8 * s + j];
+                    }
+                    ctx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bp, ctx, 0, 0, 0);
                 }
-                ctx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bp, ctx, 0, 0, 0);
             }
         }
     }
@@ -2851,13 +2884,13 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_kv(LabArgs a)
     for (int r = 0; r < 16; ++r) o[2 * LB_DH + lb_row(r, g) * LB_DH + cl] = ctx[r];
 }
 
-template <int D>
-__global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
+template <int D, bool F = false>
+__global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
 {
     constexpr int KS = D / 16, NOB = D / 64;         // o blocks per wave (two waves per pixel block)
-    constexpr bool WREG = D <= 64, WOREG = false;    // W_q / W_out fragments in registers (else L1 / L2)
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[LB_PX][D + 8];
-    __shared__ __attribute__((aligned(16))) __bf16 Hs[LB_PX][LB_HID + 8];
+    constexpr bool WREG = D <= 64 && !F, WOREG = false;   // W_q / W_out fragments in registers (else L1 / L2)
+    __shared__ __attribute__((aligned(16))) typename LbX<D, F>::T Xs[LB_PX][LbX<D, F>::P];
+    __shared__ __attribute__((aligned(16))) typename LbX<LB_HID, F>::T Hs[LB_PX][LbX<LB_HID, F>::P];
     __shared__ float red[4][LB_PX];
     __shared__ float red2[4][32];
     __shared__ float Cs[LB_HEADS][LB_DH][LB_DH + 1];
@@ -2896,13 +2929,20 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
     }
     __syncthreads();
     // A fragments of hidden = ctx^T q: row e = cl, k index j of group g <-> d = lb_row(8 s + j, g)
-    bf16x8 fc[2];
+    bf16x8 fc[F ? 1 : 2];
+    float fcf[F ? 16 : 1];                           // F: step r's k index g <-> d = lb_row(r, g)
+    if constexpr (F) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+        for (int r = 0; r < 16; ++r) fcf[r] = Cs[h][lb_row(r, g)][cl];
+    } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fc[s][j] = (__bf16)Cs[h][lb_row(8 * s + j, g)][cl];
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) fc[s][j] = (__bf16)Cs[h][lb_row(8 * s + j, g)][cl];
+    }
     // q rows of head h (A operand, row d = cl) and the wave's W_out rows (A operand, row o)
     const __bf16 *wq = a.wqkv + (size_t)(h * LB_DH + cl) * D + 8 * g;
+    const float *wq32 = a.wqkv32 + (size_t)(h * LB_DH + cl) * D + g;
     bf16x8 fq[WREG ? KS : 1];
     if constexpr (WREG) {
 #pragma unroll
@@ -2911,6 +2951,7 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
     const int pbw = __builtin_amdgcn_readfirstlane(w & 1), obw = __builtin_amdgcn_readfirstlane(w >> 1);   // y tiles:
                                                      // pixel block pbw, o blocks obw + 2 j
     const __bf16 *wo = a.wout + (size_t)(obw * 32 + cl) * LB_HID + 8 * g;
+    const float *wo32 = a.wout32 + (size_t)(obw * 32 + cl) * LB_HID + g;
     bf16x8 fo[WOREG ? NOB : 1][8];
     if constexpr (WOREG) {
 #pragma unroll
@@ -2924,18 +2965,24 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
     if (sub0 < sub1) lb_load<D>(a, b, sub0 * LB_PX, xv);
     for (int sb = sub0; sb < sub1; ++sb) {
         const int p0 = sb * LB_PX;
-        lb_store<D>(a, xv, Xs, red);                 // (its barrier: Hs / red2 of the previous tile consumed)
+        lb_store<D, F>(a, xv, Xs, red);              // (its barrier: Hs / red2 of the previous tile consumed)
         __syncthreads();
         if (sb + 1 < sub1) lb_load<D>(a, b, p0 + LB_PX, xv);
         // q[d][px] of head h, softmax over d (this lane's 16 d and lane ^ 32's), then hidden
 #pragma unroll
         for (int pb = 0; pb < 2; ++pb) {
             f32x16 q = {};
+            if constexpr (F) {
+#pragma unroll 8
+                for (int s = 0; s < D / 2; ++s)
+                    q = __builtin_amdgcn_mfma_f32_32x32x2f32(wq32[2 * s], Xs[pb * 32 + cl][2 * s + g], q, 0, 0, 0);
+            } else {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const bf16x8 aw = WREG ? fq[s] : *reinterpret_cast<const bf16x8 *>(wq + 16 * s);
-                const bf16x8 bx = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
-                q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bx, q, 0, 0, 0);
+                for (int s = 0; s < KS; ++s) {
+                    const bf16x8 aw = WREG ? fq[s] : *reinterpret_cast<const bf16x8 *>(wq + 16 * s);
+                    const bf16x8 bx = *reinterpret_cast<const bf16x8 *>(&Xs[pb * 32 + cl][16 * s + 8 * g]);
+                    q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bx, q, 0, 0, 0);
+                }
             }
             float mx = -INFINITY;
 #pragma unroll
@@ -2947,20 +2994,27 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
             sm += __shfl_xor(sm, 32);
             const float inv = 1.0f / sm;
             f32x16 hid = {};
+            if constexpr (F) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                bf16x8 bq;
+                for (int r = 0; r < 16; ++r) hid = __builtin_amdgcn_mfma_f32_32x32x2f32(fcf[r], q[r] * inv, hid, 0, 0, 0);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) bq[j] = (__bf16)(q[8 * s + j] * inv);
-                hid = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fc[s], bq, hid, 0, 0, 0);
-            }
-            // hidden[e][px] -> Hs[px][32 h + e]: rows 4 q4 .. 4 q4 + 3 are four consecutive e
+                for (int r = 0; r < 16; ++r) Hs[pb * 32 + cl][h * LB_DH + lb_row(r, g)] = hid[r];
+            } else {
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-                __attribute__((ext_vector_type(4))) __bf16 o4;
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 bq;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) o4[i] = (__bf16)hid[4 * q4 + i];
-                *reinterpret_cast<decltype(o4) *>(&Hs[pb * 32 + cl][h * LB_DH + lb_row(4 * q4, g)]) = o4;
+                    for (int j = 0; j < 8; ++j) bq[j] = (__bf16)(q[8 * s + j] * inv);
+                    hid = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fc[s], bq, hid, 0, 0, 0);
+                }
+                // hidden[e][px] -> Hs[px][32 h + e]: rows 4 q4 .. 4 q4 + 3 are four consecutive e
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    __attribute__((ext_vector_type(4))) __bf16 o4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o4[i] = (__bf16)hid[4 * q4 + i];
+                    *reinterpret_cast<decltype(o4) *>(&Hs[pb * 32 + cl][h * LB_DH + lb_row(4 * q4, g)]) = o4;
+                }
             }
         }
         __syncthreads();
@@ -2986,12 +3040,19 @@ __global__ __launch_bounds__(256, LbOcc<D>::N) void k_lab_out(LabArgs a)
 #pragma unroll
         for (int j = 0; j < NOB; ++j) {
             y[j] = f32x16{};
+            if constexpr (F) {
+#pragma unroll 8
+                for (int s = 0; s < LB_HID / 2; ++s)
+                    y[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wo32[(size_t)j * 64 * LB_HID + 2 * s],
+                                                                Hs[pbw * 32 + cl][2 * s + g], y[j], 0, 0, 0);
+            } else {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const bf16x8 aw = WOREG ? fo[j][s]
-                                        : *reinterpret_cast<const bf16x8 *>(wo + (size_t)j * 64 * LB_HID + 16 * s);
-                const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(&Hs[pbw * 32 + cl][16 * s + 8 * g]);
-                y[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bh, y[j], 0, 0, 0);
+                for (int s = 0; s < 8; ++s) {
+                    const bf16x8 aw = WOREG ? fo[j][s]
+                                            : *reinterpret_cast<const bf16x8 *>(wo + (size_t)j * 64 * LB_HID + 16 * s);
+                    const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(&Hs[pbw * 32 + cl][16 * s + 8 * g]);
+                    y[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bh, y[j], 0, 0, 0);
+                }
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -3862,6 +3923,52 @@ int rdq_linear_attention_bf16(int32_t B, int32_t dim, int32_t n, int32_t nmem, f
     } else {
         hipLaunchKernelGGL(k_lab_kv<128>, grid, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_lab_out<128>, grid, dim3(256), 0, st, a);
+    }
+    RDQ_CHECK(hipGetLastError());
+    return 0;
+}
+
+// the fp32 form: WGs for about 1024 subtiles (small batches: the combine reads every chunk's partials)
+static void lab_split32(int B, int n, int *nsub, int *nch)
+{
+    const int tiles = (n + LB_PX - 1) / LB_PX;
+    int s_ = (int)std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)tiles * B + 1023) / 1024));
+    s_ = std::min(s_, tiles);
+    *nsub = s_;
+    *nch = (tiles + s_ - 1) / s_;
+}
+
+size_t rdq_linear_attention_f32_ws_bytes(int32_t B, int32_t dim, int32_t n)
+{
+    if (B < 1 || n < 1 || (dim != 64 && dim != 128)) return 0;
+    int nsub, nch;
+    lab_split32(B, n, &nsub, &nch);
+    return (size_t)B * nch * LB_PART * sizeof(float);
+}
+
+int rdq_linear_attention_f32(int32_t B, int32_t dim, int32_t n, int32_t nmem, float scale, const float *x,
+                             const float *g_in, const float *wqkv, const float *mem_kv, const float *wout,
+                             const float *b_out, const float *g_out, float *y, void *ws, size_t ws_bytes,
+                             hipStream_t st)
+{
+    if (B < 1 || n < 1 || nmem < 0 || (dim != 64 && dim != 128) || !x || !g_in || !wqkv ||
+        (nmem > 0 && !mem_kv) || !wout || !g_out || !y || !ws || y == x)
+        return RDQ_E_INVALID;
+    if ((int64_t)B * dim * n >= ((int64_t)1 << 31) || ws_bytes < rdq_linear_attention_f32_ws_bytes(B, dim, n))
+        return RDQ_E_INVALID;
+    LabArgs a{};
+    a.x = x; a.g_in = g_in; a.mem = mem_kv; a.b_out = b_out; a.g_out = g_out;
+    a.wqkv32 = wqkv; a.wout32 = wout;
+    a.part = static_cast<float *>(ws); a.y = y;
+    a.n = n; a.nmem = nmem; a.scale = scale;
+    lab_split32(B, n, &a.nsub, &a.nch);
+    const dim3 grid(a.nch, B);
+    if (dim == 64) {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_lab_kv<64, true>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_lab_out<64, true>), grid, dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_lab_kv<128, true>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_lab_out<128, true>), grid, dim3(256), 0, st, a);
     }
     RDQ_CHECK(hipGetLastError());
     return 0;

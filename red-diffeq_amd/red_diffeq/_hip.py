@@ -134,6 +134,10 @@ SIGNATURES = {
                                              c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                              c_void_p, c_void_p]),
     "rdq_linear_attention_bf16_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_linear_attention_f32_ws_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "rdq_linear_attention_f32": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p]),
     "rdq_linear_attention_bf16": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),

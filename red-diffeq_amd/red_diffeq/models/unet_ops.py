@@ -200,6 +200,14 @@ def rms_conv(x, norm, conv):
     return conv2d(rmsnorm(x, norm.g), conv)
 
 
+# fp32 LinearAttention in the two-launch form (rdq_linear_attention_f32) where it applies; default off:
+# measured slower where the fp32 path runs (B = 1: the U-Net 1.20 -> 1.65 ms, the chunk combine and one
+# L1 weight load per fp32 MFMA step dominate; B = 25: 7.82 -> 7.64 ms, 72 x 72 blocks 230 -> 277 us,
+# 36 / 18 faster).  The three-launch form (rms_conv + context + output projection) stays the default;
+# tests compare the two.
+FUSED_LA_F32 = False
+
+
 def linear_attention(x, m):
     """LinearAttention.forward(x) + x (diffusion.py:182-195 and the residual at 286/297)."""
     conv = m.to_out[0]
@@ -207,6 +215,11 @@ def linear_attention(x, m):
         # the whole block in two launches, qkv and the hidden tensor never written (rdq_linear_attention_bf16)
         return torch.ops.red_diffeq.linear_attn_bf16(x, m.norm.g, m.to_qkv.weight, m.mem_kv, conv.weight, conv.bias,
                                                      m.to_out[1].g, m.heads, float(m.scale))
+    if _PREC["mode"] == "fp32" and FUSED_LA_F32 and ops.linear_attn_bf16_fusable(x, m.to_qkv.weight, conv.weight,
+                                                                                 m.heads):
+        # the same two-launch block on fp32 MFMA (rdq_linear_attention_f32)
+        return torch.ops.red_diffeq.linear_attn_f32(x, m.norm.g, m.to_qkv.weight, m.mem_kv, conv.weight, conv.bias,
+                                                    m.to_out[1].g, m.heads, float(m.scale))
     qkv = rms_conv(x, m.norm, m.to_qkv)
     if _PREC["mode"] == "fp32" and ops.linear_attn_block_fusable(qkv.shape[1], m.heads, conv.weight.shape[0]):
         # context -> (combine, softmax(q) x context, to_out conv, RMSNorm, + x) in one launch (fp32 only: at

@@ -864,6 +864,33 @@ def _(x, g_in, w_qkv, mem_kv, w_out, b_out, g_out, heads, scale):
     return torch.empty_like(x)
 
 
+@torch.library.custom_op(f"{LIB}::linear_attn_f32", mutates_args=())
+def linear_attn_f32(x: Tensor, g_in: Tensor, w_qkv: Tensor, mem_kv: Tensor, w_out: Tensor, b_out: Optional[Tensor],
+                    g_out: Tensor, heads: int, scale: float) -> Tensor:
+    """LinearAttention.forward(x) + x (diffusion.py:182-195, residual 286/297) in fp32, two launches
+    (rdq_linear_attention_f32: qkv and the hidden tensor never written)."""
+    _hip.require_device(x)
+    if not linear_attn_bf16_fusable(x, w_qkv, w_out, heads):
+        raise ValueError("linear_attn_f32: shape not supported (see linear_attn_bf16_fusable)")
+    x = x.contiguous()
+    B, D, H, W = x.shape
+    L = _hip.lib()
+    nws = int(L.rdq_linear_attention_f32_ws_bytes(B, D, H * W))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _hip.check(L.rdq_linear_attention_f32(B, D, H * W, mem_kv.shape[-1], float(scale), _hip.ptr(x),
+                                          _hip.ptr(g_in.contiguous()), _hip.ptr(w_qkv.contiguous()),
+                                          _hip.ptr(mem_kv.contiguous()), _hip.ptr(w_out.contiguous()),
+                                          _hip.ptr(b_out) if b_out is not None else None, _hip.ptr(g_out.contiguous()),
+                                          _hip.ptr(y), _hip.ptr(ws), nws, _hip.stream_of(x)), "rdq_linear_attention_f32")
+    return y
+
+
+@linear_attn_f32.register_fake
+def _(x, g_in, w_qkv, mem_kv, w_out, b_out, g_out, heads, scale):
+    return torch.empty_like(x)
+
+
 @torch.library.custom_op(f"{LIB}::attn", mutates_args=())
 def attn(qkv: Tensor, mem_kv: Tensor, heads: int) -> Tensor:
     """Attention core with Attend(flash=False) (diffusion.py:209-218): softmax(q k^T d^-1/2) v over
@@ -1083,6 +1110,6 @@ for _op, _name in ((conv2d_mfma, "conv2d_mfma"), (conv2d_rms, "conv2d_rms"), (co
                    (gn_silu, "gn_silu"),
                    (rmsnorm, "rmsnorm"), (linear, "linear"), (time_mlp, "time_mlp"),
                    (linear_silu_multi, "linear_silu_multi"),
-                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (linear_attn_block, "linear_attn_block"), (linear_attn_bf16, "linear_attn_bf16"), (attn, "attn"),
+                   (sinusoidal_emb, "sinusoidal_emb"), (linear_attn, "linear_attn"), (linear_attn_block, "linear_attn_block"), (linear_attn_bf16, "linear_attn_bf16"), (linear_attn_f32, "linear_attn_f32"), (attn, "attn"),
                    (red_q_sample, "red_q_sample"), (red_eps, "red_eps"), (metrics, "metrics")):
     _forward_only(_op, _name)

@@ -296,6 +296,31 @@ def test_linear_attention_bf16_fused(cuda, C, H, B):
     close(got, ref, rel=3e-2, what="fused bf16 vs fp64")
 
 
+@pytest.mark.parametrize("C,H,B", [(64, 72, 1), (64, 72, 25), (128, 36, 3), (64, 10, 2)])
+def test_linear_attention_f32_fused_vs_unfused(cuda, C, H, B):
+    """The fp32 two-launch LinearAttention (rdq_linear_attention_f32) vs the three-launch fp32 path and
+    vs the torch restatement: fp32 tolerance (1e-5 of the output range; the summation orders differ)."""
+    from red_diffeq.models.diffusion import LinearAttention
+    from red_diffeq.models import unet_ops as ops
+    torch.manual_seed(60 + C + H + B)
+    m = LinearAttention(C).to(cuda)
+    with torch.no_grad():
+        m.norm.g.mul_(1 + 0.2 * torch.randn_like(m.norm.g))
+        m.to_out[1].g.mul_(1 + 0.2 * torch.randn_like(m.to_out[1].g))
+        m.to_out[0].bias.normal_(0, 0.1)
+    x = torch.randn(B, C, H, H, device=cuda)
+    with torch.no_grad():
+        unf = ops.linear_attention(x, m)
+        old, ops.FUSED_LA_F32 = ops.FUSED_LA_F32, True
+        try:
+            got = ops.linear_attention(x, m)
+        finally:
+            ops.FUSED_LA_F32 = old
+        ref = R.linear_attention(x, m) + x
+    close(got, ref, rel=1e-5, what="fused fp32 vs torch")
+    close(got, unf, rel=1e-5, what="fused vs three-launch fp32")
+
+
 # 9 x 9 (the U-Net's level), 8 x 8 and 16 x 16, B = 1 and 2
 @pytest.mark.parametrize("C,H,B", [(256, 9, 2), (512, 9, 1), (256, 8, 1), (128, 16, 1)])
 def test_full_attention(cuda, C, H, B):
