@@ -3815,7 +3815,7 @@ int rdq_linear_silu_multi(int32_t B, int32_t in, const float *x, int32_t n, cons
         L.out[j] = out[j];
         L.start[j + 1] = L.start[j] + out[j];
     }
-    if (B >= 64 && in == 256)
+    if (B > LSB / 2 && in == 256)
         hipLaunchKernelGGL(k_wdot_silu_b, dim3((L.start[n] + 4 * WDR - 1) / (4 * WDR), (B + 63) / 64), dim3(256), 0, st, B,
                            x, L);
     else if (B > LSB / 2 && in <= 256)

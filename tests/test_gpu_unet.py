@@ -230,8 +230,9 @@ def test_time_mlp_and_scale_shifts(cuda):
 
 @pytest.mark.parametrize("B", [45, 130])
 def test_time_mlp_and_scale_shifts_batched(cuda, B):
-    """The large-batch kernels (B > 16: k_time_mlp_b / k_linear_silu_multi_b; B >= 64: the
-    sample-per-lane k_wdot_silu_b) give every sample exactly what the per-sample launch gives it."""
+    """The large-batch kernels (B > 16: k_time_mlp_b and the sample-per-lane k_wdot_silu_b, whose
+    workgroups take 64 samples: a partial last group at both sizes) give every sample exactly what the
+    per-sample launch gives it."""
     from red_diffeq.models.diffusion import Unet
     from red_diffeq.models import unet_ops as ops
     torch.manual_seed(8)
