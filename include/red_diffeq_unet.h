@@ -130,6 +130,7 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
  *   halo-staged 3x3 kernel (the two share the operand rounding; tests/test_gpu_unet.py compares them).
  * Returns the previous value, or RDQ_E_INVALID for an unknown option. */
 #define RDQ_UNET_OPT_BF16_PER_TAP 1
+#define RDQ_UNET_OPT_CONV3_MIN_TILES 2   /* least (256-pixel x 64-channel) tiles for the halo-staged 3x3 conv (default 64) */
 int rdq_unet_set_option(int32_t option, int32_t value);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);

@@ -3078,7 +3078,10 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
 }
 
 // the halo-staged kernel takes 3x3 / pad 1 convs (plain, with a concatenated skip, or on a nearest-
-// upsampled input) whose tile grid fills the chip; everything else stays on the per-tap kernel
+// upsampled input) with at least C3_MIN_TILES tiles; everything else stays on the per-tap kernel. The
+// halo kernel wins even on a part-filled chip (bf16 U-Net forward, B = 25: 4.15 -> 3.13 ms, B = 100:
+// 8.0 -> 6.2 ms, B = 344: 18.5 -> 18.1 ms going from 512 to 64); below ~64 tiles it loses at B <= 8
+static int C3_MIN_TILES = 64;    // rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES); tools/conv3_threshold_ab.py
 bool conv3_ok(const rdq_conv_desc *d)
 {
     if (d->kh != 3 || d->kw != 3 || d->pad != 1) return false;
@@ -3089,7 +3092,7 @@ bool conv3_ok(const rdq_conv_desc *d)
     // the halo gather addresses each input tensor with 32-bit element offsets
     const int64_t plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? HW / 4 : HW;
     if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane >= (int64_t)1 << 32) return false;
-    return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN) >= 512;
+    return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN) >= C3_MIN_TILES;
 }
 
 int bf_cinp(const rdq_conv_desc *d) { return (d->cin1 + d->cin2 + BF_BK - 1) / BF_BK * BF_BK; }
@@ -3547,6 +3550,12 @@ static int g_bf16_per_tap = 0;   // RDQ_UNET_OPT_BF16_PER_TAP
 
 int rdq_unet_set_option(int32_t option, int32_t value)
 {
+    if (option == RDQ_UNET_OPT_CONV3_MIN_TILES) {
+        if (value < 1) return RDQ_E_INVALID;
+        const int old = C3_MIN_TILES;
+        C3_MIN_TILES = value;
+        return old;
+    }
     if (option != RDQ_UNET_OPT_BF16_PER_TAP) return RDQ_E_INVALID;
     const int old = g_bf16_per_tap;
     g_bf16_per_tap = value != 0;

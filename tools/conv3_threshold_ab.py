@@ -1,0 +1,62 @@
+"""A/B of the halo-staged 3x3 conv's least tile count (rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES)):
+times the bf16 U-Net forward (dim 64, mults 1,2,4,8, 72x72) for each threshold and reports the output
+difference against the first threshold listed.
+python tools/conv3_threshold_ab.py [--B 344] [--min-tiles 512 384 256 128] [--reps 10]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
+from red_diffeq import _hip  # noqa: E402
+from red_diffeq.models.diffusion import Unet  # noqa: E402
+
+OPT_CONV3_MIN_TILES = 2
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, nargs="+", default=[344])
+    ap.add_argument("--min-tiles", type=int, nargs="+", default=[512, 384, 256, 128])
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(dev).eval()
+    net.set_precision("bf16")
+    lib = _hip.lib()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for B in a.B:
+        x = torch.randn(B, 1, 72, 72, device=dev).clamp(-1, 1)
+        t = torch.randint(0, 1000, (B,), device=dev)
+        base = None
+        for mt in a.min_tiles:
+            net.__dict__.pop("_graphs", None)          # small batches replay a captured graph: recapture
+            old = lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, mt)
+            assert old > 0
+            try:
+                with torch.no_grad():
+                    for _ in range(2):
+                        y = net(x, t)
+                    torch.cuda.synchronize()
+                    ts = []
+                    for _ in range(a.reps):
+                        ev[0].record()
+                        y = net(x, t)
+                        ev[1].record()
+                        torch.cuda.synchronize()
+                        ts.append(ev[0].elapsed_time(ev[1]))
+            finally:
+                lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, old)
+            if base is None:
+                base = y.clone()
+            d = ((y - base).abs().max() / base.abs().max()).item()
+            print(json.dumps({"B": B, "min_tiles": mt, "ms_median": round(sorted(ts)[len(ts) // 2], 3),
+                              "ms_min": round(min(ts), 3), "rel_diff_vs_first": d}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
