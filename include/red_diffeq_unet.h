@@ -131,14 +131,16 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
  * Returns the previous value, or RDQ_E_INVALID for an unknown option. */
 #define RDQ_UNET_OPT_BF16_PER_TAP 1
 #define RDQ_UNET_OPT_CONV3_MIN_TILES 2   /* least (256-pixel x 64-channel) tiles for the halo-staged 3x3 conv (default 64) */
+#define RDQ_UNET_OPT_BF16_RAW 3   /* rdq_conv2d_bf16_gn_*: hold the raw conv output as bf16 (default 1) */
 int rdq_unet_set_option(int32_t option, int32_t value);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 
 /* Block.forward in two launches on the bf16 halo-staged conv (the batched, mixed-precision U-Net of
- * configs[4]): y = SiLU(GroupNorm_G(conv3x3_bf16(input) + bias) * (scale+1) + shift) [+ post_residual],
- * the GroupNorm statistics reduced in the conv's epilogue (fp64, fixed trees) instead of a separate
- * statistics pass over the conv output.  rdq_conv2d_bf16_gn_ws_bytes returns 0 where this form does not
+ * configs[4]): y = SiLU(GroupNorm_G(h) * (scale+1) + shift) [+ post_residual], h = bf16(conv3x3_bf16(input)
+ * + bias): the raw conv output is held as bf16 between the two launches (half the bytes written and
+ * re-read), and the GroupNorm statistics of h are reduced in the conv's epilogue (fp64, fixed trees)
+ * instead of a separate statistics pass.  rdq_conv2d_bf16_gn_ws_bytes returns 0 where this form does not
  * apply (not the halo-staged conv: see rdq_conv2d_bf16; H*W < 256; C/G outside {8,16,32,64}).
  * wp: rdq_conv2d_bf16_pack's weights; ws: the conv output + the partial statistics. */
 size_t rdq_conv2d_bf16_gn_ws_bytes(const rdq_conv_desc *d, int32_t G);

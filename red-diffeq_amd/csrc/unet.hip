@@ -229,6 +229,17 @@ __device__ __forceinline__ float gn_silu1(float x, float mean, float rstd, float
     return v / (1.0f + expf(-v));
 }
 
+// element loads of a normalise pass's input: fp32, or the bf16 halo-staged conv's raw output
+__device__ __forceinline__ float ldx(const float *p) { return *p; }
+__device__ __forceinline__ float ldx(const __bf16 *p) { return (float)*p; }
+__device__ __forceinline__ float4 ldx4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 ldx4(const __bf16 *p)
+{
+    const uint2 u = *reinterpret_cast<const uint2 *>(p);
+    return float4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                  __uint_as_float(u.y & 0xffff0000u)};
+}
+
 template <int TAPS> struct CcCfg;
 template <> struct CcCfg<9> { static constexpr int CPS = 8, BK = 72, NA = 9, QPR = 18, NWQ = 5; };
 template <> struct CcCfg<1> { static constexpr int CPS = 64, BK = 64, NA = 8, QPR = 16, NWQ = 4; };
@@ -822,8 +833,8 @@ __global__ __launch_bounds__(256) void k_gn_apply(int C, int HW, int G, int nch,
 // sample in order, then a fixed xor tree — and the pass adds an optional residual after the SiLU
 // (ResnetBlock's identity shortcut, diffusion.py:168).  V float4 per thread (large batches: V = 4, so
 // the per-workgroup statistics reduction is paid once per 4096 elements instead of 1024)
-template <bool SMALL, int V = 1>
-__global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const float *__restrict__ x,
+template <bool SMALL, int V = 1, typename TX = float>
+__global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nch, const TX *__restrict__ x,
                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
                                                     const float *__restrict__ ss, const double *__restrict__ gnp,
                                                     float eps, const float *__restrict__ post, float *__restrict__ y,
@@ -842,7 +853,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
         const int i4 = ((ch * V + k) * 256 + (int)threadIdx.x) * 4;
         v[k] = r[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
         if (!SMALL && vec && i4 < HW) {
-            v[k] = *reinterpret_cast<const float4 *>(x + base + i4);
+            v[k] = ldx4(x + base + i4);
             if (post) r[k] = *reinterpret_cast<const float4 *>(post + base + i4);
         }
     }
@@ -881,7 +892,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
         for (int e = threadIdx.x; e < n; e += 256) {
             const int cc = g * cpg + cl0 + e / HW;
             const float s1 = sso ? ss[(size_t)b * 2 * C + cc] + 1.0f : 0.0f, sh1 = sso ? ss[(size_t)b * 2 * C + C + cc] : 0.0f;
-            float u = gn_silu1(x[base0 + e], mean, rstd, gamma[cc], beta[cc], sso, s1, sh1);
+            float u = gn_silu1(ldx(x + base0 + e), mean, rstd, gamma[cc], beta[cc], sso, s1, sh1);
             if (post) u += post[base0 + e];
             y[base0 + e] = u;
         }
@@ -904,7 +915,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
     } else {
         const int e1 = min(HW, (ch + 1) * 1024 * V);
         for (int i = ch * 1024 * V + (int)threadIdx.x; i < e1; i += 256) {
-            float u = gn_silu1(x[base + i], mean, rstd, ga, be, sso, sc1, sh);
+            float u = gn_silu1(ldx(x + base + i), mean, rstd, ga, be, sso, sc1, sh);
             if (post) u += post[base + i];
             y[base + i] = u;
         }
@@ -918,7 +929,8 @@ __global__ __launch_bounds__(256) void k_gn_apply_t(int C, int HW, int G, int nc
 // consumer rounds its operands to bf16 anyway, so its result is bit-identical to the fp32 path's
 // while this pass writes half the bytes and the conv reads half.  Workgroup: 256 pixels of one
 // (sample, group), every octet of the group.
-__global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const float *__restrict__ x,
+template <typename TX = float>
+__global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const TX *__restrict__ x,
                                                    const float *__restrict__ gamma, const float *__restrict__ beta,
                                                    const float *__restrict__ ss, const double *__restrict__ gnp,
                                                    float eps, __bf16 *__restrict__ y, int bm)
@@ -951,10 +963,10 @@ __global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const f
     }
     // this thread's first octet in flight behind the statistics
     const int pc = min(p, HW - 1);
-    const float *xb = x + ((size_t)b * C + g * cpg) * HW + pc;
+    const TX *xb = x + ((size_t)b * C + g * cpg) * HW + pc;
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = xb[(size_t)j * HW];
+    for (int j = 0; j < 8; ++j) v[j] = ldx(xb + (size_t)j * HW);
     __syncthreads();
     const float mean = st2[0], rstd = st2[1];
     const bool sso = ss != nullptr;
@@ -962,7 +974,7 @@ __global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const f
         float nx[8];
         if (o + 1 < cpg / 8) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) nx[j] = xb[(size_t)(8 * (o + 1) + j) * HW];
+            for (int j = 0; j < 8; ++j) nx[j] = ldx(xb + (size_t)(8 * (o + 1) + j) * HW);
         }
         bf16x8 h;
 #pragma unroll
@@ -983,7 +995,8 @@ __global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const f
 // without writing the C-channel activation.  Workgroup = 64 pixels of one sample, 16 waves; wave w takes
 // channels [w C/16, (w+1) C/16) and the 1x1 sums are combined over the waves in wave order.
 constexpr int GO_MAXF = 4, GO_NW = 16;
-__global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int G, const float *__restrict__ x,
+template <typename TX = float>
+__global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int G, const TX *__restrict__ x,
                                                              const float *__restrict__ gamma,
                                                              const float *__restrict__ beta,
                                                              const float *__restrict__ ss,
@@ -1006,7 +1019,7 @@ __global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int 
     for (int u = 0; u < 4; ++u) {
         const int c = min(c0 + u, C - 1);
         const size_t o = ((size_t)b * C + c) * HW + pc;
-        xv[u] = x[o];
+        xv[u] = ldx(x + o);
         rv[u] = post ? post[o] : 0.0f;
     }
     // (sample, group) statistics: wave w reduces groups w, w + GO_NW, ... exactly as k_gn_apply_t's wave 0
@@ -1037,7 +1050,7 @@ __global__ __launch_bounds__(64 * GO_NW) void k_gn_apply_out(int C, int HW, int 
     const bool sso = ss != nullptr;
     for (int c = c0; c < c1; ++c) {
         const int u = c - c0, g = c / cpg;
-        const float xe = u < 4 ? xv[u] : x[((size_t)b * C + c) * HW + pc];
+        const float xe = u < 4 ? xv[u] : ldx(x + ((size_t)b * C + c) * HW + pc);
         const float re = u < 4 ? rv[u] : (post ? post[((size_t)b * C + c) * HW + pc] : 0.0f);
         const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
         float v = gn_silu1(xe, st[g][0], st[g][1], gamma[c], beta[c], sso, sc1, sh);
@@ -2342,6 +2355,8 @@ struct C3Args {
     const __bf16 *x8;                // IN8: the input as bf16 octets [B][cin / 8][H W][8] (cin2 = 0)
     const __bf16 *w;                 // [cout][9][cinp]
     float *y;
+    __bf16 *yb;                      // non-null: the output rounded to bf16 and stored here instead of y
+                                     // (the GroupNorm statistics are then those of the rounded values)
     double *gnp;                     // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
     int cinp, K, M, HW, R, cch, plane, G;
 };
@@ -2554,16 +2569,36 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
                 acc[c][mb][r] = (acc[c][mb][r] + bv[c][r]) + rv[mb][c][r];
                 asm volatile("" : "+v"(acc[c][mb][r]));
             }
+    if (a.yb) {
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-        if (m0 + pl[mb] >= a.M) continue;
+        for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+            for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
-            }
+                for (int r = 0; r < 16; ++r) acc[c][mb][r] = (float)(__bf16)acc[c][mb][r];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            if (m0 + pl[mb] >= a.M) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.yb[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = (__bf16)acc[c][mb][r];
+                }
+        }
+    } else {
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            if (m0 + pl[mb] >= a.M) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
+                }
+        }
     }
     if (!a.gnp) return;
     // GroupNorm statistics of the tile's outputs (for k_gn_apply_t with bm = C3_BM; HW >= C3_BM so a
@@ -3081,6 +3116,7 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
 // upsampled input) with at least C3_MIN_TILES tiles; everything else stays on the per-tap kernel. The
 // halo kernel wins even on a part-filled chip (bf16 U-Net forward, B = 25: 4.15 -> 3.13 ms, B = 100:
 // 8.0 -> 6.2 ms, B = 344: 18.5 -> 18.1 ms going from 512 to 64); below ~64 tiles it loses at B <= 8
+static int C3_BF16_RAW = 1;      // rdq_unet_set_option(RDQ_UNET_OPT_BF16_RAW)
 static int C3_MIN_TILES = 64;    // rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES); tools/conv3_threshold_ab.py
 bool conv3_ok(const rdq_conv_desc *d)
 {
@@ -3138,6 +3174,12 @@ bool conv_desc_ok(const rdq_conv_desc *d)
         if (nch < 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<true>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
         else if (gn4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false, 4>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
         else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false>), GRID, dim3(256), 0, ST, __VA_ARGS__);      \
+    } while (0)
+#define LAUNCH_GN_TB(GRID, ST, ...)                                                                    \
+    do {                                                                                               \
+        if (nch < 0) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<true, 1, __bf16>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
+        else if (gn4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false, 4, __bf16>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_t<false, 1, __bf16>), GRID, dim3(256), 0, ST, __VA_ARGS__); \
     } while (0)
 #define LAUNCH_GN(GRID, ST, ...)                                                                       \
     do {                                                                                               \
@@ -3459,7 +3501,7 @@ int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
     }
     const int HW = c.HW;
-    hipLaunchKernelGGL(k_gn_apply_out, dim3((HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, HW, G, c.y, gamma, beta,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_out<float>), dim3((HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, HW, G, c.y, gamma, beta,
                        scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf);
     RDQ_CHECK(hipGetLastError());
     return 0;
@@ -3550,6 +3592,11 @@ static int g_bf16_per_tap = 0;   // RDQ_UNET_OPT_BF16_PER_TAP
 
 int rdq_unet_set_option(int32_t option, int32_t value)
 {
+    if (option == RDQ_UNET_OPT_BF16_RAW) {
+        const int old = C3_BF16_RAW;
+        C3_BF16_RAW = value != 0;
+        return old;
+    }
     if (option == RDQ_UNET_OPT_CONV3_MIN_TILES) {
         if (value < 1) return RDQ_E_INVALID;
         const int old = C3_MIN_TILES;
@@ -3647,6 +3694,7 @@ static bool bf16_gn_conv(const rdq_conv_desc *d, const float *x, const float *x2
     float *h = static_cast<float *>(ws);
     c = C3Args{};
     c.d = *d; c.x = x; c.x2 = x2; c.w = static_cast<const __bf16 *>(wp); c.bias = bias; c.res = nullptr; c.y = h;
+    c.yb = C3_BF16_RAW ? reinterpret_cast<__bf16 *>(h) : nullptr;   // raw conv output held as bf16
     c.gnp = reinterpret_cast<double *>(h + M * d->cout);
     c.G = G;
     c.cinp = bf_cinp(d);
@@ -3676,8 +3724,12 @@ int rdq_conv2d_bf16_gn_silu8(const rdq_conv_desc *d, const float *x, const float
         !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st))
         return RDQ_E_INVALID;
     const int HW = c.HW;
-    hipLaunchKernelGGL(k_gn_apply8, dim3((HW + 255) / 256, d->B * G), dim3(256), 0, st, d->cout, HW, G, c.y, gamma,
-                       beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
+    if (c.yb)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply8<__bf16>), dim3((HW + 255) / 256, d->B * G), dim3(256), 0, st, d->cout,
+                           HW, G, c.yb, gamma, beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply8<float>), dim3((HW + 255) / 256, d->B * G), dim3(256), 0, st, d->cout,
+                           HW, G, c.y, gamma, beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3693,8 +3745,12 @@ int rdq_conv2d_bf16_gn_silu_x8(const rdq_conv_desc *d, const void *x8, const voi
     int nch = 0;
     bool gn4 = false;
     const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
-    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
-                       scale_shift, c.gnp, eps, post_residual, y, C3_BM);
+    if (c.yb)
+        LAUNCH_GN_TB(dim3(gxa, d->B * G), st, C, HW, G, nch, c.yb, gamma, beta, scale_shift, c.gnp, eps, post_residual, y,
+                     C3_BM);
+    else
+        LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta, scale_shift, c.gnp, eps, post_residual, y,
+                    C3_BM);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3709,8 +3765,12 @@ int rdq_conv2d_bf16_gn_silu(const rdq_conv_desc *d, const float *x, const float 
     int nch = 0;
     bool gn4 = false;
     const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
-    LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta,
-                       scale_shift, c.gnp, eps, post_residual, y, C3_BM);
+    if (c.yb)
+        LAUNCH_GN_TB(dim3(gxa, d->B * G), st, C, HW, G, nch, c.yb, gamma, beta, scale_shift, c.gnp, eps, post_residual, y,
+                     C3_BM);
+    else
+        LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, c.y, gamma, beta, scale_shift, c.gnp, eps, post_residual, y,
+                    C3_BM);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3724,8 +3784,14 @@ int rdq_conv2d_bf16_gn_silu_out(const rdq_conv_desc *d, const float *x, const fl
     if (!yf || !wf || !gamma || !beta || nf < 1 || nf > GO_MAXF || G > 64 ||
         !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st))
         return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_gn_apply_out, dim3((c.HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, c.HW, G, c.y,
-                       gamma, beta, scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf, C3_BM);
+    if (c.yb)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_out<__bf16>), dim3((c.HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st,
+                           d->cout, c.HW, G, c.yb, gamma, beta, scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf,
+                           C3_BM);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_out<float>), dim3((c.HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st,
+                           d->cout, c.HW, G, c.y, gamma, beta, scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf,
+                           C3_BM);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

@@ -450,8 +450,9 @@ def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
 
 
 # Block.forward on the bf16 halo-staged conv with the GroupNorm statistics in its epilogue
-# (rdq_conv2d_bf16_gn_silu, the configs[4] batched U-Net) vs the same conv followed by the separate
-# GroupNorm pass: the conv output is the same kernel's; the statistics differ in fp64 summation order
+# (rdq_conv2d_bf16_gn_silu, the configs[4] batched U-Net) vs the same conv, its output rounded to bf16
+# (the fused path holds the raw conv output as bf16), followed by the separate GroupNorm pass: the
+# statistics differ in fp64 summation order only
 @pytest.mark.parametrize("cin1,cin2,cout,H,B,ss,post,mode", [
     (64, 0, 64, 72, 32, True, True, "plain"), (64, 64, 64, 72, 32, True, False, "plain"),
     (128, 0, 128, 36, 128, False, True, "plain"), (256, 0, 256, 18, 128, True, False, "plain"),
@@ -475,7 +476,8 @@ def test_conv_bf16_gn_silu_fused(cuda, cin1, cin2, cout, H, B, ss, post, mode):
     with torch.no_grad(), ops.precision("bf16"):
         got = torch.ops.red_diffeq.conv2d_bf16_gn_silu(x, x2, conv.weight, conv.bias, 1, md, norm.weight, norm.bias,
                                                        sc, 8, float(norm.eps), pr)
-        ref = ops.group_norm_affine_silu(ops.conv2d(x, conv, x2=x2, mode=md), norm, sc)
+        raw = ops.conv2d(x, conv, x2=x2, mode=md).to(torch.bfloat16).float()
+        ref = ops.group_norm_affine_silu(raw, norm, sc)
         if post:
             ref = ref + pr
     close(got, ref, rel=1e-5)

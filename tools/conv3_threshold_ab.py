@@ -15,6 +15,7 @@ from red_diffeq import _hip  # noqa: E402
 from red_diffeq.models.diffusion import Unet  # noqa: E402
 
 OPT_CONV3_MIN_TILES = 2
+OPT_BF16_RAW = 3
 
 
 def main():
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--B", type=int, nargs="+", default=[344])
     ap.add_argument("--min-tiles", type=int, nargs="+", default=[512, 384, 256, 128])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--bf16-raw", type=int, nargs="+", default=[1],
+                    help="RDQ_UNET_OPT_BF16_RAW values to A/B (raw conv output held as bf16 or fp32)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -33,8 +36,9 @@ def main():
         x = torch.randn(B, 1, 72, 72, device=dev).clamp(-1, 1)
         t = torch.randint(0, 1000, (B,), device=dev)
         base = None
-        for mt in a.min_tiles:
+        for mt, raw in [(m, r) for m in a.min_tiles for r in a.bf16_raw]:
             net.__dict__.pop("_graphs", None)          # small batches replay a captured graph: recapture
+            old_raw = lib.rdq_unet_set_option(OPT_BF16_RAW, raw)
             old = lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, mt)
             assert old > 0
             try:
@@ -51,10 +55,11 @@ def main():
                         ts.append(ev[0].elapsed_time(ev[1]))
             finally:
                 lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, old)
+                lib.rdq_unet_set_option(OPT_BF16_RAW, old_raw)
             if base is None:
                 base = y.clone()
             d = ((y - base).abs().max() / base.abs().max()).item()
-            print(json.dumps({"B": B, "min_tiles": mt, "ms_median": round(sorted(ts)[len(ts) // 2], 3),
+            print(json.dumps({"B": B, "min_tiles": mt, "bf16_raw": raw, "ms_median": round(sorted(ts)[len(ts) // 2], 3),
                               "ms_min": round(min(ts), 3), "rel_diff_vs_first": d}), flush=True)
 
 
