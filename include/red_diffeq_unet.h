@@ -132,6 +132,7 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
 #define RDQ_UNET_OPT_BF16_PER_TAP 1
 #define RDQ_UNET_OPT_CONV3_MIN_TILES 2   /* least (256-pixel x 64-channel) tiles for the halo-staged 3x3 conv (default 64) */
 #define RDQ_UNET_OPT_BF16_RAW 3   /* rdq_conv2d_bf16_gn_*: hold the raw conv output as bf16 (default 1) */
+#define RDQ_UNET_OPT_CONV3F_MIN_TILES 4   /* least tiles for the fp32 halo-staged 3x3 conv (0: never; default 192) */
 int rdq_unet_set_option(int32_t option, int32_t value);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);

@@ -2354,12 +2354,154 @@ struct C3Args {
     const float *x, *x2, *bias, *res;
     const __bf16 *x8;                // IN8: the input as bf16 octets [B][cin / 8][H W][8] (cin2 = 0)
     const __bf16 *w;                 // [cout][9][cinp]
+    const float *wf;                 // k_conv3_f32: the fp32 weights in torch's own layout [cout][cin][3][3]
     float *y;
     __bf16 *yb;                      // non-null: the output rounded to bf16 and stored here instead of y
                                      // (the GroupNorm statistics are then those of the rounded values)
     double *gnp;                     // non-null: GroupNorm(G) partial statistics per (m tile, group, slot)
     int cinp, K, M, HW, R, cch, plane, G;
 };
+
+// the halo-staged convs' epilogue (k_conv3_bf16, k_conv3_f32): bias, residual, the store (fp32, or
+// rounded to bf16 when a.yb is set) and the tile's GroupNorm partial statistics.  halo: the kernel's
+// halo buffers (free after the last chunk's barrier; >= 32 KiB); c3g: [8-channel block][slot][s, q].
+__device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2], const int (&pl)[2], void *halo,
+                                            double (*c3g)[2][2])
+{
+    const rdq_conv_desc &d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int m0 = blockIdx.x * C3_BM, n0 = blockIdx.y * C3_BN;
+    // epilogue: the bias and residual of all 64 outputs of the lane are loaded before the first
+    // store (gfx9 retires stores and loads in one in-order count: a load issued after a store would
+    // wait for it), then every output is formed, then stored
+    int ob[2], opix[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int mc = min(m0 + pl[mb], a.M - 1);
+        ob[mb] = mc / a.HW;
+        opix[mb] = mc - ob[mb] * a.HW;
+    }
+    float bv[2][16] = {}, rv[2][2][16] = {};
+    if (a.bias) {                       // (conditions hoisted: a per-element "load or 0" would make
+#pragma unroll                          //  the compiler branch and wait around every load)
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bv[c][r] = a.bias[n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+    }
+    if (a.res) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) rv[mb][c][r] = a.res[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]];
+            }
+    }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[c][mb][r] = (acc[c][mb][r] + bv[c][r]) + rv[mb][c][r];
+                asm volatile("" : "+v"(acc[c][mb][r]));
+            }
+    if (a.yb) {
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[c][mb][r] = (float)(__bf16)acc[c][mb][r];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            if (m0 + pl[mb] >= a.M) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.yb[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = (__bf16)acc[c][mb][r];
+                }
+        }
+    } else {
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            if (m0 + pl[mb] >= a.M) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
+                }
+        }
+    }
+    if (!a.gnp) return;
+    // GroupNorm statistics of the tile's outputs (for k_gn_apply_t with bm = C3_BM; HW >= C3_BM so a
+    // tile spans at most two samples): fp64 sum and sum of squares per 8-channel block e = c*4 + (r >> 2)
+    // (a lane's 4 channels r & 3; the other half-wave holds the block's other 4) and sample slot.  Each
+    // thread's partials go through the halo buffer (free after the last chunk's barrier), four blocks
+    // at a time, and 16 threads per (block, slot, sum) add 16 of them each in thread order, then a
+    // fixed xor tree: deterministic, no long shuffle chains of fp64 per lane.
+    double *red = static_cast<double *>(halo);          // [16][256] per round (32 KiB)
+    const int b0 = m0 / a.HW;
+    int sl[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int m = m0 + pl[mb];
+        sl[mb] = m < a.M ? m / a.HW - b0 : -1;
+    }
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+#pragma unroll
+        for (int el = 0; el < 4; ++el) {
+            const int e = rd * 4 + el;
+            double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                double s1 = 0.0, q1 = 0.0;
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const double xv = acc[e >> 2][mb][(e & 3) * 4 + r4];
+                    s1 += xv;
+                    q1 += xv * xv;
+                }
+                gs[0] += sl[mb] == 0 ? s1 : 0.0;
+                gq[0] += sl[mb] == 0 ? q1 : 0.0;
+                gs[1] += sl[mb] == 1 ? s1 : 0.0;
+                gq[1] += sl[mb] == 1 ? q1 : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                red[((el * 2 + k) * 2 + 0) * 256 + tid] = gs[k];
+                red[((el * 2 + k) * 2 + 1) * 256 + tid] = gq[k];
+            }
+        }
+        __syncthreads();
+        const int combo = tid >> 4, part = tid & 15;
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v += red[combo * 256 + part + 16 * j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (part == 0) c3g[rd * 4 + (combo >> 2)][(combo >> 1) & 1][combo & 1] = v;
+        __syncthreads();
+    }
+    const int cpg = d.cout / a.G, gt = C3_BN / cpg, epg = cpg / 8;
+    if (tid < 2 * gt) {
+        const int g = tid >> 1, k = tid & 1;
+        double s = 0.0, q = 0.0;
+        for (int e = g * epg; e < (g + 1) * epg; ++e) {
+            s += c3g[e][k][0];
+            q += c3g[e][k][1];
+        }
+        double *o = a.gnp + (((size_t)blockIdx.x * a.G + n0 / cpg + g) * 2 + k) * 2;
+        o[0] = s;
+        o[1] = q;
+    }
+}
 
 template <int MODE, bool IN8 = false>
 __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
@@ -2533,137 +2675,160 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
     for (int cc = 0; cc + 1 < a.cch; ++cc) chunk(cc, std::true_type{});
     chunk(a.cch - 1, std::false_type{});
 
-    // epilogue: the bias and residual of all 64 outputs of the lane are loaded before the first
-    // store (gfx9 retires stores and loads in one in-order count: a load issued after a store would
-    // wait for it), then every output is formed, then stored
-    int ob[2], opix[2];
+    __shared__ double c3g[8][2][2];
+    c3_epilogue(a, acc, pl, &Hs[0][0][0], c3g);
+}
+
+// ------------------------------------------------------------- conv2d 3x3, fp32, halo-staged
+// k_conv3_bf16's structure on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: exact fp32 products,
+// the reference's precision) for the batched fp32 U-Net (configs/openfwi/red-diffeq.yaml's B = 25,
+// the fp32 option of configs[4]).  A 16-channel chunk's halo is 80-B rows of 16 floats (the bf16
+// kernel's row bytes, so its conflict-free ds_read_b128 pattern carries over); two lane groups read
+// float4s of channels 8 q + 4 g .. + 3 and feed them to four MFMA k-steps, the weights through the
+// same mapping, so every channel meets its own weight once.  Weights are read in torch's layout
+// (no packing pass): a thread's four channels of a tap are four loads 9 floats apart, three taps
+// ahead.  The halo items of the next chunk (2 octets x 402 rows: four per thread) are issued over
+// taps 0-3 and stored four taps later.  Epilogue and GroupNorm statistics: c3_epilogue.
+constexpr int C3F_BK = 16, C3F_NI = 4, C3F_LD = 20;
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
+{
+    __shared__ __attribute__((aligned(16))) float Hs[2][C3_ROWS][C3F_LD];    // 2 x 31.4 KiB
+    __shared__ __attribute__((aligned(16))) float Ws[2][C3_BN][C3F_LD];
+    const rdq_conv_desc &d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * C3_BM, n0 = blockIdx.y * C3_BN;
+    const int cin = d.cin1 + d.cin2;
+    // halo items: octet ho of the chunk for rows q = lane + 64 (2 k + (wv >> 1)); source pixel packed
+    // b << 20 | pix as in k_conv3_bf16 (~0u: outside the batch or past the halo -> zeros)
+    const int ho = wv & 1;
+    unsigned it_src[C3F_NI];
+#pragma unroll
+    for (int k = 0; k < C3F_NI; ++k) {
+        const int q = lane + 64 * (2 * k + (wv >> 1)), p = m0 - d.W - 1 + q;
+        const bool in = q < a.R && p >= 0 && p < a.M;
+        const int b = in ? p / a.HW : 0, pp = in ? p - b * a.HW : 0;
+        int pix = pp;
+        if constexpr (MODE == RDQ_IN_UPSAMPLE2) {
+            const int ih = pp / d.W, iw = pp - ih * d.W;
+            pix = (ih >> 1) * (d.W >> 1) + (iw >> 1);
+        }
+        it_src[k] = in ? ((unsigned)b << 20 | (unsigned)pix) : ~0u;
+    }
+    auto hload = [&](int k, int cc, float (&v)[8]) -> bool {
+        const unsigned s = it_src[k];
+        const int c = cc * C3F_BK + 8 * ho;
+        const bool lo = c < d.cin1;
+        const float *__restrict__ base = lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
+        const unsigned cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane;
+        const bool ok = s != ~0u && c < cin;
+        const unsigned o = ok ? (s >> 20) * cstride + (s & 0xfffff) : 0u;
+        if (c >= cin) base = a.x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = base[o + (unsigned)(j * a.plane)];
+        return ok;
+    };
+    auto hstore = [&](int buf, int k, const float (&v)[8], bool ok) {
+        const int q = lane + 64 * (2 * k + (wv >> 1));
+        if (q < a.R) {
+            float4 *dst = reinterpret_cast<float4 *>(&Hs[buf][q][8 * ho]);
+            dst[0] = ok ? float4{v[0], v[1], v[2], v[3]} : float4{0.0f, 0.0f, 0.0f, 0.0f};
+            dst[1] = ok ? float4{v[4], v[5], v[6], v[7]} : float4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    // weight role: row wn (of 64), channels wq .. wq + 3 of the chunk (cin % 8 == 0: all four inside or
+    // all outside the input channels)
+    const int wn = tid >> 2, wq = (tid & 3) * 4;
+    const float *wrow = a.wf + (size_t)(n0 + wn) * cin * 9;
+    auto wload = [&](int cc, int t) -> float4 {
+        const int c = cc * C3F_BK + wq;
+        const bool ok = c < cin;
+        const float *pw = wrow + (ok ? c * 9 + t : 0);
+        const float4 v{pw[0], pw[9], pw[18], pw[27]};
+        return ok ? v : float4{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+    auto wstash = [&](int buf, const float4 &v) { *reinterpret_cast<float4 *>(&Ws[buf][wn][wq]) = v; };
+    int pl[2];
+    unsigned tmask[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
-        const int mc = min(m0 + pl[mb], a.M - 1);
-        ob[mb] = mc / a.HW;
-        opix[mb] = mc - ob[mb] * a.HW;
-    }
-    float bv[2][16] = {}, rv[2][2][16] = {};
-    if (a.bias) {                       // (conditions hoisted: a per-element "load or 0" would make
-#pragma unroll                          //  the compiler branch and wait around every load)
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bv[c][r] = a.bias[n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
-    }
-    if (a.res) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-#pragma unroll
-                for (int mb = 0; mb < 2; ++mb) rv[mb][c][r] = a.res[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]];
-            }
-    }
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc[c][mb][r] = (acc[c][mb][r] + bv[c][r]) + rv[mb][c][r];
-                asm volatile("" : "+v"(acc[c][mb][r]));
-            }
-    if (a.yb) {
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[c][mb][r] = (float)(__bf16)acc[c][mb][r];
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            if (m0 + pl[mb] >= a.M) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    a.yb[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = (__bf16)acc[c][mb][r];
-                }
-        }
-    } else {
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            if (m0 + pl[mb] >= a.M) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
-                }
-        }
-    }
-    if (!a.gnp) return;
-    // GroupNorm statistics of the tile's outputs (for k_gn_apply_t with bm = C3_BM; HW >= C3_BM so a
-    // tile spans at most two samples): fp64 sum and sum of squares per 8-channel block e = c*4 + (r >> 2)
-    // (a lane's 4 channels r & 3; the other half-wave holds the block's other 4) and sample slot.  Each
-    // thread's partials go through the halo buffer (free after the last chunk's barrier), four blocks
-    // at a time, and 16 threads per (block, slot, sum) add 16 of them each in thread order, then a
-    // fixed xor tree: deterministic, no long shuffle chains of fp64 per lane.
-    __shared__ double c3g[8][2][2];                     // [8-channel block][slot][s, q]
-    double *red = reinterpret_cast<double *>(&Hs[0][0][0]);   // [16][256] per round (32 KiB)
-    const int b0 = m0 / a.HW;
-    int sl[2];
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
+        pl[mb] = wv * 64 + mb * 32 + (lane & 31);
         const int m = m0 + pl[mb];
-        sl[mb] = m < a.M ? m / a.HW - b0 : -1;
+        const int pix = m < a.M ? m % a.HW : 0, oh = pix / d.W, ow = pix - oh * d.W;
+        unsigned bits = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ih = oh + t / 3 - 1, iw = ow + t % 3 - 1;
+            bits |= ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W) ? 1u << t : 0u;
+        }
+        tmask[mb] = m < a.M ? bits : 0u;
     }
+    const int kg = 4 * (lane >> 5);
+    f32x16 acc[2][2];
 #pragma unroll
-    for (int rd = 0; rd < 2; ++rd) {
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int el = 0; el < 4; ++el) {
-            const int e = rd * 4 + el;
-            double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
+        for (int mb = 0; mb < 2; ++mb) acc[c][mb] = f32x16{};
+    {   // chunk 0's halo
+        float v[C3F_NI][8];
+        bool ok[C3F_NI];
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-                double s1 = 0.0, q1 = 0.0;
+        for (int k = 0; k < C3F_NI; ++k) ok[k] = hload(k, 0, v[k]);
 #pragma unroll
-                for (int r4 = 0; r4 < 4; ++r4) {
-                    const double xv = acc[e >> 2][mb][(e & 3) * 4 + r4];
-                    s1 += xv;
-                    q1 += xv * xv;
+        for (int k = 0; k < C3F_NI; ++k) hstore(0, k, v[k], ok[k]);
+    }
+    float4 wr[3];
+    wr[0] = wload(0, 0);
+    wr[1] = wload(0, 1);
+    wr[2] = wload(0, 2);
+    wstash(0, wr[0]);
+    __syncthreads();
+
+    auto chunk = [&](int cc, auto pf) {
+        constexpr bool PF = decltype(pf)::value;
+        float hv[C3F_NI][8];
+        bool hok[C3F_NI];
+        const int hb = cc & 1;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int s = cc * 9 + t;
+            wr[t % 3] = wload(min(cc + (t + 3) / 9, a.cch - 1), (t + 3) % 9);
+            if constexpr (PF) {
+                if (t >= 4 && t < 4 + C3F_NI) hstore(hb ^ 1, t - 4, hv[t - 4], hok[t - 4]);
+                if (t < C3F_NI) hok[t] = hload(t, cc + 1, hv[t]);
+            }
+            const int toff = (t / 3) * d.W + t % 3;
+            const float *wsb = &Ws[s & 1][0][0];
+#pragma unroll
+            for (int q2 = 0; q2 < 2; ++q2) {
+                const int kk = 8 * q2 + kg;
+                float4 bfr[2], afr[2];
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) {
+                    float4 v = *reinterpret_cast<const float4 *>(&Hs[hb][pl[mb] + toff][kk]);
+                    if (!((tmask[mb] >> t) & 1u)) v = float4{0.0f, 0.0f, 0.0f, 0.0f};
+                    bfr[mb] = v;
                 }
-                gs[0] += sl[mb] == 0 ? s1 : 0.0;
-                gq[0] += sl[mb] == 0 ? q1 : 0.0;
-                gs[1] += sl[mb] == 1 ? s1 : 0.0;
-                gq[1] += sl[mb] == 1 ? q1 : 0.0;
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    afr[c] = *reinterpret_cast<const float4 *>(wsb + (c * 32 + (lane & 31)) * C3F_LD + kk);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int mb = 0; mb < 2; ++mb)
+                            acc[c][mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(afr[c][j], bfr[mb][j], acc[c][mb], 0, 0, 0);
             }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                red[((el * 2 + k) * 2 + 0) * 256 + tid] = gs[k];
-                red[((el * 2 + k) * 2 + 1) * 256 + tid] = gq[k];
-            }
+            wstash((s + 1) & 1, wr[(t + 1) % 3]);
+            __syncthreads();
         }
-        __syncthreads();
-        const int combo = tid >> 4, part = tid & 15;
-        double v = 0.0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v += red[combo * 256 + part + 16 * j];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-        if (part == 0) c3g[rd * 4 + (combo >> 2)][(combo >> 1) & 1][combo & 1] = v;
-        __syncthreads();
-    }
-    const int cpg = d.cout / a.G, gt = C3_BN / cpg, epg = cpg / 8;
-    if (tid < 2 * gt) {
-        const int g = tid >> 1, k = tid & 1;
-        double s = 0.0, q = 0.0;
-        for (int e = g * epg; e < (g + 1) * epg; ++e) {
-            s += c3g[e][k][0];
-            q += c3g[e][k][1];
-        }
-        double *o = a.gnp + (((size_t)blockIdx.x * a.G + n0 / cpg + g) * 2 + k) * 2;
-        o[0] = s;
-        o[1] = q;
-    }
+    };
+    for (int cc = 0; cc + 1 < a.cch; ++cc) chunk(cc, std::true_type{});
+    chunk(a.cch - 1, std::false_type{});
+    __shared__ double c3g[8][2][2];
+    c3_epilogue(a, acc, pl, &Hs[0][0][0], c3g);
 }
 
 // ------------------------------------------------------ stem conv (7 x 7, one input channel)
@@ -3118,9 +3283,10 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
 // 8.0 -> 6.2 ms, B = 344: 18.5 -> 18.1 ms going from 512 to 64); below ~64 tiles it loses at B <= 8
 static int C3_BF16_RAW = 1;      // rdq_unet_set_option(RDQ_UNET_OPT_BF16_RAW)
 static int C3_MIN_TILES = 64;    // rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES); tools/conv3_threshold_ab.py
-bool conv3_ok(const rdq_conv_desc *d)
+static int C3F_MIN_TILES = 192;  // k_conv3_f32; rdq_unet_set_option(RDQ_UNET_OPT_CONV3F_MIN_TILES), 0 = never
+static int64_t conv3_tiles(const rdq_conv_desc *d)
 {
-    if (d->kh != 3 || d->kw != 3 || d->pad != 1) return false;
+    if (d->kh != 3 || d->kw != 3 || d->pad != 1) return 0;
     if (d->in_mode != RDQ_IN_PLAIN && d->in_mode != RDQ_IN_UPSAMPLE2) return false;
     if (d->cin1 % 8 || d->cin2 % 8 || d->cout % C3_BN || d->W > C3_WMAX || d->B >= 4096) return false;
     const int64_t HW = (int64_t)d->H * d->W, M = d->B * HW;
@@ -3128,7 +3294,29 @@ bool conv3_ok(const rdq_conv_desc *d)
     // the halo gather addresses each input tensor with 32-bit element offsets
     const int64_t plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? HW / 4 : HW;
     if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane >= (int64_t)1 << 32) return false;
-    return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN) >= C3_MIN_TILES;
+    return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN);
+}
+bool conv3_ok(const rdq_conv_desc *d) { return conv3_tiles(d) >= C3_MIN_TILES; }
+bool conv3f_ok(const rdq_conv_desc *d) { return C3F_MIN_TILES > 0 && conv3_tiles(d) >= C3F_MIN_TILES; }
+
+// k_conv3_f32 on a conv3f_ok descriptor (raw fp32 weights); gnp: GroupNorm partials (bm = C3_BM) or null
+void launch_conv3_f32(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
+                      const float *res, float *y, double *gnp, int G, hipStream_t st)
+{
+    C3Args c{};
+    c.d = *d; c.x = x; c.x2 = x2; c.wf = w; c.bias = bias; c.res = res; c.y = y; c.gnp = gnp; c.G = G;
+    c.cinp = (d->cin1 + d->cin2 + C3F_BK - 1) / C3F_BK * C3F_BK;
+    c.K = 9 * c.cinp;
+    c.HW = d->H * d->W;
+    c.M = d->B * c.HW;
+    c.R = C3_BM + 2 * d->W + 2;
+    c.cch = c.cinp / C3F_BK;
+    c.plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? c.HW / 4 : c.HW;
+    const dim3 grid((c.M + C3_BM - 1) / C3_BM, d->cout / C3_BN);
+    if (d->in_mode == RDQ_IN_UPSAMPLE2)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_f32<RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3_f32<RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
 }
 
 int bf_cinp(const rdq_conv_desc *d) { return (d->cin1 + d->cin2 + BF_BK - 1) / BF_BK * BF_BK; }
@@ -3237,6 +3425,11 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UNSHUFFLE2 && (d->cin1 % 4 != 0 || d->cin2 != 0)) return RDQ_E_INVALID;
     if (d->in_mode == RDQ_IN_UPSAMPLE2 && ((d->H | d->W) & 1 || d->cin2 != 0)) return RDQ_E_INVALID;
+    if (conv3f_ok(d)) {
+        launch_conv3_f32(d, x, x2, w, bias, residual, y, nullptr, 0, st);
+        RDQ_CHECK(hipGetLastError());
+        return 0;
+    }
     if (cc_ok(d)) {
         CcArgs c{};
         c.d = *d; c.x = x; c.x2 = x2; c.w = w; c.bias = bias; c.res = residual; c.y = y;
@@ -3334,6 +3527,15 @@ static bool gn_conv_args(CcArgs &c, const rdq_conv_desc *d, const float *x, cons
     return true;
 }
 
+// the conv of a gn_conv_args Block on the fp32 halo-staged kernel when it applies (a 256-pixel tile
+// then spans at most two samples, as the statistics' slots assume); true: launched, bm = C3_BM
+static bool conv3f_gn(const CcArgs &c, const rdq_conv_desc *d, int32_t G, hipStream_t st)
+{
+    if (!conv3f_ok(d) || d->H * d->W < C3_BM) return false;
+    launch_conv3_f32(d, c.x, c.x2, c.w, c.bias, nullptr, c.y, c.gnp, G, st);
+    return true;
+}
+
 int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, const float *w, const float *bias,
                        int32_t G, float eps, const float *gamma, const float *beta, const float *scale_shift,
                        const float *post_residual, float *y, void *ws, size_t ws_bytes, uint32_t *tickets,
@@ -3344,12 +3546,13 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     float *h = c.y;
     double *gnp = c.gnp;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-    if (d->kh == 3) {
+    const int bm = conv3f_gn(c, d, G, st) ? C3_BM : CC_BM;    // launched there, or here:
+    if (bm == CC_BM && d->kh == 3) {
         if (d->in_mode == RDQ_IN_UPSAMPLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    } else {
+    } else if (bm == CC_BM) {
         if (d->in_mode == RDQ_IN_UNSHUFFLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
         else
@@ -3360,7 +3563,7 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     bool gn4 = false;
     const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
-                       scale_shift, gnp, eps, post_residual, y);
+                       scale_shift, gnp, eps, post_residual, y, bm);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3427,14 +3630,21 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
     e.S = (slabs_s && tickets) ? cc_splits(&ds, slabs_s, &e.per_split) : 1;
     if (e.S == 1) e.per_split = e.nstages;
     const int gy_a = (d->cout + CC_BN - 1) / CC_BN, gy_b = (cout_s + CC_BN - 1) / CC_BN;
-    const dim3 grid((c.M + CC_BM - 1) / CC_BM, gy_a + gy_b, std::max(c.S, e.S));
-    hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
+    int bm = CC_BM;
+    if (conv3f_gn(c, d, G, st)) {     // the 3x3 on the halo-staged kernel, the shortcut on its own
+        bm = C3_BM;
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), dim3((e.M + CC_BM - 1) / CC_BM, gy_b, e.S),
+                           dim3(256), 0, st, e);
+    } else {
+        const dim3 grid((c.M + CC_BM - 1) / CC_BM, gy_a + gy_b, std::max(c.S, e.S));
+        hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
+    }
     const int C = d->cout, HW = c.HW;
     int nch = 0;
     bool gn4 = false;
     const int gxa = gn_grid(d->B, C, G, HW, &nch, &gn4);
     LAUNCH_GN_T(dim3(gxa, d->B * G), st, C, HW, G, nch, h, gamma, beta,
-                       scale_shift, c.gnp, eps, nullptr, y);
+                       scale_shift, c.gnp, eps, nullptr, y, bm);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3489,12 +3699,13 @@ int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *
         !gn_conv_args(c, d, x, x2, w, bias, G, ws, ws_bytes, tickets))
         return RDQ_E_INVALID;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
-    if (d->kh == 3) {
+    const int bm = conv3f_gn(c, d, G, st) ? C3_BM : CC_BM;    // launched there, or here:
+    if (bm == CC_BM && d->kh == 3) {
         if (d->in_mode == RDQ_IN_UPSAMPLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    } else {
+    } else if (bm == CC_BM) {
         if (d->in_mode == RDQ_IN_UNSHUFFLE2)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
         else
@@ -3502,7 +3713,7 @@ int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *
     }
     const int HW = c.HW;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_out<float>), dim3((HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, HW, G, c.y, gamma, beta,
-                       scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf);
+                       scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf, bm);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -3592,6 +3803,12 @@ static int g_bf16_per_tap = 0;   // RDQ_UNET_OPT_BF16_PER_TAP
 
 int rdq_unet_set_option(int32_t option, int32_t value)
 {
+    if (option == RDQ_UNET_OPT_CONV3F_MIN_TILES) {
+        if (value < 0) return RDQ_E_INVALID;
+        const int old = C3F_MIN_TILES;
+        C3F_MIN_TILES = value;
+        return old;
+    }
     if (option == RDQ_UNET_OPT_BF16_RAW) {
         const int old = C3_BF16_RAW;
         C3_BF16_RAW = value != 0;

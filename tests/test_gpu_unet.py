@@ -449,6 +449,63 @@ def test_conv3_bf16_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
     close(got, per_tap, rel=2e-5)
 
 
+@pytest.mark.parametrize("cin1,cin2,cout,H,B,mode,res", [
+    (64, 0, 64, 72, 10, "plain", False),        # tiles straddle images (5184 % 256 = 64), ragged last tile
+    (64, 64, 64, 36, 40, "plain", True),        # concatenated skip + residual (decoder ResNet block)
+    (24, 16, 128, 36, 20, "plain", False),      # channel padding inside a 16-channel chunk (40 -> 48)
+    (128, 0, 128, 18, 104, "up", False),        # nearest-upsampled input (9 -> 18)
+    (256, 256, 512, 9, 80, "plain", True),      # 9 x 9 level: halo of 256 + 20 rows, 8 cout tiles
+])
+def test_conv3_f32_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
+    """The fp32 halo-staged 3x3 kernel (k_conv3_f32, >= 192 tiles): against the fp64 conv on the host
+    and against the per-tap fp32 kernel (rdq_unet_set_option(RDQ_UNET_OPT_CONV3F_MIN_TILES, 0)):
+    exact fp32 products, only the summation order differs."""
+    from red_diffeq import _hip
+    from red_diffeq.models import unet_ops as ops
+    F = torch.nn.functional
+    torch.manual_seed(15)
+    Hin = H // 2 if mode == "up" else H
+    conv = nn.Conv2d(cin1 + cin2, cout, 3, padding=1).to(cuda)
+    a = torch.randn(B, cin1, Hin, Hin, device=cuda)
+    b = torch.randn(B, cin2, H, H, device=cuda) if cin2 else None
+    r = torch.randn(B, cout, H, H, device=cuda) if res else None
+    md = ops.UPSAMPLE2 if mode == "up" else ops.PLAIN
+    got = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
+    old = _hip.lib().rdq_unet_set_option(4, 0)                   # RDQ_UNET_OPT_CONV3F_MIN_TILES
+    assert old == 192
+    try:
+        per_tap = ops.conv2d(a, conv, x2=b, mode=md, residual=r)
+    finally:
+        _hip.lib().rdq_unet_set_option(4, old)
+    xin = R.upsample_nearest2(a) if mode == "up" else (torch.cat((a, b), 1) if cin2 else a)
+    ref = F.conv2d(xin.double().cpu(), conv.weight.double().cpu(), conv.bias.double().cpu(), padding=1)
+    ref = (ref + (r.double().cpu() if res else 0)).float().to(cuda)
+    close(got, ref, rel=5e-6, what="halo fp32 vs fp64")
+    close(per_tap, ref, rel=5e-6, what="per-tap fp32 vs fp64")
+    close(got, per_tap, rel=5e-6)
+
+
+def test_unet_fp32_halo_conv_batched(cuda):
+    """The fp32 U-Net at the reference's openfwi batch (B = 25: its 72 x 72 and 36 x 36 Blocks, the
+    up path's block1 + shortcut and the fused tail on k_conv3_f32) against the same network with every
+    conv on the per-tap kernel."""
+    from red_diffeq import _hip
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(6)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(cuda).eval()
+    x = torch.randn(25, 1, 72, 72, device=cuda).clamp(-1, 1)
+    t = torch.randint(0, 1000, (25,), device=cuda)
+    with torch.no_grad():
+        y = net(x, t)
+        old = _hip.lib().rdq_unet_set_option(4, 0)
+        try:
+            net.__dict__.pop("_graphs", None)
+            ref = net(x, t)
+        finally:
+            _hip.lib().rdq_unet_set_option(4, old)
+    close(y, ref, rel=2e-5)
+
+
 # Block.forward on the bf16 halo-staged conv with the GroupNorm statistics in its epilogue
 # (rdq_conv2d_bf16_gn_silu, the configs[4] batched U-Net) vs the same conv, its output rounded to bf16
 # (the fused path holds the raw conv output as bf16), followed by the separate GroupNorm pass: the

@@ -1,7 +1,8 @@
-"""A/B of the halo-staged 3x3 conv's least tile count (rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES)):
-times the bf16 U-Net forward (dim 64, mults 1,2,4,8, 72x72) for each threshold and reports the output
-difference against the first threshold listed.
-python tools/conv3_threshold_ab.py [--B 344] [--min-tiles 512 384 256 128] [--reps 10]"""
+"""A/B of the halo-staged 3x3 convs' options: least tile count of the bf16 kernel
+(RDQ_UNET_OPT_CONV3_MIN_TILES), raw conv output held as bf16 (RDQ_UNET_OPT_BF16_RAW) and least tile count
+of the fp32 kernel (RDQ_UNET_OPT_CONV3F_MIN_TILES, 0 = off); times the U-Net forward (dim 64, mults
+1,2,4,8, 72x72) for each combination and reports the output difference against the first one.
+python tools/conv3_threshold_ab.py [--B 344] [--precision bf16] [--min-tiles 512 128] [--f32-min-tiles 0 128]"""
 import argparse
 import json
 import os
@@ -16,6 +17,7 @@ from red_diffeq.models.diffusion import Unet  # noqa: E402
 
 OPT_CONV3_MIN_TILES = 2
 OPT_BF16_RAW = 3
+OPT_CONV3F_MIN_TILES = 4
 
 
 def main():
@@ -25,20 +27,23 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bf16-raw", type=int, nargs="+", default=[1],
                     help="RDQ_UNET_OPT_BF16_RAW values to A/B (raw conv output held as bf16 or fp32)")
+    ap.add_argument("--f32-min-tiles", type=int, nargs="+", default=[128])
+    ap.add_argument("--precision", default="bf16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(dev).eval()
-    net.set_precision("bf16")
+    net.set_precision(a.precision)
     lib = _hip.lib()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for B in a.B:
         x = torch.randn(B, 1, 72, 72, device=dev).clamp(-1, 1)
         t = torch.randint(0, 1000, (B,), device=dev)
         base = None
-        for mt, raw in [(m, r) for m in a.min_tiles for r in a.bf16_raw]:
+        for mt, raw, ft in [(m, r, f) for m in a.min_tiles for r in a.bf16_raw for f in a.f32_min_tiles]:
             net.__dict__.pop("_graphs", None)          # small batches replay a captured graph: recapture
             old_raw = lib.rdq_unet_set_option(OPT_BF16_RAW, raw)
+            old_ft = lib.rdq_unet_set_option(OPT_CONV3F_MIN_TILES, ft)
             old = lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, mt)
             assert old > 0
             try:
@@ -56,10 +61,11 @@ def main():
             finally:
                 lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, old)
                 lib.rdq_unet_set_option(OPT_BF16_RAW, old_raw)
+                lib.rdq_unet_set_option(OPT_CONV3F_MIN_TILES, old_ft)
             if base is None:
                 base = y.clone()
             d = ((y - base).abs().max() / base.abs().max()).item()
-            print(json.dumps({"B": B, "min_tiles": mt, "bf16_raw": raw, "ms_median": round(sorted(ts)[len(ts) // 2], 3),
+            print(json.dumps({"B": B, "precision": a.precision, "min_tiles": mt, "bf16_raw": raw, "f32_min_tiles": ft, "ms_median": round(sorted(ts)[len(ts) // 2], 3),
                               "ms_min": round(min(ts), 3), "rel_diff_vs_first": d}), flush=True)
 
 
