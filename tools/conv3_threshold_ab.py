@@ -23,13 +23,18 @@ OPT_CONV3F_MIN_TILES = 4
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, nargs="+", default=[344])
-    ap.add_argument("--min-tiles", type=int, nargs="+", default=[512, 384, 256, 128])
+    ap.add_argument("--min-tiles", type=int, nargs="+", default=[64])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bf16-raw", type=int, nargs="+", default=[1],
                     help="RDQ_UNET_OPT_BF16_RAW values to A/B (raw conv output held as bf16 or fp32)")
-    ap.add_argument("--f32-min-tiles", type=int, nargs="+", default=[128])
+    ap.add_argument("--f32-min-tiles", type=int, nargs="+", default=[-1], help="-1: the library default")
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--fused-la-f32", default=None, choices=["auto", "on", "off"],
+                    help="unet_ops.FUSED_LA_F32 for this run (default: the module's)")
     a = ap.parse_args()
+    if a.fused_la_f32:
+        from red_diffeq.models import unet_ops
+        unet_ops.FUSED_LA_F32 = {"auto": None, "on": True, "off": False}[a.fused_la_f32]
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(dev).eval()
@@ -43,7 +48,8 @@ def main():
         for mt, raw, ft in [(m, r, f) for m in a.min_tiles for r in a.bf16_raw for f in a.f32_min_tiles]:
             net.__dict__.pop("_graphs", None)          # small batches replay a captured graph: recapture
             old_raw = lib.rdq_unet_set_option(OPT_BF16_RAW, raw)
-            old_ft = lib.rdq_unet_set_option(OPT_CONV3F_MIN_TILES, ft)
+            old_ft = lib.rdq_unet_set_option(OPT_CONV3F_MIN_TILES, 0)
+            lib.rdq_unet_set_option(OPT_CONV3F_MIN_TILES, old_ft if ft < 0 else ft)
             old = lib.rdq_unet_set_option(OPT_CONV3_MIN_TILES, mt)
             assert old > 0
             try:

@@ -1,7 +1,8 @@
 """Per-shape timing of the U-Net's convolutions (dim 64, 72x72): each shape's op captured back to
 back in a hipGraph, replayed, device time per call and TFLOP/s against the fp32 matrix peak, or with
 --bf16 (the configs[4] batch: --B 344) against the bf16 dense peak.
-python tools/conv_micro.py [--only NAME] [--reps R] [--B B ...] [--bf16] [--inner N]"""
+python tools/conv_micro.py [--only NAME] [--reps R] [--B B ...] [--bf16] [--inner N] [--f32-min-tiles T ...]
+(--f32-min-tiles: rdq_unet_set_option(RDQ_UNET_OPT_CONV3F_MIN_TILES) values to compare; 0 = per-tap only)"""
 import argparse
 import json
 import os
@@ -11,7 +12,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "red-diffeq_amd"))
-from red_diffeq import ops  # noqa: E402
+from red_diffeq import _hip, ops  # noqa: E402
 
 # name: (cin1, cin2, cout, k, H, mode)
 SHAPES = {
@@ -65,8 +66,18 @@ if __name__ == "__main__":
     ap.add_argument("--B", type=int, nargs="+", default=[1])
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--inner", type=int, default=20)
+    ap.add_argument("--f32-min-tiles", type=int, nargs="+", default=[None])
     a = ap.parse_args()
     names = [a.only] if a.only else list(SHAPES)
     for B in a.B:
         for n in names:
-            print(json.dumps(run(n, B, a.reps, a.inner, a.bf16)), flush=True)
+            for ft in a.f32_min_tiles:
+                old = None if ft is None else _hip.lib().rdq_unet_set_option(4, ft)
+                try:
+                    r = run(n, B, a.reps, a.inner, a.bf16)
+                finally:
+                    if old is not None:
+                        _hip.lib().rdq_unet_set_option(4, old)
+                if ft is not None:
+                    r["f32_min_tiles"] = ft
+                print(json.dumps(r), flush=True)
