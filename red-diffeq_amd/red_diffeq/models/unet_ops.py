@@ -200,12 +200,19 @@ def rms_conv(x, norm, conv):
     return conv2d(rmsnorm(x, norm.g), conv)
 
 
-# fp32 LinearAttention in the two-launch form (rdq_linear_attention_f32) where it applies; default off:
-# measured slower where the fp32 path runs (B = 1: the U-Net 1.20 -> 1.65 ms, the chunk combine and one
-# L1 weight load per fp32 MFMA step dominate; B = 25: 7.82 -> 7.64 ms, 72 x 72 blocks 230 -> 277 us,
-# 36 / 18 faster).  The three-launch form (rms_conv + context + output projection) stays the default;
-# tests compare the two.
-FUSED_LA_F32 = False
+# fp32 LinearAttention in the two-launch form (rdq_linear_attention_f32): True / False force it, None
+# (default) takes it for the dim-64 blocks of batches of >= 16 (tools/la_f32_ab.py, one block per
+# replayed graph: dim 64 at 72 x 72 B = 25 465 -> 348 us, B = 100 1767 -> 1121 us, 36 x 36 149 -> 131 /
+# 487 -> 349 us; slower at B = 1 (47 -> 81 us: the chunk combine and one L1 weight load per fp32 MFMA
+# step) and for dim 128 at every batch measured).  Otherwise the three-launch form (rms_conv + context +
+# output projection); tests compare the two.
+FUSED_LA_F32 = None
+
+
+def _fused_la_f32(x):
+    if FUSED_LA_F32 is not None:
+        return FUSED_LA_F32
+    return x.shape[1] == 64 and x.shape[0] >= 16
 
 
 def linear_attention(x, m):
@@ -215,8 +222,8 @@ def linear_attention(x, m):
         # the whole block in two launches, qkv and the hidden tensor never written (rdq_linear_attention_bf16)
         return torch.ops.red_diffeq.linear_attn_bf16(x, m.norm.g, m.to_qkv.weight, m.mem_kv, conv.weight, conv.bias,
                                                      m.to_out[1].g, m.heads, float(m.scale))
-    if _PREC["mode"] == "fp32" and FUSED_LA_F32 and ops.linear_attn_bf16_fusable(x, m.to_qkv.weight, conv.weight,
-                                                                                 m.heads):
+    if _PREC["mode"] == "fp32" and _fused_la_f32(x) and ops.linear_attn_bf16_fusable(x, m.to_qkv.weight,
+                                                                                      conv.weight, m.heads):
         # the same two-launch block on fp32 MFMA (rdq_linear_attention_f32)
         return torch.ops.red_diffeq.linear_attn_f32(x, m.norm.g, m.to_qkv.weight, m.mem_kv, conv.weight, conv.bias,
                                                     m.to_out[1].g, m.heads, float(m.scale))

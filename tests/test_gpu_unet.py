@@ -311,9 +311,11 @@ def test_linear_attention_f32_fused_vs_unfused(cuda, C, H, B):
         m.to_out[0].bias.normal_(0, 0.1)
     x = torch.randn(B, C, H, H, device=cuda)
     with torch.no_grad():
-        unf = ops.linear_attention(x, m)
-        old, ops.FUSED_LA_F32 = ops.FUSED_LA_F32, True
+        old = ops.FUSED_LA_F32
         try:
+            ops.FUSED_LA_F32 = False
+            unf = ops.linear_attention(x, m)
+            ops.FUSED_LA_F32 = True
             got = ops.linear_attention(x, m)
         finally:
             ops.FUSED_LA_F32 = old
