@@ -489,8 +489,9 @@ def test_conv3_f32_halo_staged(cuda, cin1, cin2, cout, H, B, mode, res):
 
 def test_unet_fp32_halo_conv_batched(cuda):
     """The fp32 U-Net at the reference's openfwi batch (B = 25: its 72 x 72 and 36 x 36 Blocks, the
-    up path's block1 + shortcut and the fused tail on k_conv3_f32) against the same network with every
-    conv on the per-tap kernel."""
+    up path's block1 + shortcut and the fused tail on k_conv3_f32, the fused fp32 LinearAttention of
+    the dim-64 blocks) against the same network with every conv on the per-tap kernel, and against the
+    plain PyTorch fp32 restatement (tests/unet_torch_ref.py; TF32 off)."""
     from red_diffeq import _hip
     from red_diffeq.models.diffusion import Unet
     torch.manual_seed(6)
@@ -505,7 +506,15 @@ def test_unet_fp32_halo_conv_batched(cuda):
             ref = net(x, t)
         finally:
             _hip.lib().rdq_unet_set_option(4, old)
-    close(y, ref, rel=2e-5)
+    close(y, ref, rel=2e-5, what="halo vs per-tap network")
+    tf32 = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = False
+    try:
+        with torch.no_grad():
+            ref_torch = R.unet_forward(net, x, t)
+    finally:
+        torch.backends.cudnn.allow_tf32 = tf32
+    close(y, ref_torch, rel=2e-5, what="vs torch fp32")
 
 
 # Block.forward on the bf16 halo-staged conv with the GroupNorm statistics in its epilogue
