@@ -2506,7 +2506,9 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
 template <int MODE, bool IN8 = false>
 __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 {
-    __shared__ __attribute__((aligned(16))) __bf16 Hs[2][C3_ROWS][BF_LD];     // 2 x 31.4 KiB
+    // row C3_ROWS of each buffer stays zero: a lane whose tap leaves the image reads it (one address
+    // select per tap instead of zeroing the fragment's four registers per k step)
+    __shared__ __attribute__((aligned(16))) __bf16 Hs[2][C3_ROWS + 1][BF_LD];     // 2 x 31.5 KiB
     __shared__ __attribute__((aligned(16))) __bf16 Ws[2][C3_BN][BF_LD];
     const rdq_conv_desc &d = a.d;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2541,23 +2543,30 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
         v = *reinterpret_cast<const bf16x8 *>(a.x8 + o);
         return ok;
     };
-    auto hload = [&](int k, int cc, float (&v)[8]) -> bool {
-        const unsigned s = it_src[k];
-        const int c = cc * BF_BK + 8 * wv;
+    // (fp32 input) the chunk's 8-channel group of the wave through a buffer resource on its first
+    // channel plane: the item's sample / pixel offset in a VGPR, the channel j's plane offset in the
+    // SGPR soffset (no per-load address arithmetic); an item outside the image, or channels past
+    // cin, get an offset past the resource and load zeros (no per-element select)
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    auto hsrc = [&](int cc, unsigned &cstride, bool &cok) -> __amdgpu_buffer_rsrc_t {
+        const int c = cc * BF_BK + 8 * wvu;
         const bool lo = c < d.cin1;
-        const float *__restrict__ base = lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
-        const unsigned cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane;
-        const bool ok = s != ~0u && c < cin;
-        const unsigned o = ok ? (s >> 20) * cstride + (s & 0xfffff) : 0u;
-        if (c >= cin) base = a.x;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = base[o + (unsigned)(j * a.plane)];
-        return ok;
+        cok = c < cin;
+        cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane * 4u;
+        const float *base = !cok ? a.x : lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, 0x7fffffff, 0x00020000);
     };
-    auto hpack = [&](const float (&v)[8], bool ok) -> bf16x8 {
+    auto hload = [&](int k, const __amdgpu_buffer_rsrc_t &rs, unsigned cstride, bool cok, float (&v)[8]) {
+        const unsigned s = it_src[k];
+        const int vo = (s != ~0u && cok) ? (int)((s >> 20) * cstride + (s & 0xfffff) * 4u) : (int)0x80000000u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * a.plane * 4, 0));
+    };
+    auto hpack = [&](const float (&v)[8]) -> bf16x8 {
         bf16x8 h;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) h[j] = (__bf16)(ok ? v[j] : 0.0f);
+        for (int j = 0; j < 8; ++j) h[j] = (__bf16)v[j];
         return h;
     };
     auto hstore = [&](int buf, int k, const bf16x8 &h) {
@@ -2604,12 +2613,15 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
         for (int k = 0; k < C3_NI; ++k) hstore(0, k, ok[k] ? v[k] : bf16x8{});
     } else {
         float v[C3_NI][8];
-        bool ok[C3_NI];
+        unsigned cs;
+        bool cok;
+        const __amdgpu_buffer_rsrc_t rs = hsrc(0, cs, cok);
 #pragma unroll
-        for (int k = 0; k < C3_NI; ++k) ok[k] = hload(k, 0, v[k]);
+        for (int k = 0; k < C3_NI; ++k) hload(k, rs, cs, cok, v[k]);
 #pragma unroll
-        for (int k = 0; k < C3_NI; ++k) hstore(0, k, hpack(v[k], ok[k]));
+        for (int k = 0; k < C3_NI; ++k) hstore(0, k, hpack(v[k]));
     }
+    if (tid < 2 * BF_LD / 8) reinterpret_cast<bf16x8 *>(&Hs[tid / (BF_LD / 8)][C3_ROWS][0])[tid % (BF_LD / 8)] = bf16x8{};
     // weight ring: three taps in registers; tap s is fetched at tap s - 3 into the slot tap s - 3 left
     // (stashed at the end of tap s - 4) and stashed at the end of tap s - 1: two taps of latency
     bf16x8 wr[3];
@@ -2629,6 +2641,10 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
         bf16x8 hv8[IN8 ? 6 : 1];
         bool hok[6];
         const int hb = cc & 1;
+        unsigned ncs = 0;
+        bool ncok = false;
+        __amdgpu_buffer_rsrc_t nrs;
+        if constexpr (PF && !IN8) nrs = hsrc(cc + 1, ncs, ncok);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int s = cc * 9 + t;
@@ -2638,27 +2654,27 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
                 for (int k = 0; k < C3_NI; ++k)
                     if (IT[k] + 4 == t) {
                         if constexpr (IN8) hstore(hb ^ 1, k, hok[k % 6] ? hv8[k % 6] : bf16x8{});
-                        else hstore(hb ^ 1, k, hpack(hv[k % 6], hok[k % 6]));
+                        else hstore(hb ^ 1, k, hpack(hv[k % 6]));
                     }
 #pragma unroll
                 for (int k = 0; k < C3_NI; ++k)
                     if (IT[k] == t) {
                         if constexpr (IN8) hok[k % 6] = hload8(k, cc + 1, hv8[k % 6]);
-                        else hok[k % 6] = hload(k, cc + 1, hv[k % 6]);
+                        else hload(k, nrs, ncs, ncok, hv[k % 6]);
                     }
             }
             const int toff = (t / 3) * d.W + t % 3;
             const __bf16 *wsb = &Ws[s & 1][0][0];
+            int hrow[2];
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) hrow[mb] = ((tmask[mb] >> t) & 1u) ? pl[mb] + toff : C3_ROWS;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const int kk = 16 * ks + kh;
                 bf16x8 bfr[2], afr[2];
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb) {
-                    bf16x8 v = *reinterpret_cast<const bf16x8 *>(&Hs[hb][pl[mb] + toff][kk]);
-                    if (!((tmask[mb] >> t) & 1u)) v = bf16x8{};
-                    bfr[mb] = v;
-                }
+                for (int mb = 0; mb < 2; ++mb)
+                    bfr[mb] = *reinterpret_cast<const bf16x8 *>(&Hs[hb][hrow[mb]][kk]);
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
                     afr[c] = *reinterpret_cast<const bf16x8 *>(wsb + (c * 32 + (lane & 31)) * BF_LD + kk);
@@ -2694,7 +2710,7 @@ constexpr int C3F_BK = 16, C3F_NI = 4, C3F_LD = 20;
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
 {
-    __shared__ __attribute__((aligned(16))) float Hs[2][C3_ROWS][C3F_LD];    // 2 x 31.4 KiB
+    __shared__ __attribute__((aligned(16))) float Hs[2][C3_ROWS + 1][C3F_LD];    // + a zero row (k_conv3_bf16)
     __shared__ __attribute__((aligned(16))) float Ws[2][C3_BN][C3F_LD];
     const rdq_conv_desc &d = a.d;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2716,25 +2732,29 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
         }
         it_src[k] = in ? ((unsigned)b << 20 | (unsigned)pix) : ~0u;
     }
-    auto hload = [&](int k, int cc, float (&v)[8]) -> bool {
-        const unsigned s = it_src[k];
-        const int c = cc * C3F_BK + 8 * ho;
+    // the octet's channels through a buffer resource on its first plane, as k_conv3_bf16's gather
+    const int hou = __builtin_amdgcn_readfirstlane(ho);
+    auto hsrc = [&](int cc, unsigned &cstride, bool &cok) -> __amdgpu_buffer_rsrc_t {
+        const int c = cc * C3F_BK + 8 * hou;
         const bool lo = c < d.cin1;
-        const float *__restrict__ base = lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
-        const unsigned cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane;
-        const bool ok = s != ~0u && c < cin;
-        const unsigned o = ok ? (s >> 20) * cstride + (s & 0xfffff) : 0u;
-        if (c >= cin) base = a.x;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = base[o + (unsigned)(j * a.plane)];
-        return ok;
+        cok = c < cin;
+        cstride = (unsigned)(lo ? d.cin1 : d.cin2) * (unsigned)a.plane * 4u;
+        const float *base = !cok ? a.x : lo ? a.x + (size_t)c * a.plane : a.x2 + (size_t)(c - d.cin1) * a.plane;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, 0x7fffffff, 0x00020000);
     };
-    auto hstore = [&](int buf, int k, const float (&v)[8], bool ok) {
+    auto hload = [&](int k, const __amdgpu_buffer_rsrc_t &rs, unsigned cstride, bool cok, float (&v)[8]) {
+        const unsigned s = it_src[k];
+        const int vo = (s != ~0u && cok) ? (int)((s >> 20) * cstride + (s & 0xfffff) * 4u) : (int)0x80000000u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, j * a.plane * 4, 0));
+    };
+    auto hstore = [&](int buf, int k, const float (&v)[8]) {
         const int q = lane + 64 * (2 * k + (wv >> 1));
         if (q < a.R) {
             float4 *dst = reinterpret_cast<float4 *>(&Hs[buf][q][8 * ho]);
-            dst[0] = ok ? float4{v[0], v[1], v[2], v[3]} : float4{0.0f, 0.0f, 0.0f, 0.0f};
-            dst[1] = ok ? float4{v[4], v[5], v[6], v[7]} : float4{0.0f, 0.0f, 0.0f, 0.0f};
+            dst[0] = float4{v[0], v[1], v[2], v[3]};
+            dst[1] = float4{v[4], v[5], v[6], v[7]};
         }
     };
     // weight role: row wn (of 64), channels wq .. wq + 3 of the chunk (cin % 8 == 0: all four inside or
@@ -2772,12 +2792,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
         for (int mb = 0; mb < 2; ++mb) acc[c][mb] = f32x16{};
     {   // chunk 0's halo
         float v[C3F_NI][8];
-        bool ok[C3F_NI];
+        unsigned cs;
+        bool cok;
+        const __amdgpu_buffer_rsrc_t rs = hsrc(0, cs, cok);
 #pragma unroll
-        for (int k = 0; k < C3F_NI; ++k) ok[k] = hload(k, 0, v[k]);
+        for (int k = 0; k < C3F_NI; ++k) hload(k, rs, cs, cok, v[k]);
 #pragma unroll
-        for (int k = 0; k < C3F_NI; ++k) hstore(0, k, v[k], ok[k]);
+        for (int k = 0; k < C3F_NI; ++k) hstore(0, k, v[k]);
     }
+    if (tid < 2 * C3F_LD / 4)
+        reinterpret_cast<float4 *>(&Hs[tid / (C3F_LD / 4)][C3_ROWS][0])[tid % (C3F_LD / 4)] = float4{0.0f, 0.0f, 0.0f, 0.0f};
     float4 wr[3];
     wr[0] = wload(0, 0);
     wr[1] = wload(0, 1);
@@ -2788,28 +2812,30 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
     auto chunk = [&](int cc, auto pf) {
         constexpr bool PF = decltype(pf)::value;
         float hv[C3F_NI][8];
-        bool hok[C3F_NI];
         const int hb = cc & 1;
+        unsigned ncs = 0;
+        bool ncok = false;
+        __amdgpu_buffer_rsrc_t nrs;
+        if constexpr (PF) nrs = hsrc(cc + 1, ncs, ncok);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int s = cc * 9 + t;
             wr[t % 3] = wload(min(cc + (t + 3) / 9, a.cch - 1), (t + 3) % 9);
             if constexpr (PF) {
-                if (t >= 4 && t < 4 + C3F_NI) hstore(hb ^ 1, t - 4, hv[t - 4], hok[t - 4]);
-                if (t < C3F_NI) hok[t] = hload(t, cc + 1, hv[t]);
+                if (t >= 4 && t < 4 + C3F_NI) hstore(hb ^ 1, t - 4, hv[t - 4]);
+                if (t < C3F_NI) hload(t, nrs, ncs, ncok, hv[t]);
             }
             const int toff = (t / 3) * d.W + t % 3;
             const float *wsb = &Ws[s & 1][0][0];
+            int hrow[2];
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) hrow[mb] = ((tmask[mb] >> t) & 1u) ? pl[mb] + toff : C3_ROWS;
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
                 const int kk = 8 * q2 + kg;
                 float4 bfr[2], afr[2];
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb) {
-                    float4 v = *reinterpret_cast<const float4 *>(&Hs[hb][pl[mb] + toff][kk]);
-                    if (!((tmask[mb] >> t) & 1u)) v = float4{0.0f, 0.0f, 0.0f, 0.0f};
-                    bfr[mb] = v;
-                }
+                for (int mb = 0; mb < 2; ++mb) bfr[mb] = *reinterpret_cast<const float4 *>(&Hs[hb][hrow[mb]][kk]);
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
                     afr[c] = *reinterpret_cast<const float4 *>(wsb + (c * 32 + (lane & 31)) * C3F_LD + kk);
@@ -3291,9 +3317,9 @@ static int64_t conv3_tiles(const rdq_conv_desc *d)
     if (d->cin1 % 8 || d->cin2 % 8 || d->cout % C3_BN || d->W > C3_WMAX || d->B >= 4096) return false;
     const int64_t HW = (int64_t)d->H * d->W, M = d->B * HW;
     if (HW >= (1 << 20) || M >= (int64_t)1 << 30) return false;
-    // the halo gather addresses each input tensor with 32-bit element offsets
+    // the halo gather addresses each input tensor with 31-bit byte offsets (buffer loads)
     const int64_t plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? HW / 4 : HW;
-    if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane >= (int64_t)1 << 32) return false;
+    if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane * 4 >= (int64_t)1 << 31) return false;
     return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN);
 }
 bool conv3_ok(const rdq_conv_desc *d) { return conv3_tiles(d) >= C3_MIN_TILES; }
