@@ -3006,6 +3006,11 @@ template <int D, bool F = false> struct LbOcc {      // (F: fp32 staging, LDS-bo
 
 // F: the fp32 form (the reference's arithmetic, small batches): the same structure on
 // v_mfma_f32_32x32x2_f32 (k index of lane group g = g: one float per lane and k-step), fp32 staging
+// softmax exponentials of the LinearAttention kernels: the bf16 form rounds its operands to bf16
+// anyway, so it takes the hardware exp2 (v_exp_f32 after a scale by log2 e) instead of expf's
+// range-reduced evaluation; the fp32 form keeps expf (the reference's precision)
+template <bool F> __device__ __forceinline__ float lab_exp(float x) { return F ? expf(x) : __expf(x); }
+
 template <int D, bool F = false>
 __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_kv(LabArgs a)
 {
@@ -3069,12 +3074,12 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_kv(LabArgs a)
             }
             tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
             const float mnew = fmaxf(mrun, tmax);
-            const float f = mrun == -INFINITY ? 0.0f : expf(mrun - mnew);
+            const float f = mrun == -INFINITY ? 0.0f : lab_exp<F>(mrun - mnew);
             mrun = mnew;
             float ps = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float e = kt[r] == -INFINITY ? 0.0f : expf(kt[r] - mnew);
+                const float e = kt[r] == -INFINITY ? 0.0f : lab_exp<F>(kt[r] - mnew);
                 kt[r] = e;
                 ps += e;
             }
@@ -3136,14 +3141,14 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
         for (int c = 0; c < a.nch; ++c) {
             const float *pc = pb0 + (size_t)c * LB_PART;
             const float mc = pc[d];
-            const float f = mc == -INFINITY ? 0.0f : expf(mc - M);
+            const float f = mc == -INFINITY ? 0.0f : lab_exp<F>(mc - M);
             den += f * pc[LB_DH + d];
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] += f * pc[2 * LB_DH + lb_row(r, g) * LB_DH + d];
         }
         const float *mv = a.mem + (size_t)(1 * LB_HEADS + h) * LB_DH * a.nmem;
         for (int j = 0; j < a.nmem; ++j) {
-            const float e = expf(mk[j] - M);
+            const float e = lab_exp<F>(mk[j] - M);
             den += e;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] += e * mv[(size_t)lb_row(r, g) * a.nmem + j];
@@ -3216,7 +3221,7 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
             mx = fmaxf(mx, __shfl_xor(mx, 32));
             float sm = 0.0f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) { q[r] = expf(q[r] - mx); sm += q[r]; }
+            for (int r = 0; r < 16; ++r) { q[r] = lab_exp<F>(q[r] - mx); sm += q[r]; }
             sm += __shfl_xor(sm, 32);
             const float inv = 1.0f / sm;
             f32x16 hid = {};
