@@ -322,15 +322,39 @@ def unet_rate(dev, reps=20):
             "mfma_frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
 
 
+def unet_rate_batched(dev, B=25, reps=10):
+    """The U-Net forward at configs/openfwi/red-diffeq.yaml's batch (B = 25 tiles of 72 x 72, fp32):
+    ms per forward (module call), conv TFLOP/s and the fraction of the fp32 matrix peak."""
+    from red_diffeq.models.diffusion import Unet
+    torch.manual_seed(0)
+    net = Unet(dim=64, dim_mults=(1, 2, 4, 8), channels=1).to(dev).eval()
+    x = torch.randn(B, 1, 72, 72, device=dev).clamp(-1, 1)
+    t = torch.randint(0, 1000, (B,), device=dev)
+    with torch.no_grad():
+        for _ in range(2):
+            net(x, t)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            net(x, t)
+        e1.record()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tfs = B * UNET_GFLOP_72 / (ms * 1e-3) / 1e3
+    return {"workload": f"U-Net eps-predictor, dim 64, 72x72, B={B}, fp32 (openfwi yaml batch)", "ms": round(ms, 4),
+            "conv_tflops": round(tfs, 2), "mfma_frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
+
+
 def conv_class_rates(dev, reps=10, inner=20):
-    """fp32 conv classes of the U-Net (MFMA k_conv_cc) at B = 1 (the loop) and B = 8 (batched
-    patches): device time per launch from a hipGraph of `inner` back-to-back launches (launch gaps
-    included), TFLOP/s and the fraction of the fp32 matrix peak."""
+    """fp32 conv classes of the U-Net at B = 1 (the loop; per-tap k_conv_cc), B = 8 and B = 25 (the
+    openfwi yaml batch; the 72 x 72 classes on the halo-staged k_conv3_f32 there): device time per
+    launch from a hipGraph of `inner` back-to-back launches (launch gaps included), TFLOP/s and the
+    fraction of the fp32 matrix peak."""
     shapes = {"l72_3x3_64to64": (64, 0, 64, 72), "l72_3x3_cat128to64": (64, 64, 64, 72),
               "l9_3x3_512to512": (512, 0, 512, 9)}
     out = {}
     for name, (c1, c2, co, H) in shapes.items():
-        for B in (1, 8):
+        for B in (1, 8, 25):
             g = torch.Generator(device=dev).manual_seed(0)
             x = torch.randn(B, c1, H, H, device=dev, generator=g)
             x2 = torch.randn(B, c2, H, H, device=dev, generator=g) if c2 else None
@@ -542,6 +566,7 @@ def main():
     if world == 1 and not a.no_red:
         out["unet"] = unet_rate(dev)
         out["unet"]["conv_classes"] = conv_class_rates(dev)
+        out["unet"]["batched_b25"] = unet_rate_batched(dev)
         out["configs2_red_loop"] = {"workload": "configs[2]: OpenFWI CurveVel-A 70x70, 32 shots, full RED-DiffEq "
                                                 "loop (fwd+adj + U-Net regulariser + Adam + metrics), random-init U-Net",
                                     "ms_per_iter": red_loop_wallclock(dev, a),
