@@ -2374,13 +2374,18 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
     // epilogue: the bias and residual of all 64 outputs of the lane are loaded before the first
     // store (gfx9 retires stores and loads in one in-order count: a load issued after a store would
     // wait for it), then every output is formed, then stored
-    int ob[2], opix[2];
+    // outputs, residual and bias go through buffer resources: the lane's part of an element offset
+    // (sample, its channel quad, pixel) is one VGPR per m block, the rest (the register's channel)
+    // the SGPR soffset; rows past the image get an out-of-range offset (stores dropped, loads 0)
+    int vo[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
-        const int mc = min(m0 + pl[mb], a.M - 1);
-        ob[mb] = mc / a.HW;
-        opix[mb] = mc - ob[mb] * a.HW;
+        const int m = m0 + pl[mb];
+        const int ob = m / a.HW, opix = m - ob * a.HW;
+        vo[mb] = m < a.M ? (ob * d.cout + 4 * (lane >> 5)) * a.HW + opix : -1;
     }
+    auto soff = [&](int c, int r) { return (n0 + c * 32 + (r & 3) + 8 * (r >> 2)) * a.HW; };
+    constexpr int OOB = (int)0x80000000u;
     float bv[2][16] = {}, rv[2][2][16] = {};
     if (a.bias) {                       // (conditions hoisted: a per-element "load or 0" would make
 #pragma unroll                          //  the compiler branch and wait around every load)
@@ -2389,14 +2394,16 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
             for (int r = 0; r < 16; ++r) bv[c][r] = a.bias[n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
     }
     if (a.res) {
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.res), (short)0,
+                                                                            0x7fffffff, 0x00020000);
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            for (int r = 0; r < 16; ++r)
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb) rv[mb][c][r] = a.res[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]];
-            }
+                for (int mb = 0; mb < 2; ++mb)
+                    rv[mb][c][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rr, vo[mb] < 0 ? OOB : vo[mb] * 4, soff(c, r) * 4, 0));
     }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -2408,35 +2415,30 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
                 asm volatile("" : "+v"(acc[c][mb][r]));
             }
     if (a.yb) {
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.yb, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[c][mb][r] = (float)(__bf16)acc[c][mb][r];
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            if (m0 + pl[mb] >= a.M) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    a.yb[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = (__bf16)acc[c][mb][r];
+                    const __bf16 h = (__bf16)acc[c][mb][r];
+                    acc[c][mb][r] = (float)h;
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), ry,
+                                                          vo[mb] < 0 ? OOB : vo[mb] * 2, soff(c, r) * 2, 0);
                 }
-        }
     } else {
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            if (m0 + pl[mb] >= a.M) continue;
+        for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + c * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    a.y[((size_t)ob[mb] * d.cout + n) * a.HW + opix[mb]] = acc[c][mb][r];
+                    const float v = acc[c][mb][r];     // (a bit_cast of the vector element itself stored
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry,   //  element 0 every time)
+                                                          vo[mb] < 0 ? OOB : vo[mb] * 4, soff(c, r) * 4, 0);
                 }
-        }
     }
     if (!a.gnp) return;
     // GroupNorm statistics of the tile's outputs (for k_gn_apply_t with bm = C3_BM; HW >= C3_BM so a
@@ -3325,6 +3327,7 @@ static int64_t conv3_tiles(const rdq_conv_desc *d)
     // the halo gather addresses each input tensor with 31-bit byte offsets (buffer loads)
     const int64_t plane = d->in_mode == RDQ_IN_UPSAMPLE2 ? HW / 4 : HW;
     if ((int64_t)d->B * std::max(d->cin1, d->cin2) * plane * 4 >= (int64_t)1 << 31) return false;
+    if (M * d->cout * 4 >= (int64_t)1 << 31) return false;     // output / residual: the same, epilogue
     return (M + C3_BM - 1) / C3_BM * (d->cout / C3_BN);
 }
 bool conv3_ok(const rdq_conv_desc *d) { return conv3_tiles(d) >= C3_MIN_TILES; }
