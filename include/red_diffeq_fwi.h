@@ -74,8 +74,9 @@ int rdq_fwi_sizes(const rdq_fwi_plan *plan, int32_t B, rdq_fwi_sizes_t *out);
 /* 1 = capture each time loop into a cached hipGraph (default), 0 = direct launches. */
 int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
 /* Time steps advanced per launch by the forward / adjoint kernels (temporal blocking depth,
- * 1..4) and the number of concurrent shot-group launch chains (1..16).  Results are identical
- * for every setting; only speed changes. */
+ * 1..4; the wide chunked adjoint has its own depth, rdq_fwi_set_wide_adj_steps) and the number of
+ * concurrent shot-group launch chains (1..16).  Results are identical for every setting; only speed
+ * changes. */
 int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
 /* Kernel variant flags (a new plan starts at RDQ_VARIANT_FWD_GEN):
  *   RDQ_VARIANT_FWD_GEN    the chunked forward regenerates alpha/temp1/temp2 from the model in
@@ -94,12 +95,24 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
  *                          with L2-resident hand-offs (identical results; slower);
  *   RDQ_VARIANT_NARROW_CHUNKED the chunked (non-resident) kernels run 64-column regions, one column
  *                          per lane, instead of 128-column regions of two columns per lane
- *                          (identical results; more halo traffic). */
+ *                          (identical results; more halo traffic);
+ *   RDQ_VARIANT_CHUNKED_ADJ_FMA the wide chunked adjoint contracts its stencils into FMAs (about 4 %
+ *                          faster at configs[4]; dL/dv within ~2e-5 of the oracle, the sponge sum gk,
+ *                          a difference of nearly equal adjoint levels, within ~1.3e-4).  Without it
+ *                          (default) the chunked adjoint keeps the oracle's exact order: gA / gbeta
+ *                          bit-identical, gk to fp64 summation order.  Ignored when
+ *                          RDQ_VARIANT_ADJ_EXACT is set or nbc < 20. */
 #define RDQ_VARIANT_FWD_GEN 1
 #define RDQ_VARIANT_ADJ_EXACT 2
 #define RDQ_VARIANT_NO_XCD_LOCAL 4
 #define RDQ_VARIANT_NARROW_CHUNKED 8
+#define RDQ_VARIANT_CHUNKED_ADJ_FMA 16
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
+/* Time steps per launch of the WIDE chunked adjoint (k_adj_tw, 1..6; default 6: 167 launches at
+ * configs[4]'s nt instead of 250 at 4).  rdq_fwi_set_tuning's adj_steps sets the persistent and the
+ * narrow chunked adjoints' depth only.  A time loop whose nt is not a multiple of the depth ends with
+ * one shorter launch of its own depth.  Results are identical for every depth. */
+int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *plan, int32_t steps);
 /* Rows per wave of the 64 x 96-region persistent kernels: forward 6, 8, 12 or 24 (16, 12, 8 or 4
  * waves per workgroup), adjoint (FMA build) 6, 8 or 12.  Same region geometry and results.  The time
  * step is latency-bound, so more resident waves win (configs[1], tools/ab_rw.sh, tools/ab_adj_nb6.sh):

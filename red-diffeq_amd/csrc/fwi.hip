@@ -547,6 +547,8 @@ __global__ __launch_bounds__(64 * TB_NW) void k_fwd_tb(FwdTBArgs a)
     }
 }
 
+constexpr int TW_ADJ_MAXT = 6;          // deepest wide chunked adjoint (k_adj_tw instantiations 1 .. 6)
+constexpr int ADJ_W_MAX = TW_ADJ_MAXT > TB_MAXT ? TW_ADJ_MAXT : TB_MAXT;   // wavelet samples per chunked adjoint launch
 struct AdjTBArgs {
     TBGeo g;
     CoefGen cg;                          // model + sponge amplitude (wide kernels regenerate alpha / kappa)
@@ -559,7 +561,7 @@ struct AdjTBArgs {
     double *gk_part;                     // [B*ns][nblk]
     float *gbeta;                        // [B*ns]
     int k0, nsteps, nblk;
-    float w[8];                          // w[k0-1-t] (wide kernels: up to TW_ADJ_MAXT steps)
+    float w[ADJ_W_MAX];                  // w[k0-1-t], t < nsteps (narrow: <= TB_MAXT, wide: <= TW_ADJ_MAXT steps)
 };
 
 // Adjoint with the same register-region blocking, walking k = k0, k0-1, ...:
@@ -2454,6 +2456,8 @@ struct rdq_fwi_plan {
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
+    bool adj_tw_fma = false;    // wide chunked adjoint with FMA contraction (RDQ_VARIANT_CHUNKED_ADJ_FMA; default:
+                                // the oracle's exact order, bitwise gA / gbeta / gk terms)
     bool wide = true;           // chunked kernels on 128-column regions (k_fwd_tw / k_adj_tw) vs 64-column
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;
@@ -2570,7 +2574,7 @@ void launch_adj(int T, dim3 grid, hipStream_t st, const Args &a)
 // wide chunked regions: forward 16 waves x 8 rows (128 x 128), adjoint 16 waves x 4 rows (128 x 64:
 // its seven two-column fields per row fill the 128 VGPRs of a 1024-thread workgroup)
 constexpr int TW_FWD_NW = 16, TW_FWD_R = 8, TW_ADJ_NW = 16, TW_ADJ_R = 4;
-constexpr int TW_ADJ_MAXT = 6;          // deepest wide adjoint (k_adj_tw instantiations 1 .. 6)
+static_assert(ADJ_W_MAX >= TW_ADJ_MAXT && ADJ_W_MAX >= TB_MAXT, "AdjTBArgs::w holds one sample per step of a launch");
 int tw_tiles_x(int Wp, int T) { return (Wp + (TW_W - 4 * T) - 1) / (TW_W - 4 * T); }
 int tw_tiles_y(int Hp, int T, bool adj)
 {
@@ -2991,15 +2995,15 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
-            for (int t = 0; t < 8; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
+            for (int t = 0; t < ADJ_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
             const int pin = i & 1, pout = pin ^ 1;
             a.in_l1 = ring + (size_t)(2 * pin) * L;
             a.in_l2 = ring + (size_t)(2 * pin + 1) * L;
             a.out_l1 = ring + (size_t)(2 * pout) * L;
             a.out_l2 = ring + (size_t)(2 * pout + 1) * L;
-            // (tail: T' < T); FMA form only where the persistent adjoint uses it too (nbc >= 20: a thin
-            // sponge's standing modes amplify the contraction's rounding, 1.5e-5 at nbc = 4)
-            if (p->wide) launch_adj_w(a.nsteps, (p->Wp & 1) == 0, !p->adj_fma, grid, cs, a);
+            // (tail: T' < T); the exact order unless RDQ_VARIANT_CHUNKED_ADJ_FMA asked for the contracted
+            // stencils (and only where nbc >= 20: a thin sponge's standing modes amplify the contraction)
+            if (p->wide) launch_adj_w(a.nsteps, (p->Wp & 1) == 0, !p->adj_tw_fma, grid, cs, a);
             else launch_adj(T, grid, cs, a);
         }
     }
@@ -3177,19 +3181,33 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     return 0;
 }
 
+int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *p, int32_t steps)
+{
+    if (!p || steps < 1 || steps > TW_ADJ_MAXT) return RDQ_E_INVALID;
+    if (p->adj_Tw != steps) {   // graphs encode the launch sequence
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->adj_Tw = steps;
+    return 0;
+}
+
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
-    if (!p || (flags & ~15)) return RDQ_E_INVALID;
+    if (!p || (flags & ~31)) return RDQ_E_INVALID;
     const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0;
     const bool fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0 && recurrence_ok(p);
+    const bool twfma = (flags & RDQ_VARIANT_CHUNKED_ADJ_FMA) != 0 && (flags & RDQ_VARIANT_ADJ_EXACT) == 0 &&
+                       recurrence_ok(p);
     const int xcd = (flags & RDQ_VARIANT_NO_XCD_LOCAL) ? 0 : 1;
     const bool wide = (flags & RDQ_VARIANT_NARROW_CHUNKED) == 0;
-    if (p->fwd_gen != gen || p->adj_fma != fma || p->xcd_mode != xcd || p->wide != wide) {
+    if (p->fwd_gen != gen || p->adj_fma != fma || p->adj_tw_fma != twfma || p->xcd_mode != xcd || p->wide != wide) {
         drop_graphs(p);
         p->cache.clear();
     }
     p->fwd_gen = gen;
     p->adj_fma = fma;
+    p->adj_tw_fma = twfma;
     p->xcd_mode = xcd;
     p->wide = wide;
     return 0;

@@ -63,9 +63,11 @@ def grad_all_reduce(x, group=None, monitor=None):
 
 
 def shot_slice(fwi_forward, ns_total):
-    """(start, stop) of the shots the operator models, or None when it models them all."""
+    """(start, stop) of the shots the operator models, or None when it models them all -- unless the
+    caller asked for sharding explicitly (FWIForward(shots=...): `shots_explicit`), which keeps the
+    sharded path (gradient all-reduce, global observation count) even for one rank holding every shot."""
     shots = getattr(fwi_forward, "shots", None)
-    if shots is None or (shots[0] == 0 and shots[1] == ns_total):
+    if shots is None or (shots[0] == 0 and shots[1] == ns_total and not getattr(fwi_forward, "shots_explicit", False)):
         return None
     return shots
 

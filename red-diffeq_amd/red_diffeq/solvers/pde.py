@@ -88,14 +88,22 @@ class FwiPlan:
     def set_graphs(self, enable):
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
-    def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True, wide_chunked=True):
+    def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True, wide_chunked=True,
+                    chunked_adj_fma=False):
         """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
         the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction; xcd_local:
         persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs;
-        wide_chunked: chunked kernels on 128-column regions (two columns per lane) instead of 64."""
+        wide_chunked: chunked kernels on 128-column regions (two columns per lane) instead of 64;
+        chunked_adj_fma: the wide chunked adjoint contracts its stencils into FMAs (opt-in; the default
+        chunked adjoint keeps the oracle's exact order)."""
         flags = ((1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
-                 | (0 if wide_chunked else 8))
+                 | (0 if wide_chunked else 8) | (16 if chunked_adj_fma else 0))
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
+
+    def set_wide_adj_steps(self, steps):
+        """Time steps per launch of the wide chunked adjoint (1..6, default 6); set_tuning's adj_steps
+        sets the persistent / narrow chunked adjoints' depth.  Results are identical for every depth."""
+        _hip.check(self.lib.rdq_fwi_set_wide_adj_steps(self.handle, int(steps)), "rdq_fwi_set_wide_adj_steps")
 
     def set_rows_per_wave(self, fwd_rows, adj_rows):
         """Rows per wave of the 64 x 96-region persistent kernels (forward 6 / 8 / 12 / 24, adjoint
@@ -107,8 +115,15 @@ class FwiPlan:
         """True / 1: persistent launches when they fit (small surveys in 64 x 64 regions of 16 waves x
         4 rows, else 64 x 96 regions, else 64 x 64 of 8 waves x 8 rows); 16 / 12 / 8: persistent with
         that region class only; False / 0: chunked launches.  Results are identical in every mode.
-        -1 (fault-path tests): persistent launches oversubscribed past residency, which fail."""
+        -1 (fault-path tests): persistent launches oversubscribed past residency, which fail.
+        A direct call during an engine fallback (FWIForward.fallback_to_chunked) replaces the mode the
+        restore would bring back."""
         mode = int(enable) if not isinstance(enable, bool) else int(enable)
+        self._set_mode(mode)
+        if self._saved_mode is not None:
+            self._saved_mode = mode
+
+    def _set_mode(self, mode):
         _hip.check(self.lib.rdq_fwi_set_persistent(self.handle, mode), "rdq_fwi_set_persistent")
         self.persist_mode = mode
 
@@ -211,8 +226,10 @@ class FWIForward(nn.Module):
         self.ctx = ctx
         # shot-parallel sharding: this operator models only shots[start:stop]
         self.shots = (0, len(ctx["sx"])) if shots is None else (int(shots[0]), int(shots[1]))
+        self.shots_explicit = shots is not None
         self._plans = {}
         self._last = None
+        self._fallen_back = False      # between fallback_to_chunked() and restore_persistent()
 
     # --- reference helpers kept with their signatures -------------------------------------
     def ricker(self, f, dt, nt):
@@ -257,6 +274,10 @@ class FWIForward(nn.Module):
                 self._plans[key].set_graphs(False)
             if os.environ.get("RDQ_ROWS_PER_WAVE"):          # "fwd,adj" (tools/ab_rw.sh, red_loop A/B)
                 self._plans[key].set_rows_per_wave(*[int(x) for x in os.environ["RDQ_ROWS_PER_WAVE"].split(",")])
+            if self._fallen_back:     # created during a fallback: chunked until restore_persistent()
+                plan = self._plans[key]
+                plan._saved_mode = plan.persist_mode
+                plan._set_mode(0)
         return self._plans[key]
 
     def _fused_denorm(self):
@@ -294,24 +315,28 @@ class FWIForward(nn.Module):
     def fallback_to_chunked(self):
         """After a persistent-launch failure: every plan runs the chunked (non-resident) kernels until
         restore_persistent(), and the status words are cleared (stream-ordered).  Each plan's mode
-        is saved once (a second fallback before the restore keeps the first saved mode)."""
+        is saved once (a second fallback before the restore keeps the first saved mode); plans created
+        while fallen back (a new grid shape) start chunked too (_plan)."""
+        self._fallen_back = True
         for plan in self._plans.values():
             if plan._saved_mode is None:
                 plan._saved_mode = plan.persist_mode
-            plan.set_persistent(False)
+            plan._set_mode(0)
             plan.status_t.zero_()
 
     def restore_persistent(self):
         """Back to the persistent kernels (where they fit) after fallback_to_chunked(): the engine
         re-promotes after a number of clean iterations (core/inversion.py _FaultMonitor).  Each plan
         gets back the mode it had before the fallback: a plan pinned to the chunked kernels (0) or to
-        one region class (8 / 12 / 16) keeps it; the fault-path test mode (-1) comes back as auto (1)."""
+        one region class (8 / 12 / 16) keeps it; the fault-path test mode (-1) comes back as auto (1).
+        A plan whose mode was set directly (set_persistent) during the fallback keeps that mode."""
+        self._fallen_back = False
         for plan in self._plans.values():
             mode = plan._saved_mode
             if mode is None:
                 continue                           # never fell back: nothing to restore
             plan._saved_mode = None
-            plan.set_persistent(1 if mode == -1 else mode)
+            plan._set_mode(1 if mode == -1 else mode)
 
     def coefficients(self, v):
         """Debug/inspection: the K3 fields (alpha, temp1, temp2, kappa, beta, v) on the padded grid."""

@@ -274,3 +274,5 @@ def test_shot_slice_helper():
     assert shot_slice(F(), 8) is None
     F.shots = (2, 5)
     assert shot_slice(F(), 8) == (2, 5)
+    F.shots, F.shots_explicit = (0, 8), True    # sharding asked for explicitly: kept at one rank too
+    assert shot_slice(F(), 8) == (0, 8)

@@ -533,8 +533,10 @@ def test_inversion_loop_vs_reference(cuda, name):
 def test_marmousi_scale_grid_vs_oracle(cuda):
     """configs[4] grid (500 x 3000 model, nbc 120: 740 x 3240 padded, ng = 3000): one shot does not
     fit a resident launch, so the chunked temporal-blocked kernels run it (every T); forward
-    bit-exact and adjoint gA / gbeta bit-exact vs the oracle (exact-order adjoint) on a short
-    record (nt = 150, the shortest the Ricker wavelet allows), 2 shots at both ends of the line."""
+    bit-exact and adjoint gA / gbeta bit-exact vs the oracle (the default chunked adjoint keeps the
+    exact order) on a short record (nt = 150, the shortest the Ricker wavelet allows), 2 shots at both
+    ends of the line.  Forward depths 2 / 4 (150 % 4 = 2: a tail launch), wide adjoint depths 4 / 6
+    (150 % 4 = 2: a tail launch)."""
     from red_diffeq.utils.synthetic import make_model
     nz, nx = 500, 3000
     ctx = dict(n_grid=nx, nt=150, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=nx, ns=2)
@@ -552,11 +554,11 @@ def test_marmousi_scale_grid_vs_oracle(cuda):
     so, c = f.forward(vn, keep_history=True)
     oA, oK, ob = f.adjoint(c, dseis_np)
     del c
-    plan.set_variant(adj_exact=True)
-    for T in (2, 4):
+    for T, Tw in ((2, 4), (4, 6)):
         plan.set_tuning(T, T, 1)
+        plan.set_wide_adj_steps(Tw)
         info = plan.launch_info(B)
-        assert not info["fwd_persistent"] and not info["adj_persistent"]
+        assert not info["fwd_persistent"] and not info["adj_persistent"] and info["adj_T"] == Tw
         coeffs, vstat = plan.coeffs(v, 0)
         seis, hist = plan.forward(coeffs, B, keep_history=True)
         gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
@@ -569,11 +571,14 @@ def test_marmousi_scale_grid_vs_oracle(cuda):
         np.testing.assert_allclose(gk.view(B, -1).sum(1).cpu().numpy(), oK, rtol=1e-7)
 
 
-def _chunked_run(plan, v, B, dseis, wide, exact, T):
-    """Chunked forward + adjoint: (seis, per-shot gA [B, ns, Hp, Wp], gbeta [B, ns], gk sum [B])."""
+def _chunked_run(plan, v, B, dseis, wide, exact, T, fma=False, Tw=6):
+    """Chunked forward + adjoint: (seis, per-shot gA [B, ns, Hp, Wp], gbeta [B, ns], gk sum [B]).
+    T: forward / narrow adjoint depth; Tw: the wide adjoint's depth; fma: the opt-in contracted wide
+    adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)."""
     plan.set_persistent(False)
-    plan.set_variant(adj_exact=exact, wide_chunked=wide)
+    plan.set_variant(adj_exact=exact, wide_chunked=wide, chunked_adj_fma=fma)
     plan.set_tuning(T, T, 1)
+    plan.set_wide_adj_steps(Tw)
     assert not plan.launch_info(B)["adj_persistent"]
     coeffs, vstat = plan.coeffs(v, 0)
     seis, hist = plan.forward(coeffs, B, keep_history=True)
@@ -592,14 +597,15 @@ def _shot_sum(gA):
     return acc
 
 
-@pytest.mark.parametrize("nx,nbc,T", [(71, 10, 4), (71, 10, 3), (84, 10, 4), (40, 4, 2)])
-def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T):
+@pytest.mark.parametrize("nx,nbc,T,Tw", [(71, 10, 4, 6), (71, 10, 3, 5), (84, 10, 4, 4), (40, 4, 2, 6)])
+def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T, Tw):
     """The chunked kernels on 128-column regions (two columns per lane; k_fwd_tw / k_adj_tw) on an odd
     padded width (Wp = 91: a lane's column pair wraps across the domain edge, 4-byte accesses), an
-    even one (Wp = 104: 8-byte pairs) and a thin sponge (nbc = 4): forward bit-exact and exact-order
-    gA / gbeta bit-exact vs the oracle and equal, shot by shot, to the 64-column kernels; nt = 162 is
-    not a multiple of T, so the tail launch runs its own depth.  The FMA variant (the default) within
-    fp32 tolerance."""
+    even one (Wp = 104: 8-byte pairs) and a thin sponge (nbc = 4): forward bit-exact and the default
+    (exact-order) gA / gbeta bit-exact vs the oracle and equal, shot by shot, to the 64-column kernels.
+    nt = 162 with forward depths 4 / 3 / 2 (162 % 4 = 2: the forward's tail launch runs its own depth)
+    and wide adjoint depths 6 / 5 / 4 (162 % 5 = 2, 162 % 4 = 2: the adjoint's tail too).  The opt-in
+    FMA variant within fp32 tolerance."""
     from red_diffeq.utils.synthetic import make_model
     ctx = dict(n_grid=nx, nt=162, dx=10.0, dt=0.001, nbc=nbc, f=15.0, sz=10, gz=10, ng=nx, ns=3)
     vn = vnorm(make_model("curvefault", 40, nx, seed=31, batch=2))
@@ -612,7 +618,10 @@ def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T):
     rng = np.random.default_rng(11)
     dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
     dseis = torch.from_numpy(dseis_np).to(cuda)
-    wide = _chunked_run(plan, v, B, dseis, True, True, T)
+    plan.set_persistent(False)
+    plan.set_wide_adj_steps(Tw)
+    assert plan.launch_info(B)["adj_T"] == Tw
+    wide = _chunked_run(plan, v, B, dseis, True, False, T, Tw=Tw)      # the default chunked adjoint
     narrow = _chunked_run(plan, v, B, dseis, False, True, T)
     f = O.OracleFWI(dict(ctx), B)
     so, c = f.forward(vn, keep_history=True)
@@ -623,24 +632,54 @@ def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T):
     assert bits_equal(wide[2], ob) and bits_equal(narrow[2], ob)
     np.testing.assert_allclose(wide[3], oK, rtol=1e-7)
     np.testing.assert_allclose(narrow[3], wide[3], rtol=1e-12)
-    fma = _chunked_run(plan, v, B, dseis, True, False, T)
+    fma = _chunked_run(plan, v, B, dseis, True, False, T, fma=True, Tw=Tw)
     assert bits_equal(fma[0], so)
     gA, oA = fma[1].astype(np.float64).sum(1), oA.astype(np.float64)   # (nbc = 4 grows to 1e25: fp64 norms)
+    if nbc < 20:                               # thin sponge: the FMA request is ignored (exact order)
+        assert bits_equal(fma[1], wide[1])
     assert np.linalg.norm(gA - oA) / np.linalg.norm(oA) < 2e-6
     np.testing.assert_allclose(fma[2], ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
     np.testing.assert_allclose(fma[3], oK, rtol=2e-5)
 
 
+@pytest.mark.parametrize("nt", [157, 158, 159, 160, 161])
+def test_wide_adjoint_tail_depths_bitexact(cuda, nt):
+    """every tail depth of the wide adjoint (nt % 6 = 1 .. 5 at the default depth 6: the
+    k_adj_tw<1..5> instantiations production runs for nt = 1000 at depth 6 run a tail of 4) against the
+    oracle, bitwise: gA, gbeta, and gk to fp64 summation order; the forward's tail (nt % 4) too."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=71, nt=nt, dx=10.0, dt=0.001, nbc=20, f=15.0, sz=10, gz=10, ng=71, ns=2)
+    vn = vnorm(make_model("curvevel", 36, 71, seed=5, batch=2))
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vn).to(cuda)
+    plan = fwi._plan(36, 71, v.device)
+    B = 2
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(nt)
+    dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
+    got = _chunked_run(plan, v, B, torch.from_numpy(dseis_np).to(cuda), True, False, 4)
+    assert plan.launch_info(B)["adj_launches"] == (nt + 5) // 6
+    f = O.OracleFWI(dict(ctx), B)
+    so, c = f.forward(vn, keep_history=True)
+    oA, oK, ob = f.adjoint(c, dseis_np)
+    assert bits_equal(got[0], so)
+    assert bits_equal(_shot_sum(got[1]), oA)
+    assert bits_equal(got[2], ob)
+    np.testing.assert_allclose(got[3], oK, rtol=1e-7)
+    go = f.finalize(c, oA, oK, ob)
+    assert np.linalg.norm(got[4] - go) / np.linalg.norm(go) < 1e-6
+
+
 @pytest.mark.parametrize("name,kw", FWD)
-def test_wide_chunked_fma_adjoint_vs_oracle(cuda, name, kw):
-    """The default chunked adjoint (FMA contraction) on every forward fixture: gA within 2e-6 rel-L2 of
-    the oracle's, gbeta within 2e-5, and the velocity gradient (K4) within 5e-5 rel-L2 of the oracle's
-    (the bar the exact path meets against the reference's autograd; measured 1.6e-5 at OpenFWI, the
-    persistent default's recurrence form 1.0e-5).
-    The sponge sum gk = sum K P (L_{k+1} - L_k) is a difference of nearly equal adjoint levels, so
-    the contraction's rounding shows there most (1.3e-4 relative at OpenFWI, ns = 5, nt = 400); it
-    enters the gradient at one cell (the first argmin of the velocity).
-    Thin-sponge fixtures (nbc < 20) run the exact order."""
+def test_wide_chunked_adjoint_vs_oracle(cuda, name, kw):
+    """The default chunked adjoint (k_adj_tw, the oracle's exact order; the path every non-resident
+    grid such as configs[4] runs) on every forward fixture: gA / gbeta bit-exact vs the oracle, gk to
+    fp64 summation order, the velocity gradient (K4) within 1e-6 rel-L2 of the oracle's.
+    The opt-in contracted variant (RDQ_VARIANT_CHUNKED_ADJ_FMA, ~4 % faster at configs[4]) beside it:
+    gA within 2e-6 rel-L2; its sponge sum gk = sum K P (L_{k+1} - L_k) is a difference of nearly
+    equal adjoint levels, so the contraction's rounding shows there most (1.3e-4 relative at OpenFWI,
+    ns = 5, nt = 400), and through gk's one cell (the first argmin of the velocity) dL/dv within 5e-5.
+    Thin-sponge fixtures (nbc < 20) run the exact order for both."""
     z = load_golden(name)
     ctx = ctx_of(z)
     fwi = make_fwi(ctx, **kw)
@@ -651,15 +690,25 @@ def test_wide_chunked_fma_adjoint_vs_oracle(cuda, name, kw):
     sz = plan.sizes(B)
     rng = np.random.default_rng(3)
     dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
-    got = _chunked_run(plan, v, B, torch.from_numpy(dseis_np).to(cuda), True, False, 4)
+    dseis = torch.from_numpy(dseis_np).to(cuda)
     f = O.OracleFWI(ctx, B, **kw)
     _, c = f.forward(vn, keep_history=True)
     oA, oK, ob = f.adjoint(c, dseis_np)
-    gA, oA = got[1].astype(np.float64).sum(1), oA.astype(np.float64)
-    assert np.linalg.norm(gA - oA) / np.linalg.norm(oA) < 2e-6
-    np.testing.assert_allclose(got[2], ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
-    np.testing.assert_allclose(got[3], oK, rtol=3e-4)
-    go = f.finalize(c, oA.astype(np.float32), oK, ob)
+    go = f.finalize(c, oA, oK, ob)
+    got = _chunked_run(plan, v, B, dseis, True, False, 4)
+    assert bits_equal(_shot_sum(got[1]), oA)
+    assert bits_equal(got[2].reshape(ob.shape), ob)
+    np.testing.assert_allclose(got[3], oK, rtol=1e-7)
     rel = np.linalg.norm(got[4] - go) / np.linalg.norm(go)
+    record_margin("wide_chunked_dLdv_rel_l2", name, rel, 1e-6)
+    assert rel < 1e-6
+    fma = _chunked_run(plan, v, B, dseis, True, False, 4, fma=True)
+    gA, oA64 = fma[1].astype(np.float64).sum(1), oA.astype(np.float64)
+    assert np.linalg.norm(gA - oA64) / np.linalg.norm(oA64) < 2e-6
+    np.testing.assert_allclose(fma[2], ob, rtol=2e-5, atol=2e-6 * np.abs(ob).max())
+    krel = float(np.max(np.abs(fma[3] - oK) / np.abs(oK)))
+    record_margin("wide_chunked_fma_gk_rel", name, krel, 3e-4)
+    assert krel < 3e-4
+    rel = np.linalg.norm(fma[4] - go) / np.linalg.norm(go)
     record_margin("wide_chunked_fma_dLdv_rel_l2", name, rel, 5e-5)
     assert rel < 5e-5

@@ -31,6 +31,36 @@ def _free_port():
     return p
 
 
+def test_rccl_world1_engine_iteration(cuda, tmp_path):
+    """the RCCL code path once on the box's one GPU.  One rank started by
+    torch.distributed.run, ``init_process_group("nccl", device_id=...)`` exactly as bench.py's N > 1 ranks
+    do, drives InversionEngine.optimize on the explicitly sharded operator (FWIForward(shots=(0, ns)):
+    the engine's sharded branch at world size 1), so every iteration's data-term gradient goes through
+    grad_all_reduce's RCCL all-reduce with the fault status word packed in as one extra element, and the
+    observation-loss log through a second all-reduce.  The result equals the unsharded single-rank run
+    (a one-rank sum is the identity) and holds the reference's trajectory."""
+    from test_gpu_loop_parity import model_rmse, run_engine
+    out = tmp_path / "rank0.npz"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RDQ_TEST_BACKEND="nccl")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "tests", "dist_engine_worker.py"), str(out)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    s = np.load(out)
+    assert str(s["backend"]) == "nccl"
+    assert bool(s["sharded"])                            # grad_all_reduce ran, the status word inside
+    z = load_golden("loop_noise_small")
+    mu1, h1 = run_engine(cuda, z)
+    err = float(model_rmse(s["mu"], mu1).max())
+    record_margin("rccl_world1_vs_single_rank_model_rmse", "loop_noise_small", err, 1e-6)
+    assert err < 1e-6
+    assert float(model_rmse(s["mu"], z["mu"]).max()) <= 1e-4
+    for k in ("obs_losses", "total_losses", "rmse", "ssim"):
+        np.testing.assert_allclose(s[k].astype(np.float64), np.array([h[k] for h in h1], np.float64), rtol=1e-6,
+                                   atol=1e-8, err_msg=k)
+
+
 def test_sharded_engine_two_ranks(cuda, tmp_path):
     from test_gpu_loop_parity import model_rmse, run_engine
     out = tmp_path / "rank0.npz"

@@ -332,6 +332,7 @@ def test_fallback_restores_each_plans_own_persistent_mode():
             self.calls = []
 
         set_persistent = FwiPlan.set_persistent
+        _set_mode = FwiPlan._set_mode
 
         @property
         def lib(self):
@@ -358,3 +359,43 @@ def test_fallback_restores_each_plans_own_persistent_mode():
     assert all(p._saved_mode is None for p in (pinned, failing, cls12))
     fwi.restore_persistent()                   # nothing saved: no change
     assert [p.persist_mode for p in (pinned, failing, cls12)] == [0, 1, 12]
+    # a direct set_persistent during the fallback is the mode the restore brings back
+    fwi.fallback_to_chunked()
+    cls12.set_persistent(8)
+    assert cls12.persist_mode == 8
+    fwi.restore_persistent()
+    assert [p.persist_mode for p in (pinned, failing, cls12)] == [0, 1, 8]
+
+
+def test_plan_created_during_fallback_starts_chunked(monkeypatch):
+    """a plan created while the operator is fallen back (a new grid shape) runs the chunked
+    kernels until restore_persistent(), which gives it back its own (auto) mode.  FwiPlan is replaced by a
+    stub, so no GPU is needed."""
+    from red_diffeq.solvers import pde
+
+    class Stub:
+        def __init__(self, *a, **k):
+            self.persist_mode, self._saved_mode, self.status_t = 1, None, torch.ones(4)
+
+        set_persistent = pde.FwiPlan.set_persistent
+        _set_mode = pde.FwiPlan._set_mode
+        handle = None
+
+        @property
+        def lib(self):
+            class L:
+                def rdq_fwi_set_persistent(self, h, mode):
+                    return 0
+            return L()
+
+    monkeypatch.setattr(pde, "FwiPlan", Stub)
+    ctx = dict(n_grid=70, ns=2, ng=70, dx=10.0, nt=200, nbc=20, f=15.0, dt=0.001, sz=10, gz=10)
+    fwi = pde.FWIForward(ctx, torch.device("cpu"))
+    old = fwi._plan(70, 70, torch.device("cpu"))
+    fwi.fallback_to_chunked()
+    new = fwi._plan(70, 90, torch.device("cpu"))
+    assert old.persist_mode == 0 and new.persist_mode == 0
+    fwi.restore_persistent()
+    assert old.persist_mode == 1 and new.persist_mode == 1
+    again = fwi._plan(70, 110, torch.device("cpu"))
+    assert again.persist_mode == 1

@@ -30,6 +30,8 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--T", type=str, default="2,3,4", help="blocking depths to time")
 ap.add_argument("--narrow", action="store_true", help="64-column chunked regions (round-3 layout)")
 ap.add_argument("--exact", action="store_true", help="exact-order adjoint (RDQ_VARIANT_ADJ_EXACT)")
+ap.add_argument("--chunked-adj-fma", action="store_true", help="contracted wide chunked adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)")
+ap.add_argument("--Tw", type=int, default=6, help="wide chunked adjoint depth (rdq_fwi_set_wide_adj_steps)")
 ap.add_argument("--chains", type=int, default=1, help="concurrent shot-group launch chains")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
@@ -39,7 +41,9 @@ ctx = dict(n_grid=a.nx, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=1
 fwi = FWIForward(dict(ctx), dev, v_denorm_func=v_denormalize, s_norm_func=s_normalize_none)
 v = v_normalize(torch.from_numpy(make_model("curvefault", a.nz, a.nx, batch=1))).to(dev)
 plan = fwi._plan(a.nz, a.nx, dev)
-plan.set_variant(fwd_gen_coeffs=not a.no_gen, wide_chunked=not a.narrow, adj_exact=a.exact)
+plan.set_variant(fwd_gen_coeffs=not a.no_gen, wide_chunked=not a.narrow, adj_exact=a.exact,
+                 chunked_adj_fma=a.chunked_adj_fma)
+plan.set_wide_adj_steps(a.Tw)
 sz = plan.sizes(1)
 npad = sz.Hp * sz.Wp
 dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
@@ -65,7 +69,7 @@ for T in [int(t) for t in a.T.split(",")]:
     plan.status()
     f, d = min(fw), min(ad)
     shot_steps = a.ns * a.nt
-    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chunked_adj_fma": a.chunked_adj_fma, "Tw": a.Tw, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
                       "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
                       "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
                       "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
