@@ -125,15 +125,21 @@ int rdq_conv2d_stem(const rdq_conv_desc *d, const float *x, const float *w, cons
 size_t rdq_conv2d_bf16_wpack_bytes(const rdq_conv_desc *d);
 int rdq_conv2d_bf16_pack(const rdq_conv_desc *d, const float *w, void *wp, hipStream_t stream);
 size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d);
-/* Process-wide U-Net kernel options (test / A-B switches; set before capturing graphs):
+/* Process-wide U-Net kernel options (test / A-B switches).  They choose kernels, and with them the
+ * fp32 summation order, for every later call in the process: the values are atomics (never torn), but
+ * a change does not reach hipGraphs captured before it, so every change bumps the counter returned by
+ * rdq_unet_options_generation (the Python U-Net keys its captured graphs on it and recaptures).
  *   RDQ_UNET_OPT_BF16_PER_TAP = 1: rdq_conv2d_bf16 always runs the per-tap kernel instead of the
  *   halo-staged 3x3 kernel (the two share the operand rounding; tests/test_gpu_unet.py compares them).
- * Returns the previous value, or RDQ_E_INVALID for an unknown option. */
+ * Returns the previous value, or RDQ_E_INVALID for an unknown option or value. */
 #define RDQ_UNET_OPT_BF16_PER_TAP 1
 #define RDQ_UNET_OPT_CONV3_MIN_TILES 2   /* least (256-pixel x 64-channel) tiles for the halo-staged 3x3 conv (default 64) */
 #define RDQ_UNET_OPT_BF16_RAW 3   /* rdq_conv2d_bf16_gn_*: hold the raw conv output as bf16 (default 1) */
 #define RDQ_UNET_OPT_CONV3F_MIN_TILES 4   /* least tiles for the fp32 halo-staged 3x3 conv (0: never; default 192) */
+#define RDQ_UNET_OPT_CC_MIN_STAGES 6   /* channel-chunk convs: least K stages per split-K piece (default 3) */
+#define RDQ_UNET_OPT_CC_SPLIT2_STAGES 7   /* grids of 128..255 tiles split K in two from this many stages (default 12) */
 int rdq_unet_set_option(int32_t option, int32_t value);
+int rdq_unet_options_generation(void);
 int rdq_conv2d_bf16(const rdq_conv_desc *d, const float *x, const float *x2, const void *wp, const float *bias,
                     const float *residual, float *y, void *ws, size_t ws_bytes, hipStream_t stream);
 

@@ -12,6 +12,7 @@
 //                 time-conditioned scale/shift + SiLU in one pass.
 //   rmsnorm / linear / sinusoidal embedding / linear & full attention / RED prologue-epilogue.
 #include <hip/hip_runtime.h>
+#include <atomic>
 
 #include <cmath>
 #include <algorithm>
@@ -685,13 +686,15 @@ void cc_extents(CcArgs &c, const rdq_conv_desc *d)
 // per CU with nothing to hide its waits) is split in two when each half keeps >= 6 stages (a
 // second workgroup on a CU shares the matrix unit but hides the first one's load / LDS latency:
 // level-9 512-channel convs at B = 8 measured 73 -> see DESIGN.md)
+static std::atomic<int> CC_MIN_STAGES{3};     // least K stages per split (RDQ_UNET_OPT_CC_MIN_STAGES)
+static std::atomic<int> CC_SPLIT2_STAGES{12}; // 128..255 tiles split in two from this many stages (RDQ_UNET_OPT_CC_SPLIT2_STAGES)
 int cc_splits(const rdq_conv_desc *d, size_t ws_bytes, int *per_split)
 {
     const int M = d->B * d->H * d->W;
     const int tiles = ((M + CC_BM - 1) / CC_BM) * ((d->cout + CC_BN - 1) / CC_BN);
     const int nstages = (d->cin1 + d->cin2) / (d->kh == 3 ? CcCfg<9>::CPS : CcCfg<1>::CPS);
-    int S = std::max(1, std::min(std::min(256 / tiles, nstages / 3), 16));
-    if (tiles >= 128 && tiles < 256 && nstages >= 12) S = 2;
+    int S = std::max(1, std::min(std::min(256 / tiles, nstages / std::max(1, CC_MIN_STAGES.load())), 16));
+    if (tiles >= 128 && tiles < 256 && nstages >= CC_SPLIT2_STAGES.load()) S = 2;
     const size_t slab = (size_t)tiles * CC_BM * CC_BN * sizeof(float);      // >= M * cout floats
     if (S > 1) S = (int)std::min<size_t>((size_t)S, ws_bytes / slab);
     S = std::max(S, 1);
@@ -3314,9 +3317,13 @@ __global__ __launch_bounds__(256, (LbOcc<D, F>::N)) void k_lab_out(LabArgs a)
 // upsampled input) with at least C3_MIN_TILES tiles; everything else stays on the per-tap kernel. The
 // halo kernel wins even on a part-filled chip (bf16 U-Net forward, B = 25: 4.15 -> 3.13 ms, B = 100:
 // 8.0 -> 6.2 ms, B = 344: 18.5 -> 18.1 ms going from 512 to 64); below ~64 tiles it loses at B <= 8
-static int C3_BF16_RAW = 1;      // rdq_unet_set_option(RDQ_UNET_OPT_BF16_RAW)
-static int C3_MIN_TILES = 64;    // rdq_unet_set_option(RDQ_UNET_OPT_CONV3_MIN_TILES); tools/conv3_threshold_ab.py
-static int C3F_MIN_TILES = 192;  // k_conv3_f32; rdq_unet_set_option(RDQ_UNET_OPT_CONV3F_MIN_TILES), 0 = never
+// Process-wide kernel options (rdq_unet_set_option).  Atomics, so a concurrent set is never torn; every
+// change bumps g_opt_gen (rdq_unet_options_generation), which the Python U-Net folds into its captured-
+// graph cache key, so graphs captured under the old choice are recaptured instead of replayed.
+static std::atomic<int> C3_BF16_RAW{1};      // RDQ_UNET_OPT_BF16_RAW
+static std::atomic<int> C3_MIN_TILES{64};    // RDQ_UNET_OPT_CONV3_MIN_TILES; tools/conv3_threshold_ab.py
+static std::atomic<int> C3F_MIN_TILES{192};  // k_conv3_f32; RDQ_UNET_OPT_CONV3F_MIN_TILES, 0 = never
+static std::atomic<int> g_opt_gen{0};
 static int64_t conv3_tiles(const rdq_conv_desc *d)
 {
     if (d->kh != 3 || d->kw != 3 || d->pad != 1) return 0;
@@ -3377,6 +3384,21 @@ void launch_conv_bf16(dim3 grid, hipStream_t st, const BfArgs &a)
     case RDQ_IN_UNSHUFFLE2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_bf16<RDQ_IN_UNSHUFFLE2, NB>), grid, dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_bf16<RDQ_IN_PLAIN, NB>), grid, dim3(256), 0, st, a); break;
     }
+}
+
+// k_conv_cc for a cc_ok descriptor: 3x3 (plain / nearest x2) or 1x1 (plain / 2x2 unshuffle)
+void launch_cc(const CcArgs &c, dim3 grid, hipStream_t st)
+{
+    const rdq_conv_desc *d = &c.d;
+#define RDQ_LCC(T, M) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<T, M>), grid, dim3(256), 0, st, c)
+    if (d->kh == 3) {
+        if (d->in_mode == RDQ_IN_UPSAMPLE2) RDQ_LCC(9, RDQ_IN_UPSAMPLE2);
+        else RDQ_LCC(9, RDQ_IN_PLAIN);
+    } else {
+        if (d->in_mode == RDQ_IN_UNSHUFFLE2) RDQ_LCC(1, RDQ_IN_UNSHUFFLE2);
+        else RDQ_LCC(1, RDQ_IN_PLAIN);
+    }
+#undef RDQ_LCC
 }
 
 bool conv_desc_ok(const rdq_conv_desc *d)
@@ -3481,17 +3503,7 @@ int rdq_conv2d(const rdq_conv_desc *d, const float *x, const float *x2, const fl
         const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
         CcArgs cl = c;
         if (c.S > 1 && !fold) cl.S = -c.S;            // slabs only; k_conv_reduce combines
-        if (d->kh == 3) {
-            if (d->in_mode == RDQ_IN_UPSAMPLE2)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, cl);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, cl);
-        } else {
-            if (d->in_mode == RDQ_IN_UNSHUFFLE2)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, cl);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, cl);
-        }
+        launch_cc(cl, grid, st);
         if (c.S > 1 && !fold) {
             const int64_t total = (int64_t)c.M * d->cout;
             hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, c.S, total,
@@ -3581,17 +3593,7 @@ int rdq_conv2d_gn_silu(const rdq_conv_desc *d, const float *x, const float *x2, 
     double *gnp = c.gnp;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
     const int bm = conv3f_gn(c, d, G, st) ? C3_BM : CC_BM;    // launched there, or here:
-    if (bm == CC_BM && d->kh == 3) {
-        if (d->in_mode == RDQ_IN_UPSAMPLE2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    } else if (bm == CC_BM) {
-        if (d->in_mode == RDQ_IN_UNSHUFFLE2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    }
+    if (bm == CC_BM) launch_cc(c, grid, st);
     const int C = d->cout, HW = c.HW;
     int nch = 0;
     bool gn4 = false;
@@ -3667,8 +3669,7 @@ int rdq_conv2d_gn_silu_sc(const rdq_conv_desc *d, const float *x, const float *x
     int bm = CC_BM;
     if (conv3f_gn(c, d, G, st)) {     // the 3x3 on the halo-staged kernel, the shortcut on its own
         bm = C3_BM;
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), dim3((e.M + CC_BM - 1) / CC_BM, gy_b, e.S),
-                           dim3(256), 0, st, e);
+        launch_cc(e, dim3((e.M + CC_BM - 1) / CC_BM, gy_b, e.S), st);
     } else {
         const dim3 grid((c.M + CC_BM - 1) / CC_BM, gy_a + gy_b, std::max(c.S, e.S));
         hipLaunchKernelGGL(k_conv_cc_pair, grid, dim3(256), 0, st, c, e, gy_a);
@@ -3734,17 +3735,7 @@ int rdq_conv2d_gn_silu_out(const rdq_conv_desc *d, const float *x, const float *
         return RDQ_E_INVALID;
     const dim3 grid((c.M + CC_BM - 1) / CC_BM, (d->cout + CC_BN - 1) / CC_BN, c.S);
     const int bm = conv3f_gn(c, d, G, st) ? C3_BM : CC_BM;    // launched there, or here:
-    if (bm == CC_BM && d->kh == 3) {
-        if (d->in_mode == RDQ_IN_UPSAMPLE2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_UPSAMPLE2>), grid, dim3(256), 0, st, c);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<9, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    } else if (bm == CC_BM) {
-        if (d->in_mode == RDQ_IN_UNSHUFFLE2)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_UNSHUFFLE2>), grid, dim3(256), 0, st, c);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv_cc<1, RDQ_IN_PLAIN>), grid, dim3(256), 0, st, c);
-    }
+    if (bm == CC_BM) launch_cc(c, grid, st);
     const int HW = c.HW;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply_out<float>), dim3((HW + 63) / 64, d->B), dim3(64 * GO_NW), 0, st, d->cout, HW, G, c.y, gamma, beta,
                        scale_shift, c.gnp, eps, post_residual, nf, wf, bf, yf, bm);
@@ -3833,32 +3824,26 @@ size_t rdq_conv2d_bf16_ws_bytes(const rdq_conv_desc *d)
     return S > 1 ? (size_t)S * d->B * d->H * d->W * d->cout * sizeof(float) : 0;
 }
 
-static int g_bf16_per_tap = 0;   // RDQ_UNET_OPT_BF16_PER_TAP
+static std::atomic<int> g_bf16_per_tap{0};   // RDQ_UNET_OPT_BF16_PER_TAP
 
 int rdq_unet_set_option(int32_t option, int32_t value)
 {
-    if (option == RDQ_UNET_OPT_CONV3F_MIN_TILES) {
-        if (value < 0) return RDQ_E_INVALID;
-        const int old = C3F_MIN_TILES;
-        C3F_MIN_TILES = value;
-        return old;
+    std::atomic<int> *opt = nullptr;
+    switch (option) {
+    case RDQ_UNET_OPT_BF16_PER_TAP: opt = &g_bf16_per_tap; value = value != 0; break;
+    case RDQ_UNET_OPT_CONV3_MIN_TILES: if (value < 1) return RDQ_E_INVALID; opt = &C3_MIN_TILES; break;
+    case RDQ_UNET_OPT_BF16_RAW: opt = &C3_BF16_RAW; value = value != 0; break;
+    case RDQ_UNET_OPT_CONV3F_MIN_TILES: if (value < 0) return RDQ_E_INVALID; opt = &C3F_MIN_TILES; break;
+    case RDQ_UNET_OPT_CC_MIN_STAGES: if (value < 1) return RDQ_E_INVALID; opt = &CC_MIN_STAGES; break;
+    case RDQ_UNET_OPT_CC_SPLIT2_STAGES: if (value < 1) return RDQ_E_INVALID; opt = &CC_SPLIT2_STAGES; break;
+    default: return RDQ_E_INVALID;
     }
-    if (option == RDQ_UNET_OPT_BF16_RAW) {
-        const int old = C3_BF16_RAW;
-        C3_BF16_RAW = value != 0;
-        return old;
-    }
-    if (option == RDQ_UNET_OPT_CONV3_MIN_TILES) {
-        if (value < 1) return RDQ_E_INVALID;
-        const int old = C3_MIN_TILES;
-        C3_MIN_TILES = value;
-        return old;
-    }
-    if (option != RDQ_UNET_OPT_BF16_PER_TAP) return RDQ_E_INVALID;
-    const int old = g_bf16_per_tap;
-    g_bf16_per_tap = value != 0;
+    const int old = opt->exchange(value);
+    if (old != value) g_opt_gen.fetch_add(1);
     return old;
 }
+
+int rdq_unet_options_generation(void) { return g_opt_gen.load(); }
 
 int rdq_conv2d_stem(const rdq_conv_desc *d, const float *x, const float *w, const float *bias, float *y, hipStream_t st)
 {

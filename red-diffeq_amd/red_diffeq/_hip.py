@@ -102,6 +102,7 @@ SIGNATURES = {
     "rdq_conv2d_bf16_pack": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p]),
     "rdq_conv2d_bf16_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "rdq_unet_set_option": (c_int32, [c_int32, c_int32]),
+    "rdq_unet_options_generation": (c_int32, []),
     "rdq_conv2d_bf16": (c_int32, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_size_t, c_void_p]),
     "rdq_conv2d_bf16_gn_ws_bytes": (c_size_t, [ctypes.POINTER(ConvDesc), c_int32]),

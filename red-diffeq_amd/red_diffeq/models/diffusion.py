@@ -278,11 +278,15 @@ class Unet(nn.Module):
         (load_state_dict(assign=True), ``p.data = t``, a new nn.Parameter on a submodule) changes it
         and forces a recapture.  In-place updates (optimizer steps, load_state_dict
         copies) keep the addresses and need none in fp32; the bf16 path reads packed copies, so
-        there the parameters' version counters are part of the key too."""
+        there the parameters' version counters are part of the key too.  So is the library's kernel-option
+        generation (rdq_unet_options_generation): graphs captured under other options are recaptured."""
         ptrs = tuple(p.data_ptr() for p in self.parameters())
+        # kernel options (rdq_unet_set_option) choose kernels at capture time: a change recaptures
+        from .. import _hip
+        opt = int(_hip.lib().rdq_unet_options_generation())
         if self.precision == "bf16":
-            return (getattr(self, "_wgen", 0), ptrs, tuple(p._version for p in self.parameters()))
-        return (getattr(self, "_wgen", 0), ptrs)
+            return (getattr(self, "_wgen", 0), opt, ptrs, tuple(p._version for p in self.parameters()))
+        return (getattr(self, "_wgen", 0), opt, ptrs)
 
     def _graphed(self, x, time):
         ent = self._graph_entry(x, time)

@@ -355,6 +355,79 @@ def gen_loop_red_configs2():
          **{k: np.array(hist[0][k]) for k in keys}, **ctx_arrays(ctx), **rec.arrays())
 
 
+class _OracleOpPerModel(torch.autograd.Function):
+    """The oracle operator one model at a time (B models x ns shots): the forward keeps no history and the
+    backward recomputes each model's forward with its history before the adjoint, so at most one model's
+    history (0.8 GB at ns = 5, nt = 400) is alive.  The oracle's arithmetic is per (model, shot), so this
+    equals the batched oracle bit for bit."""
+
+    @staticmethod
+    def forward(c, v, f):
+        vn = v.detach().contiguous().numpy().astype(np.float32)
+        c.f, c.vn = f, vn
+        return torch.from_numpy(np.concatenate([f.forward(vn[b:b + 1])[0] for b in range(vn.shape[0])]))
+
+    @staticmethod
+    def backward(c, g):
+        g = g.contiguous().numpy()
+        out = []
+        for b in range(c.vn.shape[0]):
+            _, cf = c.f.forward(c.vn[b:b + 1], keep_history=True)
+            gA, gK, gb = c.f.adjoint(cf, g[b:b + 1])
+            out.append(c.f.finalize(cf, gA, gK, gb))
+            del cf
+        return torch.from_numpy(np.concatenate(out)), None
+
+
+def gen_loop_red_b25(variant=""):
+    """The reference's shipped OpenFWI config at its own batch (configs/openfwi/red-diffeq.yaml:43,
+    batch_size 25: one InversionEngine.optimize call on 25 models x 5 shots, inversion.py:46-129, with a
+    B = 25 U-Net regulariser): 25 CurveFault models, nt = 400, the dim-8 U-Net of gen_unet, lambda 0.75,
+    lr 0.03, sigma 10, sigma_x0 1e-4, 3 iterations, the eps_x0 / t / eps draws recorded.  The reference
+    engine, regulariser and U-Net are driven by the oracle operator (one model at a time, recomputed in
+    the backward: the reference FWIForward's autograd tape at 125 slices x 400 steps is ~25 GB).  y is the
+    oracle forward (bit-exact with the reference operator's); it is not stored (14 MB): the GPU test
+    regenerates it with the HIP forward and checks its checksum."""
+    diff = ref.diffusion.GaussianDiffusion(_unet_dim8(), image_size=72, timesteps=1000, sampling_timesteps=250,
+                                           objective="pred_noise").eval()
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from oracle import oracle as O
+    ctx = dict(OPENFWI, nt=400)
+    B = 25
+    v_true = synthetic.make_model("curvefault", 70, 70, seed=8892, batch=B)
+    f = O.OracleFWI(ctx, 1, variant=variant)
+    vt = vnorm(v_true).astype(np.float32)
+    y = np.concatenate([f.forward(vt[b:b + 1])[0] for b in range(B)])
+
+    class Op:
+        def __call__(self, v):
+            return _OracleOpPerModel.apply(v, f)
+
+        def to(self, device):
+            return self
+    init = torch.cat([ref.data_trans.prepare_initial_model(torch.from_numpy(v_true[i:i + 1]), "smoothed", sigma=10.0)
+                      for i in range(B)])
+    mu0 = torch.nn.functional.pad(init, (1, 1, 1, 1), "constant", 0)
+    eng = ref.inversion.InversionEngine(diff, ref.ssim.SSIM(window_size=11), "diffusion", sigma_x0=1e-4)
+    ts = 3
+    torch.manual_seed(1234)
+    rec = record_draws()
+    t0 = time.time()
+    with rec:
+        mu, hist = eng.optimize(mu0, torch.from_numpy(v_true), torch.from_numpy(y), Op(), ts=ts, lr=0.03,
+                                reg_lambda=0.75, regularization="diffusion")
+    print(f"  b25 loop {time.time() - t0:.1f}s")
+    keys = ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse")
+    if variant:      # reproducibility-floor member: the same engine and draws on another correct fp32 operator
+        save("loop_red_b25_" + variant, mu=mu.detach().numpy(), **{k: np.stack([np.array(h[k]) for h in hist])
+                                                                    for k in keys})
+        return
+    save("loop_red_b25", reg=np.array("diffusion"), v_true=v_true, mu0=mu0.numpy(), mu=mu.detach().numpy(),
+         params=np.array([ts, 0.03, 0.75, 10.0, 0, 0.0]), noise_type=np.array("gaussian"), sigma_x0=np.array(1e-4),
+         use_time_weight=np.array(False), y_checksum=np.array([float(np.abs(y).astype(np.float64).sum())]),
+         **{k: np.stack([np.array(h[k]) for h in hist]) for k in keys}, **ctx_arrays(ctx), **rec.arrays())
+
+
 def gen_initial():
     """prepare_initial_model (utils/data_trans.py:65-107), all three initial_type branches."""
     out = {}
@@ -593,7 +666,8 @@ def gen_post():
 GENS = dict(geometry=gen_geometry, damp=gen_damp, forward=gen_forward, grad=gen_grad,
             loop=gen_loop, unet=gen_unet, red=gen_red, small_losses=gen_small_losses, dfwi=gen_dfwi,
             ilvr=gen_ilvr, loop_rng=gen_loop_rng, loop_red=gen_loop_red, initial=gen_initial, ckpt=gen_ckpt,
-            loop_red_configs2=gen_loop_red_configs2, post=gen_post)
+            loop_red_configs2=gen_loop_red_configs2, post=gen_post, loop_red_b25=gen_loop_red_b25,
+            loop_red_b25_fma=lambda: gen_loop_red_b25("fma"))
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(GENS)

@@ -123,6 +123,43 @@ def test_red_loop_configs2_at_its_size(cuda):
                                    err_msg=k)
 
 
+def test_red_loop_openfwi_yaml_b25(cuda):
+    """The reference's shipped OpenFWI config at its own batch (configs/openfwi/red-diffeq.yaml:43,
+    batch_size 25: one optimize call on 25 CurveFault models x 5 shots with a B = 25 U-Net regulariser,
+    reference inversion.py:46-129), nt = 400, the dim-8 U-Net, lambda 0.75, 3 iterations, the reference's
+    eps_x0 / t / eps draws replayed.  Reference side: the reference engine, regulariser and U-Net driven
+    by the oracle operator (make_golden.gen_loop_red_b25).  On the HIP side the 125 slices run as
+    persistent launches of slice groups that span models.  Bar: model RMSE <= 1e-4 for every one of the
+    25 models, losses and metrics within 2e-4 relative."""
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.utils.data_trans import v_normalize
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden("loop_red_b25")
+    fwi = make_fwi(ctx_of(z))
+    with torch.no_grad():
+        y = fwi(v_normalize(torch.from_numpy(z["v_true"])).to(cuda))
+    ysum = float(y.abs().double().sum())
+    assert abs(ysum - float(z["y_checksum"][0])) <= 1e-9 * ysum, (ysum, z["y_checksum"])
+    plan = fwi._plan(70, 70, y.device)
+    assert plan.launch_info(25)["fwd_persistent"]
+    eng = InversionEngine(dim8_diffusion(cuda), SSIM(window_size=11), "diffusion", sigma_x0=1e-4,
+                          show_progress=False)
+    with replay_draws(z):
+        mu, hist = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]), y, fwi, ts=3, lr=0.03,
+                                reg_lambda=0.75, regularization="diffusion")
+    d = model_rmse(mu.detach().cpu().numpy(), z["mu"])
+    print(f"loop_red_b25: velocity-model RMSE vs the reference engine per model: max {d.max():.3e}, median "
+          f"{np.median(d):.3e}")
+    record_margin("loop_red_b25_model_rmse_vs_ref", "max over 25 models", float(d.max()), 1e-4)
+    assert d.shape == (25,) and d.max() <= 1e-4, d
+    for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
+        got = np.array([h[k] for h in hist], np.float64)
+        ref = z[k].astype(np.float64)
+        rel = float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-6)))
+        record_margin("loop_red_b25_rel", k, rel, 2e-4)
+        np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-6, err_msg=k)
+
+
 def test_tv_long_trajectory_floor(cuda):
     """30 TV iterations: the HIP engine's model vs the reference's, per iteration, against the
     reference's own drift between 1 and 8 threads (measured: 0, bitwise) and between its operator and

@@ -399,3 +399,21 @@ def test_plan_created_during_fallback_starts_chunked(monkeypatch):
     assert old.persist_mode == 1 and new.persist_mode == 1
     again = fwi._plan(70, 110, torch.device("cpu"))
     assert again.persist_mode == 1
+
+
+def test_unet_options_are_atomic_and_versioned():
+    """rdq_unet_set_option returns the previous value, rejects unknown options and bad values,
+    and every change bumps rdq_unet_options_generation (the U-Net's captured-graph cache key), while a
+    set to the current value does not.  Host-only: no GPU call."""
+    from red_diffeq import _hip
+    lib = _hip.load_library()
+    g0 = lib.rdq_unet_options_generation()
+    old = lib.rdq_unet_set_option(6, 5)               # RDQ_UNET_OPT_CC_MIN_STAGES
+    try:
+        assert old == 3
+        assert lib.rdq_unet_options_generation() == g0 + 1
+        assert lib.rdq_unet_set_option(6, 5) == 5 and lib.rdq_unet_options_generation() == g0 + 1
+        assert lib.rdq_unet_set_option(6, 0) < 0 and lib.rdq_unet_set_option(99, 1) < 0
+    finally:
+        assert lib.rdq_unet_set_option(6, old) == 5
+    assert lib.rdq_unet_options_generation() == g0 + 2

@@ -67,17 +67,25 @@ if __name__ == "__main__":
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--inner", type=int, default=20)
     ap.add_argument("--f32-min-tiles", type=int, nargs="+", default=[None])
+    ap.add_argument("--opt", type=int, default=None, help="another rdq_unet_set_option option id to compare")
+    ap.add_argument("--opt-values", type=int, nargs="+", default=[None], help="... and its values")
     a = ap.parse_args()
     names = [a.only] if a.only else list(SHAPES)
     for B in a.B:
         for n in names:
             for ft in a.f32_min_tiles:
+              for ov in a.opt_values:
                 old = None if ft is None else _hip.lib().rdq_unet_set_option(4, ft)
+                old_o = None if ov is None else _hip.lib().rdq_unet_set_option(a.opt, ov)
                 try:
                     r = run(n, B, a.reps, a.inner, a.bf16)
+                    if ov is not None:
+                        r["opt"], r["opt_value"] = a.opt, ov
                 finally:
                     if old is not None:
                         _hip.lib().rdq_unet_set_option(4, old)
+                    if old_o is not None:
+                        _hip.lib().rdq_unet_set_option(a.opt, old_o)
                 if ft is not None:
                     r["f32_min_tiles"] = ft
                 print(json.dumps(r), flush=True)
