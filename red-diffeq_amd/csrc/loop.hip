@@ -61,7 +61,7 @@ struct MetArgs {
 __global__ __launch_bounds__(256) void k_metrics_tile(MetArgs a)
 {
     __shared__ float xa[IT][IT], xb[IT][IT];
-    __shared__ float hz[5][IT][MT];
+    __shared__ double hz[5][IT][MT];
     __shared__ double red[2][256];
     __shared__ double rsm[256];
     const int b = blockIdx.y, tile = blockIdx.x;
@@ -89,35 +89,40 @@ __global__ __launch_bounds__(256) void k_metrics_tile(MetArgs a)
         xb[r][c] = t;
     }
     __syncthreads();
+    // The SSIM map of ssim.py:_ssim (the fp32 window and the fp32 inputs (x + 1) / 2 of the reference)
+    // evaluated in fp64: its variances are differences E[x^2] - mu^2 of nearly equal moments, so an fp32
+    // evaluation is reproducible only to ~1e-4 of the SSIM between two summation orders (measured: the
+    // reference's CPU value vs a GPU torch run of the same module on the same model, 1.5e-4).  In fp64 the
+    // metric is the formula's value, and what is left against the reference is the reference's own fp32
+    // rounding.
     // horizontal pass: 5 moments on IT rows x MT output columns
     for (int i = tid; i < IT * MT; i += 256) {
         const int r = i / MT, c = i - r * MT;
-        float s1 = 0.f, s2 = 0.f, s11 = 0.f, s22 = 0.f, s12 = 0.f;
+        double s1 = 0.0, s2 = 0.0, s11 = 0.0, s22 = 0.0, s12 = 0.0;
 #pragma unroll
         for (int k = 0; k < WIN; ++k) {
-            const float u = xa[r][c + k], v = xb[r][c + k], w = a.win[k];
+            const double u = xa[r][c + k], v = xb[r][c + k], w = a.win[k];
             s1 += w * u; s2 += w * v; s11 += w * (u * u); s22 += w * (v * v); s12 += w * (u * v);
         }
         hz[0][r][c] = s1; hz[1][r][c] = s2; hz[2][r][c] = s11; hz[3][r][c] = s22; hz[4][r][c] = s12;
     }
     __syncthreads();
     double sm = 0.0;
-    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const double C1 = (double)(0.01f * 0.01f), C2 = (double)(0.03f * 0.03f);
     for (int i = tid; i < MT * MT; i += 256) {
         const int r = i / MT, c = i - r * MT;
         const int y = ty * MT + r, x = tx * MT + c;
         if (y >= a.H || x >= a.W) continue;
-        float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+        double m1 = 0.0, m2 = 0.0, e11 = 0.0, e22 = 0.0, e12 = 0.0;
 #pragma unroll
         for (int k = 0; k < WIN; ++k) {
-            const float w = a.win[k];
+            const double w = a.win[k];
             m1 += w * hz[0][r + k][c]; m2 += w * hz[1][r + k][c]; e11 += w * hz[2][r + k][c];
             e22 += w * hz[3][r + k][c]; e12 += w * hz[4][r + k][c];
         }
-        const float mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
-        const float s1 = e11 - mu1_sq, s2 = e22 - mu2_sq, s12 = e12 - mu12;
-        const float v = ((2.0f * mu12 + C1) * (2.0f * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2));
-        sm += (double)v;
+        const double mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
+        const double s1 = e11 - mu1_sq, s2 = e22 - mu2_sq, s12 = e12 - mu12;
+        sm += ((2.0 * mu12 + C1) * (2.0 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2));
     }
     red[0][tid] = sad; red[1][tid] = ssq; rsm[tid] = sm;
     __syncthreads();

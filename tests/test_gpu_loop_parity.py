@@ -123,14 +123,22 @@ def test_red_loop_configs2_at_its_size(cuda):
                                    err_msg=k)
 
 
-def test_red_loop_openfwi_yaml_b25(cuda):
+@pytest.mark.parametrize("adjoint", ["exact", "default"])
+def test_red_loop_openfwi_yaml_b25(cuda, adjoint):
     """The reference's shipped OpenFWI config at its own batch (configs/openfwi/red-diffeq.yaml:43,
     batch_size 25: one optimize call on 25 CurveFault models x 5 shots with a B = 25 U-Net regulariser,
     reference inversion.py:46-129), nt = 400, the dim-8 U-Net, lambda 0.75, 3 iterations, the reference's
     eps_x0 / t / eps draws replayed.  Reference side: the reference engine, regulariser and U-Net driven
     by the oracle operator (make_golden.gen_loop_red_b25).  On the HIP side the 125 slices run as
     persistent launches of slice groups that span models.  Bar: model RMSE <= 1e-4 for every one of the
-    25 models, losses and metrics within 2e-4 relative."""
+    25 models; losses and metrics within 2e-4 relative with the exact-order adjoint (gA bitwise the
+    oracle's: only the U-Net's fp32 rounding differs); the default recurrence adjoint (dL/dv within ~1e-5
+    of the exact gradient) within 5e-4 -- the reference engine on the oracle's FMA build, another correct
+    fp32 operator (make_golden loop_red_b25_fma), is 7.9e-3 model RMSE and 2.6e-3 in SSIM away.
+    SSIM's own floor is measured here: the metric (K12, its SSIM map in fp64) of the reference's OWN final
+    25 models against the reference's value for them differs by ~1.9e-4 (the reference evaluates the
+    variances E[x^2] - mu^2 in fp32; a GPU torch run of the reference SSIM module on the same models
+    differs from it by 1.5e-4), so SSIM is held to max(2e-4, 2 x that floor)."""
     from red_diffeq.core.inversion import InversionEngine
     from red_diffeq.utils.data_trans import v_normalize
     from red_diffeq.utils.ssim import SSIM
@@ -142,6 +150,7 @@ def test_red_loop_openfwi_yaml_b25(cuda):
     assert abs(ysum - float(z["y_checksum"][0])) <= 1e-9 * ysum, (ysum, z["y_checksum"])
     plan = fwi._plan(70, 70, y.device)
     assert plan.launch_info(25)["fwd_persistent"]
+    plan.set_variant(adj_exact=adjoint == "exact")
     eng = InversionEngine(dim8_diffusion(cuda), SSIM(window_size=11), "diffusion", sigma_x0=1e-4,
                           show_progress=False)
     with replay_draws(z):
@@ -150,14 +159,24 @@ def test_red_loop_openfwi_yaml_b25(cuda):
     d = model_rmse(mu.detach().cpu().numpy(), z["mu"])
     print(f"loop_red_b25: velocity-model RMSE vs the reference engine per model: max {d.max():.3e}, median "
           f"{np.median(d):.3e}")
-    record_margin("loop_red_b25_model_rmse_vs_ref", "max over 25 models", float(d.max()), 1e-4)
+    record_margin("loop_red_b25_model_rmse_vs_ref", adjoint, float(d.max()), 1e-4)
     assert d.shape == (25,) and d.max() <= 1e-4, d
+    from red_diffeq.core.fused import metrics
+    with torch.no_grad():     # the metric's own floor: the reference's final models through K12
+        m_ref = metrics(torch.from_numpy(z["mu"]).to(cuda).contiguous(),
+                        v_normalize(torch.from_numpy(z["v_true"]).to(cuda)).contiguous()).cpu().numpy()
+    floor = float(np.max(np.abs(m_ref[2] - z["ssim"][:, -1]) / np.abs(z["ssim"][:, -1])))
+    record_margin("loop_red_b25_ssim_metric_floor", "K12 on the reference's final models", floor, 2.5e-4)
+    assert floor < 2.5e-4
+    bar = 2e-4 if adjoint == "exact" else 5e-4
     for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
         got = np.array([h[k] for h in hist], np.float64)
         ref = z[k].astype(np.float64)
         rel = float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-6)))
-        record_margin("loop_red_b25_rel", k, rel, 2e-4)
-        np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-6, err_msg=k)
+        b = max(bar, 2 * floor) if k == "ssim" else bar
+        print(f"  {adjoint} {k}: max rel {rel:.3e} (bar {b:.2e})")
+        record_margin("loop_red_b25_rel_" + adjoint, k, rel, b)
+        np.testing.assert_allclose(got, ref, rtol=b, atol=1e-6, err_msg=k)
 
 
 def test_tv_long_trajectory_floor(cuda):
