@@ -108,8 +108,9 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
 #define RDQ_VARIANT_NARROW_CHUNKED 8
 #define RDQ_VARIANT_CHUNKED_ADJ_FMA 16
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
-/* Time steps per launch of the WIDE chunked adjoint (k_adj_tw, 1..6; default 6: 167 launches at
- * configs[4]'s nt instead of 250 at 4).  rdq_fwi_set_tuning's adj_steps sets the persistent and the
+/* Time steps per launch of the WIDE chunked adjoint (k_adj_tw, 1..6, or 0 = the default, 5: the
+ * fastest depth measured at configs[4] for both the exact-order and the contracted kernels,
+ * profiles/r5/configs4_wide_adj_depth.jsonl).  rdq_fwi_set_tuning's adj_steps sets the persistent and the
  * narrow chunked adjoints' depth only.  A time loop whose nt is not a multiple of the depth ends with
  * one shorter launch of its own depth.  Results are identical for every depth. */
 int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *plan, int32_t steps);

@@ -2452,7 +2452,7 @@ struct rdq_fwi_plan {
     int fwd_rw = 6, adj_rw = 6;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave;
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
-    int adj_Tw = 6;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT; profiles/r4/configs4_chunked_ab)
+    int adj_Tw = 0;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT); 0 = auto, see wide_adj_depth
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
@@ -2492,6 +2492,12 @@ TBGeo tb_geo(const rdq_fwi_plan *p, int B)
 // branches).  Concurrent chains overlap each launch's fixed latency (prologue loads, store
 // drain, dispatch) with the other chains' compute.
 int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, p->g.ns)); }
+
+// Default depth of the wide chunked adjoint, measured at configs[4] (profiles/r5/configs4_wide_adj_depth.jsonl):
+// 5 steps per launch is the fastest for both forms (exact order 116.1-116.3 ms vs 120.4 at 4 and 120.6
+// at 6; contracted 111.2 ms vs 115.1-115.7 at 6).
+constexpr int TW_ADJ_DEFAULT = 5;
+int wide_adj_depth(const rdq_fwi_plan *p) { return p->adj_Tw > 0 ? p->adj_Tw : TW_ADJ_DEFAULT; }
 
 int ensure_aux(rdq_fwi_plan *p, int S)
 {
@@ -2819,44 +2825,59 @@ void launch_adj_pt(const rdq_fwi_plan *p, int NW, int T, dim3 grid, hipStream_t 
     }
 }
 
-// The buffers a persistent launch needs zeroed (granules, accumulators, the first two history slots,
-// pt_assign's arrival counters) in ONE stream-ordered launch instead of a memset each (each memset is a
-// separate ~5 us dispatch on the step's critical path).  Regions are 16-byte aligned, sizes multiples of 4 B.
+// The buffers a launch needs zeroed (granules, accumulators, history slots, adjoint levels, pt_assign's
+// arrival counters) in ONE stream-ordered kernel instead of a memset each (each memset is a separate
+// ~5 us dispatch on the step's critical path).  Sizes are multiples of 4 B; 16-byte-aligned regions are
+// cleared with 16-byte stores, others with 4-byte ones.
+// The chunked launchers run inside hipGraph capture (run_cached), and they must not use
+// hipMemsetAsync there: on this ROCm (7.2) a captured memset node is not executed when the graph
+// exec is REPLAYED (the capture launch is correct, every later launch leaves the region untouched;
+// tools/diag_graph_rawmem.py with hipMalloc'd buffers, tools/repro/graph_kernarg.hip for the
+// single-kernel case that does work).  A kernel node replays correctly.
+constexpr int ZERO_MAXR = 6;
 struct ZeroArgs {
-    void *p[6];
-    size_t n[6];      // bytes
+    void *p[ZERO_MAXR];
+    size_t n[ZERO_MAXR];      // bytes
     int nr;
 };
 __global__ __launch_bounds__(256) void k_zero_regions(ZeroArgs z)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x, t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int r = 0; r < z.nr; ++r) {
-        uint4 *q = static_cast<uint4 *>(z.p[r]);
-        const size_t n4 = z.n[r] / 16;
-        for (size_t i = t; i < n4; i += stride) q[i] = make_uint4(0u, 0u, 0u, 0u);
-        const size_t tail = (z.n[r] - n4 * 16) / 4;
-        if (t < tail) reinterpret_cast<unsigned *>(q + n4)[t] = 0u;
+        if ((reinterpret_cast<uintptr_t>(z.p[r]) & 15) == 0) {
+            uint4 *q = static_cast<uint4 *>(z.p[r]);
+            const size_t n4 = z.n[r] / 16;
+            for (size_t i = t; i < n4; i += stride) q[i] = make_uint4(0u, 0u, 0u, 0u);
+            const size_t tail = (z.n[r] - n4 * 16) / 4;
+            if (t < tail) reinterpret_cast<unsigned *>(q + n4)[t] = 0u;
+        } else {
+            unsigned *q = static_cast<unsigned *>(z.p[r]);
+            for (size_t i = t; i < z.n[r] / 4; i += stride) q[i] = 0u;
+        }
     }
 }
 static int zero_regions(std::initializer_list<std::pair<void *, size_t>> regs, hipStream_t st)
 {
     ZeroArgs z{};
     size_t tot = 0;
+    auto flush = [&]() -> int {
+        if (!z.nr) return 0;
+        const size_t blocks = std::min<size_t>(2048, std::max<size_t>(1, (tot / 16 + 255) / 256));
+        hipLaunchKernelGGL(k_zero_regions, dim3((unsigned)blocks), dim3(256), 0, st, z);
+        RDQ_CHECK(hipGetLastError());
+        z = ZeroArgs{};
+        tot = 0;
+        return 0;
+    };
     for (const auto &r : regs) {
         if (!r.first || !r.second) continue;
-        if (z.nr == 6 || (reinterpret_cast<uintptr_t>(r.first) & 15) || (r.second & 3)) {   // caller buffers
-            RDQ_CHECK(hipMemsetAsync(r.first, 0, r.second, st));                         // off the fast path
-            continue;
-        }
+        if (r.second & 3) return RDQ_E_INVALID;                      // every region is 4-byte words
+        if (z.nr == ZERO_MAXR) RDQ_TRY(flush());
         z.p[z.nr] = r.first;
         z.n[z.nr++] = r.second;
         tot += r.second;
     }
-    if (!z.nr) return 0;
-    const size_t blocks = std::min<size_t>(2048, std::max<size_t>(1, (tot / 16 + 255) / 256));
-    hipLaunchKernelGGL(k_zero_regions, dim3((unsigned)blocks), dim3(256), 0, st, z);
-    RDQ_CHECK(hipGetLastError());
-    return 0;
+    return flush();
 }
 
 int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coeffs, float *seis, float *hist, float *ring,
@@ -2882,7 +2903,7 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
         a.g.sl_off = s0;
         a.g.nsl = std::min(per, B * p->g.ns - s0);
         const dim3 grid(pt_grid(p, T, NW, a.g.nsl, false));
-        if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
+        if (s0 > 0) RDQ_TRY(zero_regions({{p->d_status + 16, 8 * sizeof(unsigned)}}, st));   // pt_assign arrivals
         launch_fwd_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
     }
@@ -2914,7 +2935,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
         a.g.sl_off = s0;
         a.g.nsl = std::min(per, B * p->g.ns - s0);
         const dim3 grid(pt_grid(p, T, NW, a.g.nsl, true));
-        if (s0 > 0) RDQ_CHECK(hipMemsetAsync(p->d_status + 16, 0, 8 * sizeof(unsigned), st));   // pt_assign arrivals
+        if (s0 > 0) RDQ_TRY(zero_regions({{p->d_status + 16, 8 * sizeof(unsigned)}}, st));   // pt_assign arrivals
         launch_adj_pt(p, NW, T, grid, st, a);
         RDQ_CHECK(hipGetLastError());
     }
@@ -2928,8 +2949,9 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
     a.g = tb_geo(p, B);
     const size_t L = a.g.level;
     const int T = p->fwd_T, S = chain_count(p), ns = p->g.ns;
-    if (hist) RDQ_CHECK(hipMemsetAsync(hist, 0, 2 * L * sizeof(float), st));
-    else RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
+    // (no hipMemsetAsync under graph capture: see zero_regions)
+    if (hist) RDQ_TRY(zero_regions({{hist, 2 * L * sizeof(float)}}, st));
+    else RDQ_TRY(zero_regions({{ring, 4 * L * sizeof(float)}}, st));
     a.coeffs = coeffs;
     a.cg = coef_gen(p, B, coeffs);
     a.seis = seis;
@@ -2974,12 +2996,11 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     AdjTBArgs a{};
     a.g = tb_geo(p, B);
     const size_t L = a.g.level;
-    const int T = p->wide ? p->adj_Tw : p->adj_T, S = chain_count(p), ns = p->g.ns;
+    const int T = p->wide ? wide_adj_depth(p) : p->adj_T, S = chain_count(p), ns = p->g.ns;
     const int nblk_alloc = gk_blocks(p);
-    RDQ_CHECK(hipMemsetAsync(ring, 0, 4 * L * sizeof(float), st));
-    RDQ_CHECK(hipMemsetAsync(gA, 0, L * sizeof(float), st));
-    RDQ_CHECK(hipMemsetAsync(gk, 0, (size_t)B * ns * nblk_alloc * sizeof(double), st));
-    RDQ_CHECK(hipMemsetAsync(gbeta, 0, (size_t)B * ns * sizeof(float), st));
+    RDQ_TRY(zero_regions({{ring, 4 * L * sizeof(float)}, {gA, L * sizeof(float)},
+                          {gk, (size_t)B * ns * nblk_alloc * sizeof(double)}, {gbeta, (size_t)B * ns * sizeof(float)}},
+                         st));   // (no hipMemsetAsync under graph capture: see zero_regions)
     a.coeffs = coeffs; a.hist = hist; a.dseis = dseis; a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
     a.cg = coef_gen(p, B, coeffs);
     a.nblk = nblk_alloc;
@@ -3183,8 +3204,8 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
 
 int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *p, int32_t steps)
 {
-    if (!p || steps < 1 || steps > TW_ADJ_MAXT) return RDQ_E_INVALID;
-    if (p->adj_Tw != steps) {   // graphs encode the launch sequence
+    if (!p || steps < 0 || steps > TW_ADJ_MAXT) return RDQ_E_INVALID;   // 0 = auto (wide_adj_depth)
+    if (wide_adj_depth(p) != (steps ? steps : TW_ADJ_DEFAULT)) {   // graphs encode the launch sequence
         drop_graphs(p);
         p->cache.clear();
     }
@@ -3244,7 +3265,7 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     out[0] = persistent_nw(p, B, false, &perf);
     out[1] = persistent_nw(p, B, true, &pera);
     out[2] = p->fwd_T;
-    const int adjT = !out[1] && p->wide ? p->adj_Tw : p->adj_T;   // chunked adjoint: the wide kernels' depth
+    const int adjT = !out[1] && p->wide ? wide_adj_depth(p) : p->adj_T;   // chunked adjoint: the wide kernels' depth
     out[3] = adjT;
     const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
     out[4] = out[0] ? (ns + perf - 1) / perf : (nt + p->fwd_T - 1) / p->fwd_T;

@@ -101,7 +101,8 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_wide_adj_steps(self, steps):
-        """Time steps per launch of the wide chunked adjoint (1..6, default 6); set_tuning's adj_steps
+        """Time steps per launch of the wide chunked adjoint (1..6; 0 = the default, 5: fastest at
+        configs[4] for both forms); set_tuning's adj_steps
         sets the persistent / narrow chunked adjoints' depth.  Results are identical for every depth."""
         _hip.check(self.lib.rdq_fwi_set_wide_adj_steps(self.handle, int(steps)), "rdq_fwi_set_wide_adj_steps")
 

@@ -571,10 +571,10 @@ def test_marmousi_scale_grid_vs_oracle(cuda):
         np.testing.assert_allclose(gk.view(B, -1).sum(1).cpu().numpy(), oK, rtol=1e-7)
 
 
-def _chunked_run(plan, v, B, dseis, wide, exact, T, fma=False, Tw=6):
+def _chunked_run(plan, v, B, dseis, wide, exact, T, fma=False, Tw=0):
     """Chunked forward + adjoint: (seis, per-shot gA [B, ns, Hp, Wp], gbeta [B, ns], gk sum [B]).
-    T: forward / narrow adjoint depth; Tw: the wide adjoint's depth; fma: the opt-in contracted wide
-    adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)."""
+    T: forward / narrow adjoint depth; Tw: the wide adjoint's depth (0: the default, 5); fma: the opt-in
+    contracted wide adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)."""
     plan.set_persistent(False)
     plan.set_variant(adj_exact=exact, wide_chunked=wide, chunked_adj_fma=fma)
     plan.set_tuning(T, T, 1)
@@ -642,11 +642,60 @@ def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T, Tw):
     np.testing.assert_allclose(fma[3], oK, rtol=2e-5)
 
 
+@pytest.mark.parametrize("wide", [True, False])
+def test_chunked_graph_replays_on_poisoned_buffers(cuda, wide):
+    """Cached-graph REPLAYS of the chunked forward (history and ring forms) and adjoint on fixed
+    buffers that are filled with NaN before every call: each replay must zero what it accumulates
+    into (history slots 0 / 1, ring levels, gA, gk, gbeta) and equal the direct launches bit for bit.
+    (A captured hipMemsetAsync node is skipped on replay on this ROCm: the launchers zero with a
+    kernel; tools/diag_graph_rawmem.py.)"""
+    import ctypes
+    from red_diffeq import _hip
+    z = load_golden("fwd_wrap")
+    fwi = make_fwi(ctx_of(z))
+    v = torch.from_numpy(vnorm(z["v"])).to(cuda)
+    B = v.shape[0]
+    plan = fwi._plan(v.shape[2], v.shape[3], v.device)
+    plan.set_persistent(False)
+    plan.set_variant(wide_chunked=wide)
+    sz = plan.sizes(B)
+    coeffs, _ = plan.coeffs(v, 0)
+    f32 = lambda n: torch.empty(int(n) // 4, device=cuda)
+    seis, hist, ring = torch.empty(B, plan.ns, sz.nrec, plan.ng, device=cuda), f32(sz.history), f32(sz.ring)
+    seis_r = torch.empty_like(seis)
+    dseis = torch.from_numpy(np.random.default_rng(5).standard_normal(tuple(seis.shape)).astype(np.float32)).to(cuda)
+    gA, gb = f32(sz.gA), f32(sz.gbeta)
+    gk = torch.empty(int(sz.gk_part) // 8, dtype=torch.float64, device=cuda)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = _hip.ptr
+
+    def run():
+        for t in (seis, seis_r, hist, ring, gA, gb, gk):
+            t.fill_(float("nan"))
+        _hip.check(plan.lib.rdq_fwi_forward(plan.handle, B, P(coeffs), P(seis_r), ctypes.c_void_p(0), P(ring), st), "fwd")
+        _hip.check(plan.lib.rdq_fwi_forward(plan.handle, B, P(coeffs), P(seis), P(hist), P(ring), st), "fwd")
+        _hip.check(plan.lib.rdq_fwi_adjoint(plan.handle, B, P(coeffs), P(hist), P(dseis), P(ring), P(gA), P(gk), P(gb),
+                                            st), "adj")
+        torch.cuda.synchronize()
+        return [t.cpu().numpy().copy() for t in (seis, seis_r, gA, gb)] + [float(gk.sum())]
+
+    plan.set_graphs(False)
+    want = run()
+    plan.set_graphs(True)
+    for rep in range(3):                  # capture, then two replays of the same graph execs
+        got = run()
+        for name, a, b in zip(("seis", "seis_ring", "gA", "gbeta"), got, want):
+            assert bits_equal(a, b), (rep, name)
+        assert got[4] == want[4], rep
+
+
+@pytest.mark.parametrize("Tw", [6, 5])
 @pytest.mark.parametrize("nt", [157, 158, 159, 160, 161])
-def test_wide_adjoint_tail_depths_bitexact(cuda, nt):
-    """every tail depth of the wide adjoint (nt % 6 = 1 .. 5 at the default depth 6: the
-    k_adj_tw<1..5> instantiations production runs for nt = 1000 at depth 6 run a tail of 4) against the
-    oracle, bitwise: gA, gbeta, and gk to fp64 summation order; the forward's tail (nt % 4) too."""
+def test_wide_adjoint_tail_depths_bitexact(cuda, nt, Tw):
+    """every tail depth of the wide adjoint (nt % 6 = 1 .. 5 at depth 6; nt % 5 = 2, 3, 4,
+    0, 1 at the default depth 5: the k_adj_tw<1..5> instantiations a production nt runs as its tail)
+    against the oracle, bitwise: gA, gbeta, and gk to fp64 summation order; the forward's tail
+    (nt % 4) too."""
     from red_diffeq.utils.synthetic import make_model
     ctx = dict(n_grid=71, nt=nt, dx=10.0, dt=0.001, nbc=20, f=15.0, sz=10, gz=10, ng=71, ns=2)
     vn = vnorm(make_model("curvevel", 36, 71, seed=5, batch=2))
@@ -657,8 +706,8 @@ def test_wide_adjoint_tail_depths_bitexact(cuda, nt):
     sz = plan.sizes(B)
     rng = np.random.default_rng(nt)
     dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
-    got = _chunked_run(plan, v, B, torch.from_numpy(dseis_np).to(cuda), True, False, 4)
-    assert plan.launch_info(B)["adj_launches"] == (nt + 5) // 6
+    got = _chunked_run(plan, v, B, torch.from_numpy(dseis_np).to(cuda), True, False, 4, Tw=Tw)
+    assert plan.launch_info(B)["adj_launches"] == (nt + Tw - 1) // Tw
     f = O.OracleFWI(dict(ctx), B)
     so, c = f.forward(vn, keep_history=True)
     oA, oK, ob = f.adjoint(c, dseis_np)

@@ -31,7 +31,7 @@ ap.add_argument("--T", type=str, default="2,3,4", help="blocking depths to time"
 ap.add_argument("--narrow", action="store_true", help="64-column chunked regions (round-3 layout)")
 ap.add_argument("--exact", action="store_true", help="exact-order adjoint (RDQ_VARIANT_ADJ_EXACT)")
 ap.add_argument("--chunked-adj-fma", action="store_true", help="contracted wide chunked adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)")
-ap.add_argument("--Tw", type=int, default=6, help="wide chunked adjoint depth (rdq_fwi_set_wide_adj_steps)")
+ap.add_argument("--Tw", type=int, default=0, help="wide chunked adjoint depth (rdq_fwi_set_wide_adj_steps; 0 = auto)")
 ap.add_argument("--chains", type=int, default=1, help="concurrent shot-group launch chains")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
