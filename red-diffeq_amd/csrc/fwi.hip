@@ -2830,10 +2830,11 @@ void launch_adj_pt(const rdq_fwi_plan *p, int NW, int T, dim3 grid, hipStream_t 
 // ~5 us dispatch on the step's critical path).  Sizes are multiples of 4 B; 16-byte-aligned regions are
 // cleared with 16-byte stores, others with 4-byte ones.
 // The chunked launchers run inside hipGraph capture (run_cached), and they must not use
-// hipMemsetAsync there: on this ROCm (7.2) a captured memset node is not executed when the graph
-// exec is REPLAYED (the capture launch is correct, every later launch leaves the region untouched;
-// tools/diag_graph_rawmem.py with hipMalloc'd buffers, tools/repro/graph_kernarg.hip for the
-// single-kernel case that does work).  A kernel node replays correctly.
+// hipMemsetAsync there: on this ROCm (7.2) the captured memset node (present and first in the chain:
+// profiles/r5/graph_replay/captured_memset_node.dot.txt) takes effect on the graph exec's first launch
+// but not on its replays, which then read whatever the buffer held (tools/diag_graph_rawmem.py on
+// hipMalloc'd buffers; the minimal memset + kernel-chain graphs of tools/repro/graph_kernarg.hip
+// replay correctly, so the trigger is not isolated).  The zeroing kernel replays correctly.
 constexpr int ZERO_MAXR = 6;
 struct ZeroArgs {
     void *p[ZERO_MAXR];

@@ -162,9 +162,48 @@ int run_order(int which, size_t bytes, int spins, int reps)
     return bad_total;
 }
 
+// memset node + NK kernel nodes (each out[i] += 1 over the zeroed region): every replay must end at NK.
+// fill: the buffer is set to 0xFF bytes (NaN) with a plain hipMemset before every launch.
+int run_memset_chain(size_t bytes, int NK, int reps, bool fill)
+{
+    const int n = (int)(bytes / 4);
+    float *buf;
+    (void)hipMalloc(&buf, bytes);
+    hipStream_t s, cap;
+    (void)hipStreamCreate(&s);
+    (void)hipStreamCreateWithFlags(&cap, hipStreamNonBlocking);
+    hipGraph_t g;
+    (void)hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+    (void)hipMemsetAsync(buf, 0, bytes, cap);
+    for (int k = 0; k < NK; ++k) hipLaunchKernelGGL(kacc, dim3((n + 255) / 256), dim3(256), 0, cap, buf, n);
+    (void)hipStreamEndCapture(cap, &g);
+    hipGraphExec_t ex;
+    (void)hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    std::vector<float> h(n);
+    int bad_total = 0;
+    for (int r = 0; r < reps; ++r) {
+        if (fill) { (void)hipMemset(buf, 0xFF, bytes); (void)hipDeviceSynchronize(); }
+        (void)hipGraphLaunch(ex, s);
+        (void)hipMemcpyAsync(h.data(), buf, bytes, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        int bad = 0;
+        for (int i = 0; i < n; ++i) bad += h[i] != (float)NK;
+        printf("{\"chain_bytes\": %zu, \"kernels\": %d, \"fill\": %d, \"rep\": %d, \"bad\": %d, \"v0\": %g}\n", bytes, NK,
+               (int)fill, r, bad, h[0]);
+        bad_total += bad;
+    }
+    (void)hipGraphExecDestroy(ex);
+    (void)hipFree(buf);
+    (void)hipStreamDestroy(s); (void)hipStreamDestroy(cap);
+    return bad_total;
+}
+
 int main()
 {
     int bad = 0;
+    for (int nk : {1, 2, 8, 50})
+        for (bool fill : {false, true}) bad += run_memset_chain(40960, nk, 3, fill);
     for (int which : {0, 1, 2})
         for (int spins : {1000, 100000}) bad += run_order(which, 40960, spins, 3);
     for (size_t b : {4, 8, 16, 32, 64, 128, 256, 4096, 40960, 1 << 20}) bad += run_memset(b, 3);
