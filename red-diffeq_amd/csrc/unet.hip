@@ -2189,8 +2189,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
     const bool pv = gm < a.M;
     const int gb = pv ? gm / a.HW : 0, gpix = pv ? gm - gb * a.HW : 0;
     const int oh = gpix / d.W, ow = gpix - oh * d.W;
-    // weight role: rows wn + 64 j, k octet wq
-    const int wn = tid >> 2, wq = (tid & 3) * 8;
+    // weight role: rows wn + 64 j, k octet wq (eight consecutive lanes: one octet of eight consecutive
+    // rows, so each ds_write_b128 group lands on eight disjoint 16-B slots; k_conv3_bf16)
+    const int wn = (tid & 7) + 8 * (tid >> 5), wq = ((tid >> 3) & 3) * 8;
     float ra[16];
     bf16x8 rw[NB / 2];
     auto load = [&](int s) {
@@ -2351,6 +2352,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(BfArgs a)
 // ds_read_b128 group read 16 consecutive rows, conflict-free at that stride.
 constexpr int C3_BM = 256, C3_BN = 64, C3_NI = 7, C3_WMAX = 72;
 constexpr int C3_ROWS = C3_BM + 2 * C3_WMAX + 2;  // 402 <= 64 * C3_NI
+// Zero rows C3_ZROW .. C3_ZROW + 15 of the halo buffers: a lane whose tap leaves the image reads zero
+// row (its regular row & 15).  With 80-B rows a row's 16-B slot in the 64 banks is 5 row mod 16, so the
+// zero row sits on the slot the lane's regular row would have used and the ds_read_b128 groups stay
+// conflict-free at image borders (one shared zero row put every border lane on one slot: 2-way).
+constexpr int C3_ZROW = 416;
+static_assert(C3_ZROW % 16 == 0 && C3_ZROW >= C3_ROWS, "zero rows: 16-aligned, past the halo rows");
 
 struct C3Args {
     rdq_conv_desc d;
@@ -2450,7 +2457,11 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
     // thread's partials go through the halo buffer (free after the last chunk's barrier), four blocks
     // at a time, and 16 threads per (block, slot, sum) add 16 of them each in thread order, then a
     // fixed xor tree: deterministic, no long shuffle chains of fp64 per lane.
-    double *red = static_cast<double *>(halo);          // [16][256] per round (32 KiB)
+    // [16][RS] per round (34 KiB): rows RS = 272 doubles apart, so the two (block, slot, sum) rows one
+    // 32-lane ds_read_b64 group reads (combo, combo + 1) fall 32 dwords apart in the 64 banks instead
+    // of on the same ones (256 apart: a 2-way conflict on every read)
+    constexpr int RS = 272;
+    double *red = static_cast<double *>(halo);
     const int b0 = m0 / a.HW;
     int sl[2];
 #pragma unroll
@@ -2480,15 +2491,15 @@ __device__ __forceinline__ void c3_epilogue(const C3Args &a, f32x16 (&acc)[2][2]
             }
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-                red[((el * 2 + k) * 2 + 0) * 256 + tid] = gs[k];
-                red[((el * 2 + k) * 2 + 1) * 256 + tid] = gq[k];
+                red[((el * 2 + k) * 2 + 0) * RS + tid] = gs[k];
+                red[((el * 2 + k) * 2 + 1) * RS + tid] = gq[k];
             }
         }
         __syncthreads();
         const int combo = tid >> 4, part = tid & 15;
         double v = 0.0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v += red[combo * 256 + part + 16 * j];
+        for (int j = 0; j < 16; ++j) v += red[combo * RS + part + 16 * j];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
         if (part == 0) c3g[rd * 4 + (combo >> 2)][(combo >> 1) & 1][combo & 1] = v;
@@ -2512,7 +2523,10 @@ template <int MODE, bool IN8 = false>
 __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
 {
     // row C3_ROWS of each buffer stays zero: a lane whose tap leaves the image reads it (one address
-    // select per tap instead of zeroing the fragment's four registers per k step)
+    // select per tap instead of zeroing the fragment's four registers per k step).  (The bank-matched
+    // zero rows of k_conv3_f32 remove this kernel's remaining conflicts too, but the extra row
+    // arithmetic spills here or, kept per tap, costs more than the conflicts: 252 -> 256 us at l72 x
+    // 344 tiles, profiles/r5/pmc_conv3_bf16_zero_rows.jsonl.)
     __shared__ __attribute__((aligned(16))) __bf16 Hs[2][C3_ROWS + 1][BF_LD];     // 2 x 31.5 KiB
     __shared__ __attribute__((aligned(16))) __bf16 Ws[2][C3_BN][BF_LD];
     const rdq_conv_desc &d = a.d;
@@ -2578,8 +2592,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3_bf16(C3Args a)
         const int q = lane + 64 * k;
         if (q < a.R) *reinterpret_cast<bf16x8 *>(&Hs[buf][q][8 * wv]) = h;
     };
-    // weight role: row wn (of 64), 8-channel piece wq of the tap's 32
-    const int wn = tid >> 2, wq = (tid & 3) * 8;
+    // weight role: row wn (of 64), 8-channel piece wq of the tap's 32.  Eight consecutive lanes take
+    // the same piece of eight consecutive rows: a ds_write_b128 group (8 contiguous lanes, banks
+    // (a/4) mod 32) then starts at dwords 20 r mod 32 = {0, 20, 8, 28, 16, 4, 24, 12} + 4 piece, eight
+    // disjoint 16-B slots.  (Rows tid >> 2 with pieces tid & 3 put lanes 0 and 7 of every group on the
+    // same slot: a 2-way conflict on every stash, ~0.8 of the kernel's 1.1 conflict cycles per LDS
+    // instruction, profiles/r4/pmc_conv3_bf16_b344_after_gather.jsonl.)
+    const int wn = (tid & 7) + 8 * (tid >> 5), wq = ((tid >> 3) & 3) * 8;
     const __bf16 *wrow = a.w + (size_t)(n0 + wn) * a.K + wq;
     auto wload = [&](int cc, int t) -> bf16x8 {
         return *reinterpret_cast<const bf16x8 *>(wrow + t * a.cinp + cc * BF_BK);
@@ -2715,7 +2734,7 @@ constexpr int C3F_BK = 16, C3F_NI = 4, C3F_LD = 20;
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
 {
-    __shared__ __attribute__((aligned(16))) float Hs[2][C3_ROWS + 1][C3F_LD];    // + a zero row (k_conv3_bf16)
+    __shared__ __attribute__((aligned(16))) float Hs[2][C3_ZROW + 16][C3F_LD];   // + 16 zero rows (k_conv3_bf16)
     __shared__ __attribute__((aligned(16))) float Ws[2][C3_BN][C3F_LD];
     const rdq_conv_desc &d = a.d;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2764,7 +2783,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
     };
     // weight role: row wn (of 64), channels wq .. wq + 3 of the chunk (cin % 8 == 0: all four inside or
     // all outside the input channels)
-    const int wn = tid >> 2, wq = (tid & 3) * 4;
+    // (eight consecutive lanes: one piece of eight consecutive rows, conflict-free stashes as in
+    // k_conv3_bf16)
+    const int wn = (tid & 7) + 8 * (tid >> 5), wq = ((tid >> 3) & 3) * 4;
     const float *wrow = a.wf + (size_t)(n0 + wn) * cin * 9;
     auto wload = [&](int cc, int t) -> float4 {
         const int c = cc * C3F_BK + wq;
@@ -2805,8 +2826,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
 #pragma unroll
         for (int k = 0; k < C3F_NI; ++k) hstore(0, k, v[k]);
     }
-    if (tid < 2 * C3F_LD / 4)
-        reinterpret_cast<float4 *>(&Hs[tid / (C3F_LD / 4)][C3_ROWS][0])[tid % (C3F_LD / 4)] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (tid < 2 * 16 * C3F_LD / 4)
+        reinterpret_cast<float4 *>(&Hs[tid / (16 * C3F_LD / 4)][C3_ZROW][0])[tid % (16 * C3F_LD / 4)] = float4{0.0f, 0.0f, 0.0f, 0.0f};
     float4 wr[3];
     wr[0] = wload(0, 0);
     wr[1] = wload(0, 1);
@@ -2833,8 +2854,11 @@ __global__ __launch_bounds__(256, 2) void k_conv3_f32(C3Args a)
             const int toff = (t / 3) * d.W + t % 3;
             const float *wsb = &Ws[s & 1][0][0];
             int hrow[2];
+            // bank-matched zero row (C3_ZROW): pl[mb] = 64 wv + 32 mb + (lane & 31), so the regular row's
+            // residue mod 16 is the same for both mb
+            const int zr = (((lane & 15) + toff) & 15) | C3_ZROW;
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb) hrow[mb] = ((tmask[mb] >> t) & 1u) ? pl[mb] + toff : C3_ROWS;
+            for (int mb = 0; mb < 2; ++mb) hrow[mb] = ((tmask[mb] >> t) & 1u) ? pl[mb] + toff : zr;
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
                 const int kk = 8 * q2 + kg;

@@ -61,6 +61,7 @@ def test_fwi_op_autograd_is_the_adjoint(cuda, fwi_plan):
 
 
 def test_unet_and_loop_ops_opcheck(cuda):
+    import red_diffeq.ops  # noqa: F401  (registers torch.ops.red_diffeq.*; the test may run alone)
     ops = torch.ops.red_diffeq
     g = torch.Generator().manual_seed(1)
 
