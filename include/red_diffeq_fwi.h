@@ -114,6 +114,11 @@ int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
  * narrow chunked adjoints' depth only.  A time loop whose nt is not a multiple of the depth ends with
  * one shorter launch of its own depth.  Results are identical for every depth. */
 int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *plan, int32_t steps);
+/* Shots per workgroup of the WIDE chunked adjoint (1..64, or 0 = auto, the default: the largest of
+ * 8 / 4 / 2 / 1 whose launch rounds fill the CUs as well as the best): a workgroup runs that many
+ * shots of one region in turn and generates the region's alpha / kappa once for all of them.
+ * Results are identical for every setting. */
+int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *plan, int32_t shots);
 /* Rows per wave of the 64 x 96-region persistent kernels: forward 6, 8, 12 or 24 (16, 12, 8 or 4
  * waves per workgroup), adjoint (FMA build) 6, 8 or 12.  Same region geometry and results.  The time
  * step is latency-bound, so more resident waves win (configs[1], tools/ab_rw.sh, tools/ab_adj_nb6.sh):

@@ -561,6 +561,7 @@ struct AdjTBArgs {
     double *gk_part;                     // [B*ns][nblk]
     float *gbeta;                        // [B*ns]
     int k0, nsteps, nblk;
+    int spw, ns_sh;                      // wide kernels: shots per workgroup, shots of the launch's chain
     float w[ADJ_W_MAX];                  // w[k0-1-t], t < nsteps (narrow: <= TB_MAXT, wide: <= TW_ADJ_MAXT steps)
 };
 
@@ -932,15 +933,23 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
 {
     __shared__ f32x2 xq[2][NW][4][64];
     __shared__ f32x2 xp[2][NW][4][64];
+    __shared__ f32x2 As[NW][R][64];      // alpha of the wave's own rows (wave-private: no barrier), in LDS
+                                         // instead of 8 VGPRs live across the shot loop
     TW_REGION_INIT()
-    f32x2 A[R], KP[R], L0[R], L1[R], GA[R];   // temp1 / temp2 re-derived per step (bit-identical)
+    // this workgroup's shots: group jg of the model's shots (a.spw each), all on the same region, so
+    // alpha / kappa are generated once for all of them (~10 ms of the adjoint at configs[4] when every
+    // shot's workgroup generated its own: profiles/r5/configs4_adj_coef_ab.jsonl)
+    const int jg = s - g.s_off, s_first = g.s_off + jg * a.spw, nsh = min(a.spw, a.ns_sh - jg * a.spw);
+    (void)bs; (void)so;
+    f32x2 KP[R];                         // temp1 / temp2 re-derived per step (bit-identical)
     unsigned pmask = 0, smask = 0, rmask = 0;            // wave-uniform row masks
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3}, kC1X2 = {C1X2, C1X2}, k2 = {2.0f, 2.0f}, k1 = {1.0f, 1.0f};
-    f32x2 Pn[R];
+    // history P_{k-1}: only the columns the own cells' gradient stencil reaches (own +- 2: lanes H/2 - 1
+    // .. 64 - H/2), the other halo lanes' loads are out of range (no memory access, zeros): 112 of 128
+    // columns at T = 5, the history being the adjoint's largest stream
+    const bool plane = lane >= H / 2 - 1 && lane < 64 - H / 2 + 1;
+    const int pv0 = plane ? v0 : OOB, pv1 = plane ? v1 : OOB;
     {
-        const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(a.in_l1 + so, sbytes), RL2 = rsrc_of(a.in_l2 + so, sbytes);
-        const __amdgpu_buffer_rsrc_t RG = rsrc_of(a.gA + so, sbytes);
-        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)a.k0 * g.level + so, sbytes);
         int gz[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -954,49 +963,64 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
 #pragma unroll
         for (int r = 0; r < R; ++r) { c0[r] = gen_coef(a.cg, b, gz[r], gx0); c1[r] = gen_coef(a.cg, b, gz[r], gx1); }
 #pragma unroll
+        for (int r = 0; r < R; ++r) { As[w][r][lane] = f32x2{c0[r].al, c1[r].al}; KP[r] = f32x2{c0[r].kp, c1[r].kp}; }
+    }
+    const int rcv0 = rmask ? g.rlane[gx0] : -1, rcv1 = rmask ? g.rlane[gx1] : -1;
+    for (int sh = 0; sh < nsh; ++sh) {
+    // kernel arguments re-read from the kernarg segment per shot (an opaque pointer): kept live across
+    // the shot loop they exhaust the SGPRs and spill
+    const __attribute__((address_space(4))) AdjTBArgs *ka =
+        (const __attribute__((address_space(4))) AdjTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
+    const size_t soo = (size_t)bss * ka->g.slice;
+    if (sh) __syncthreads();             // the previous shot's gk reduction has read the exchange LDS
+    f32x2 L0[R], L1[R], GA[R], Pn[R];
+    {
+        const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(ka->in_l1 + soo, sbytes), RL2 = rsrc_of(ka->in_l2 + soo, sbytes);
+        const __amdgpu_buffer_rsrc_t RG = rsrc_of(ka->gA + soo, sbytes);
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(ka->hist + (size_t)ka->k0 * ka->g.level + soo, sbytes);
+#pragma unroll
         for (int r = 0; r < R; ++r) L1[r] = ld2<PAIR>(RL1, v0, v1, rofs[r] * 4);   // L_{k+1}
 #pragma unroll
         for (int r = 0; r < R; ++r) L0[r] = ld2<PAIR>(RL2, v0, v1, rofs[r] * 4);   // L_{k+2}
 #pragma unroll
-        for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, v0, v1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
+        for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, pv0, pv1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
 #pragma unroll
         for (int r = 0; r < R; ++r) GA[r] = (rin & (1u << r)) ? ld2<PAIR>(RG, vi0, vi1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
-#pragma unroll
-        for (int r = 0; r < R; ++r) { A[r] = f32x2{c0[r].al, c1[r].al}; KP[r] = f32x2{c0[r].kp, c1[r].kp}; }
     }
-    const int isx = g.isx[s];
+    const int isx = ka->g.isx[ss];
     const bool sc0 = xin0 && gx0 == isx, sc1 = xin1 && gx1 == isx;   // the source cell is an own cell
-    const int rcv0 = rmask ? g.rlane[gx0] : -1, rcv1 = rmask ? g.rlane[gx1] : -1;
-    const __amdgpu_buffer_rsrc_t DSR = rsrc_of(a.dseis + (size_t)bs * g.nrec * g.dstride);
+    const __amdgpu_buffer_rsrc_t DSR = rsrc_of(ka->dseis + (size_t)bss * ka->g.nrec * ka->g.dstride);
     const bool gbl = (smask & rin) && (sc0 || sc1);
-    float gbacc = gbl ? a.gbeta[bs] : 0.0f;
+    float gbacc = gbl ? ka->gbeta[bss] : 0.0f;
     double ksum = 0.0;                   // every gk term in fp64
 #pragma unroll
     for (int t = 0; t < T; ++t) {       // exactly T steps (the host launches a shorter tail as its own T)
         __builtin_amdgcn_sched_barrier(0);  // no step's work moved into another (live ranges: no spills)
-        const int k = a.k0 - t;
+        const int k = ka->k0 - t;
         f32x2 *cur = (t & 1) ? L0 : L1;     // L_{k+1}
         f32x2 *prv = (t & 1) ? L1 : L0;     // L_{k+2} -> L_k
         f32x2 P[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) P[r] = Pn[r];
         if (t + 1 < T) {   // history P_{k-2} of the next step, on the rows the interior's stencil needs
-            const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)(k - 1) * g.level + so, sbytes);
+            const __amdgpu_buffer_rsrc_t HR = rsrc_of(ka->hist + (size_t)(k - 1) * ka->g.level + soo, sbytes);
 #pragma unroll
-            for (int r = 0; r < R; ++r) if (pmask & (1u << r)) Pn[r] = ld2<PAIR>(HR, v0, v1, rofs[r] * 4);
+            for (int r = 0; r < R; ++r) if (pmask & (1u << r)) Pn[r] = ld2<PAIR>(HR, pv0, pv1, rofs[r] * 4);
         }
         // this step's receiver residuals, loaded before the stencil so their latency hides under it
-        const int ri = rmask ? rec_index(k - 1, g.st) : -1;   // wave-uniform
+        const int ri = rmask ? rec_index(k - 1, ka->g.st) : -1;   // wave-uniform
         f32x2 dsv = {-0.0f, -0.0f};
         if (ri >= 0) {
-            const int ro = ri * g.dstride;
+            const int ro = ri * ka->g.dstride;
             const float d0 = bload(DSR, rcv0 >= 0 ? (ro + rcv0) * 4 : OOB, 0);
             const float d1 = bload(DSR, rcv1 >= 0 ? (ro + rcv1) * 4 : OOB, 0);
             dsv = f32x2{rcv0 >= 0 ? d0 : -0.0f, rcv1 >= 0 ? d1 : -0.0f};
         }
         f32x2 q[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) q[r] = A[r] * cur[r];
+        for (int r = 0; r < R; ++r) q[r] = As[w][r][lane] * cur[r];
         tw_put<NW, R>(xq, t & 1, w, lane, q);
         tw_put<NW, R>(xp, t & 1, w, lane, P);
         __syncthreads();
@@ -1010,13 +1034,13 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
             f32x2 n2 = qm2 + qp2; n2 = n2 + x.l2; n2 = n2 + x.r2;
             if constexpr (EXACT) {
                 f32x2 nb = kC2 * n1; const f32x2 nb2 = kC3 * n2; nb = nb + nb2;
-                f32x2 t1 = kC1X2 * A[r]; t1 = t1 + k2; t1 = t1 - KP[r];      // pde.py:69
+                f32x2 t1 = kC1X2 * As[w][r][lane]; t1 = t1 + k2; t1 = t1 - KP[r];      // pde.py:69
                 const f32x2 t2 = k1 - KP[r];                                  // pde.py:70
                 f32x2 l = t1 * cur[r]; const f32x2 l2 = t2 * prv[r]; l = l - l2; l = l + nb;
                 prv[r] = l;
             } else {
                 const f32x2 nb = fma2(kC3, n2, kC2 * n1);
-                const f32x2 t1 = fma2(kC1X2, A[r], k2) - KP[r], t2 = k1 - KP[r];
+                const f32x2 t1 = fma2(kC1X2, As[w][r][lane], k2) - KP[r], t2 = k1 - KP[r];
                 prv[r] = fma2(t1, cur[r], fma2(-t2, prv[r], nb));
             }
         }
@@ -1051,13 +1075,13 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
                 ksum += (double)(xin0 ? kk.x : 0.0f);                   //  cancels: fp32 partials lost
                 ksum += (double)(xin1 ? kk.y : 0.0f);                   //  1.3e-4 of it at OpenFWI)
             }
-            if ((smask & (1u << r)) && (sc0 || sc1)) { const float gb = (sc0 ? l.x : l.y) * a.w[t]; gbacc = gbacc + gb; }
+            if ((smask & (1u << r)) && (sc0 || sc1)) { const float gb = (sc0 ? l.x : l.y) * ka->w[t]; gbacc = gbacc + gb; }
         }
     }
     {
         constexpr bool odd = (T & 1) != 0;      // newest level (L_{k0-T+1}) is in L0 if odd
-        const __amdgpu_buffer_rsrc_t O1 = rsrc_of(a.out_l1 + so, sbytes), O2 = rsrc_of(a.out_l2 + so, sbytes);
-        const __amdgpu_buffer_rsrc_t RG = rsrc_of(a.gA + so, sbytes);
+        const __amdgpu_buffer_rsrc_t O1 = rsrc_of(ka->out_l1 + soo, sbytes), O2 = rsrc_of(ka->out_l2 + soo, sbytes);
+        const __amdgpu_buffer_rsrc_t RG = rsrc_of(ka->gA + soo, sbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (rin & (1u << r)) {
@@ -1066,7 +1090,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
                 st2<PAIR>(GA[r], RG, vi0, vi1, rofs[r] * 4);
             }
     }
-    if (gbl) a.gbeta[bs] = gbacc;
+    if (gbl) ka->gbeta[bss] = gbacc;
     // deterministic workgroup reduction of the sponge-coefficient partial sum: a fixed xor tree per
     // wave, then the NW wave sums in wave order (LDS of the exchange)
 #pragma unroll
@@ -1078,8 +1102,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
     if (threadIdx.x == 0) {
         double tot = red[0];
         for (int i = 1; i < NW; ++i) tot += red[i];
-        a.gk_part[(size_t)bs * a.nblk + ti.tile] += tot;
+        ka->gk_part[(size_t)bss * ka->nblk + ti.tile] += tot;
     }
+    }   // shots
 }
 #undef TW_VERT
 #undef TW_REGION_INIT
@@ -2453,6 +2478,7 @@ struct rdq_fwi_plan {
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int adj_Tw = 0;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT); 0 = auto, see wide_adj_depth
+    int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_adj_spw)
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
@@ -2498,6 +2524,34 @@ int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, 
 // at 6; contracted 111.2 ms vs 115.1-115.7 at 6).
 constexpr int TW_ADJ_DEFAULT = 5;
 int wide_adj_depth(const rdq_fwi_plan *p) { return p->adj_Tw > 0 ? p->adj_Tw : TW_ADJ_DEFAULT; }
+
+// Shots per workgroup of a wide adjoint launch over `regions` (models x tiles) of `ns` shots.  A
+// workgroup generates its region's alpha / kappa once for all its shots, so more is cheaper per shot
+// (configs[4], 16 shots: 1 -> 8 per workgroup 122 -> 100.8 ms; profiles/r5/configs4_adj_spw.jsonl),
+// but a workgroup of many shots is a long indivisible unit: choose the largest count up to 8 whose
+// rounds of one workgroup per CU waste no more slots than the best count's (+2 %).
+int wide_adj_spw(const rdq_fwi_plan *p, int regions, int ns)
+{
+    if (p->adj_spw > 0) return std::max(1, std::min(p->adj_spw, ns));
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    double best = 0.0;
+    double eff[4];
+    const int cand[4] = {8, 4, 2, 1};
+    for (int i = 0; i < 4; ++i) {
+        const int spw = std::min(cand[i], ns), groups = (ns + spw - 1) / spw;
+        const long long wgs = (long long)regions * groups, rounds = (wgs + cus - 1) / cus;
+        eff[i] = (double)regions * ns / ((double)rounds * cus * spw);
+        best = std::max(best, eff[i]);
+    }
+    for (int i = 0; i < 4; ++i)
+        if (eff[i] >= best - 0.02) return std::min(cand[i], ns);
+    return 1;
+}
 
 int ensure_aux(rdq_fwi_plan *p, int S)
 {
@@ -3009,6 +3063,9 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     for (int c = 0; c < S; ++c) {
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
+        // wide kernels: a workgroup runs a.spw shots of one region in turn (the decode's slice groups
+        // are then shot groups)
+        a.ns_sh = a.g.ns_grp;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
         for (int k0 = p->g.nt, i = 0; k0 >= 1; k0 -= T, ++i) {
             a.k0 = k0;
@@ -3016,6 +3073,8 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
             const int Tl = p->wide ? a.nsteps : T;
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
+            a.spw = p->wide ? wide_adj_spw(p, B * a.g.ntiles, a.ns_sh) : 1;
+            a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < ADJ_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
             const int pin = i & 1, pout = pin ^ 1;
@@ -3200,6 +3259,17 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     p->fwd_T = fwd_steps;
     p->adj_T = adj_steps;
     p->chains = chains;
+    return 0;
+}
+
+int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *p, int32_t shots)
+{
+    if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_adj_spw)
+    if (p->adj_spw != shots) {   // graphs encode the grids
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->adj_spw = shots;
     return 0;
 }
 

@@ -106,6 +106,12 @@ class FwiPlan:
         sets the persistent / narrow chunked adjoints' depth.  Results are identical for every depth."""
         _hip.check(self.lib.rdq_fwi_set_wide_adj_steps(self.handle, int(steps)), "rdq_fwi_set_wide_adj_steps")
 
+    def set_wide_adj_shots(self, shots):
+        """Shots per workgroup of the wide chunked adjoint (1..64; 0 = auto, the default: up to 8, chosen
+        so the launch's rounds fill the CUs; the region's alpha / kappa are generated once for all of
+        them).  Results are identical for every setting."""
+        _hip.check(self.lib.rdq_fwi_set_wide_adj_shots(self.handle, int(shots)), "rdq_fwi_set_wide_adj_shots")
+
     def set_rows_per_wave(self, fwd_rows, adj_rows):
         """Rows per wave of the 64 x 96-region persistent kernels (forward 6 / 8 / 12 / 24, adjoint
         6 / 8 / 12; 6 is the default for both); results are the same for every choice."""

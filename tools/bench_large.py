@@ -8,6 +8,7 @@ Prints one JSON line per blocking depth: forward / adjoint ms, shot-timesteps/s,
 (12·Npad B per forward shot-step, 16·Npad B per adjoint shot-step).
 python tools/bench_large.py [--ns 16] [--nz 500] [--nx 3000] [--nt 1000] [--reps 2]"""
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -32,9 +33,13 @@ ap.add_argument("--narrow", action="store_true", help="64-column chunked regions
 ap.add_argument("--exact", action="store_true", help="exact-order adjoint (RDQ_VARIANT_ADJ_EXACT)")
 ap.add_argument("--chunked-adj-fma", action="store_true", help="contracted wide chunked adjoint (RDQ_VARIANT_CHUNKED_ADJ_FMA)")
 ap.add_argument("--Tw", type=int, default=0, help="wide chunked adjoint depth (rdq_fwi_set_wide_adj_steps; 0 = auto)")
+ap.add_argument("--spw", type=int, default=0, help="wide adjoint shots per workgroup (0: the plan's default)")
 ap.add_argument("--chains", type=int, default=1, help="concurrent shot-group launch chains")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
+ap.add_argument("--phase", action="store_true",
+                help="timing-only builds (RDQ_HIP_LIB) exporting rdq_exp_adj_phase: per-workgroup phase split of the "
+                     "wide adjoint (launch start -> step 0's exchange, steps, epilogue), mean us per workgroup")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = dict(n_grid=a.nx, nt=a.nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=a.nx, ns=a.ns)
@@ -44,6 +49,8 @@ plan = fwi._plan(a.nz, a.nx, dev)
 plan.set_variant(fwd_gen_coeffs=not a.no_gen, wide_chunked=not a.narrow, adj_exact=a.exact,
                  chunked_adj_fma=a.chunked_adj_fma)
 plan.set_wide_adj_steps(a.Tw)
+if a.spw:
+    plan.set_wide_adj_shots(a.spw)
 sz = plan.sizes(1)
 npad = sz.Hp * sz.Wp
 dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
@@ -59,9 +66,20 @@ for T in [int(t) for t in a.T.split(",")]:
         ev[0].record()
         seis, hist = plan.forward(coeffs, 1, keep_history=True)
         ev[1].record()
+        if a.phase and i == a.reps:
+            torch.cuda.synchronize()
+            ph = (ctypes.c_uint64 * 8)()
+            plan.lib.rdq_exp_adj_phase(ph)          # read-and-reset
         plan.adjoint(coeffs, hist, dseis, 1)
         ev[2].record()
         torch.cuda.synchronize()
+        if a.phase and i == a.reps:
+            plan.lib.rdq_exp_adj_phase(ph)
+            n = max(1, ph[3])
+            print(json.dumps({"adj_phase_us_per_wg": {"start_to_step0_exchange": round(ph[0] / n / 100, 3),
+                                                      "steps_after": round(ph[1] / n / 100, 3),
+                                                      "epilogue": round(ph[2] / n / 100, 3)},
+                              "workgroups": n}), flush=True)
         del hist
         if i:
             fw.append(ev[0].elapsed_time(ev[1]))
@@ -69,7 +87,7 @@ for T in [int(t) for t in a.T.split(",")]:
     plan.status()
     f, d = min(fw), min(ad)
     shot_steps = a.ns * a.nt
-    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chunked_adj_fma": a.chunked_adj_fma, "Tw": a.Tw, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chunked_adj_fma": a.chunked_adj_fma, "Tw": a.Tw, "spw": a.spw, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
                       "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
                       "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
                       "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
