@@ -254,6 +254,7 @@ struct FwdTBArgs {
     float *out_prev, *out_cur;           // ring path: P_{n+T-1}, P_{n+T}
     float *seis;
     int n0, nsteps;
+    int spw, ns_sh;                      // wide kernels: shots per workgroup, shots of the launch's chain
     float w[TB_MAXT];                    // wavelet samples w[n0 .. n0+nsteps-1]
 };
 
@@ -824,13 +825,17 @@ template <int T, int NW, int R, bool GEN, bool PAIR>
 __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
 {
     __shared__ f32x2 xch[2][NW][4][64];
+    __shared__ f32x2 As[NW][R][64];      // alpha of the wave's own rows (wave-private), as k_adj_tw
     TW_REGION_INIT()
-    const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[R], C1[R], C2v[R], P0[R], P1[R];
+    // this workgroup's shots: a.spw of the model's shots on one region (k_adj_tw): the coefficients
+    // are generated once for all of them
+    const int jg = s - g.s_off, s_first = g.s_off + jg * a.spw, nsh = min(a.spw, a.ns_sh - jg * a.spw);
+    (void)bs; (void)so;
+    f32x2 C1[R], C2v[R];
     unsigned smask = 0;
     int rrow = -1;
     {
-        const __amdgpu_buffer_rsrc_t RPv = rsrc_of(a.in_prev + so, sbytes), RCu = rsrc_of(a.in_cur + so, sbytes);
+        const float *AL = a.coeffs + (size_t)b * g.slice;
         const __amdgpu_buffer_rsrc_t RA = rsrc_of(AL, sbytes), R1 = rsrc_of(AL + g.cstride, sbytes),
                                      R2 = rsrc_of(AL + 2 * g.cstride, sbytes);
 #pragma unroll
@@ -838,27 +843,42 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
             const int gz = wrapn(uz0 + r, g.Hp);
             if constexpr (GEN) {   // regenerated from the 20 KB-per-row model (L2-resident) instead of 3 fields
                 const Coef c0 = gen_coef(a.cg, b, gz, gx0), c1 = gen_coef(a.cg, b, gz, gx1);
-                A[r] = f32x2{c0.al, c1.al}; C1[r] = f32x2{c0.t1, c1.t1}; C2v[r] = f32x2{c0.t2, c1.t2};
+                As[w][r][lane] = f32x2{c0.al, c1.al}; C1[r] = f32x2{c0.t1, c1.t1}; C2v[r] = f32x2{c0.t2, c1.t2};
             } else {
-                A[r] = ld2<PAIR>(RA, v0, v1, rofs[r] * 4);
+                As[w][r][lane] = ld2<PAIR>(RA, v0, v1, rofs[r] * 4);
                 C1[r] = ld2<PAIR>(R1, v0, v1, rofs[r] * 4);
                 C2v[r] = ld2<PAIR>(R2, v0, v1, rofs[r] * 4);
             }
-            P0[r] = ld2<PAIR>(RPv, v0, v1, rofs[r] * 4);
-            P1[r] = ld2<PAIR>(RCu, v0, v1, rofs[r] * 4);
             if (gz == g.isz) smask |= 1u << r;          // (tiny domains: a wave can hold the row twice)
             if (gz == g.igz) rrow = r;
         }
     }
-    const int isx = g.isx[s];
-    const bool sc0 = gx0 == isx, sc1 = gx1 == isx;
-    const float bsrc = smask ? a.coeffs[4 * g.cstride + (size_t)b * g.slice + (size_t)g.isz * g.ld + isx] : 0.0f;
     // receivers of the lane's two columns (usually one each), read once
     int rs0 = 0, re0 = 0, rs1 = 0, re1 = 0;
     if (rrow >= 0) { rs0 = g.rcv_start[gx0]; re0 = g.rcv_start[gx0 + 1]; rs1 = g.rcv_start[gx1]; re1 = g.rcv_start[gx1 + 1]; }
     const int rc0 = xin0 && rs0 < re0 ? g.rcv_list[rs0] : -1, rc1 = xin1 && rs1 < re1 ? g.rcv_list[rs1] : -1;
     const bool rmulti = __any(re0 - rs0 > 1 || re1 - rs1 > 1);   // wave-uniform
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
+    for (int sh = 0; sh < nsh; ++sh) {
+    // kernel arguments re-read from the kernarg segment per shot (k_adj_tw)
+    const __attribute__((address_space(4))) FwdTBArgs *ka =
+        (const __attribute__((address_space(4))) FwdTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
+    const size_t soo = (size_t)bss * ka->g.slice;
+    if (sh) __syncthreads();             // the previous shot's last exchange has been read
+    f32x2 P0[R], P1[R];
+    {
+        const __amdgpu_buffer_rsrc_t RPv = rsrc_of(ka->in_prev + soo, sbytes), RCu = rsrc_of(ka->in_cur + soo, sbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            P0[r] = ld2<PAIR>(RPv, v0, v1, rofs[r] * 4);
+            P1[r] = ld2<PAIR>(RCu, v0, v1, rofs[r] * 4);
+        }
+    }
+    const int isx = ka->g.isx[ss];
+    const bool sc0 = gx0 == isx, sc1 = gx1 == isx;
+    const float bsrc = smask ? ka->coeffs[4 * ka->g.cstride + (size_t)b * ka->g.slice + (size_t)ka->g.isz * ka->g.ld + isx] : 0.0f;
 #pragma unroll
     for (int t = 0; t < T; ++t) {       // exactly T steps (the host launches a shorter tail as its own T)
         f32x2 *cur = (t & 1) ? P0 : P1;     // P_{n+t}
@@ -876,39 +896,39 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
             f32x2 s2 = zm2 + zp2; s2 = s2 + x.l2; s2 = s2 + x.r2;
             f32x2 lap = kC2 * s1; const f32x2 l2 = kC3 * s2; lap = lap + l2;
             f32x2 a1 = C1[r] * c; const f32x2 a2 = C2v[r] * prv[r]; a1 = a1 - a2;
-            const f32x2 a3 = A[r] * lap;
+            const f32x2 a3 = As[w][r][lane] * lap;
             prv[r] = a1 + a3;
         }
         if (smask) {                                                   // pde.py:80-81
-            const float add = bsrc * a.w[t];
+            const float add = bsrc * ka->w[t];
             const f32x2 av = {sc0 ? add : -0.0f, sc1 ? add : -0.0f};   // x + (-0) == x bit for bit
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (smask & (1u << r)) prv[r] = prv[r] + av;
         }
-        const int n = a.n0 + t;
-        if (a.hist) {
-            const __amdgpu_buffer_rsrc_t HS = rsrc_of(a.hist + (size_t)(n + 2) * g.level + so, sbytes);
+        const int n = ka->n0 + t;
+        if (ka->hist) {
+            const __amdgpu_buffer_rsrc_t HS = rsrc_of(ka->hist + (size_t)(n + 2) * ka->g.level + soo, sbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (rin & (1u << r)) st2<PAIR, CP_NT>(prv[r], HS, vi0, vi1, rofs[r] * 4);   // streaming
         }
-        if (rrow >= 0 && (rin & (1u << rrow)) && (n % g.st) == 0) {   // pde.py:82-83
+        if (rrow >= 0 && (rin & (1u << rrow)) && (n % ka->g.st) == 0) {   // pde.py:82-83
             f32x2 val = prv[0];
 #pragma unroll
             for (int r = 1; r < R; ++r) if (r == rrow) val = prv[r];
-            float *SK = a.seis + ((size_t)bs * g.nrec + n / g.st) * g.ng;
+            float *SK = ka->seis + ((size_t)bss * ka->g.nrec + n / ka->g.st) * ka->g.ng;
             if (rc0 >= 0) SK[rc0] = val.x;
             if (rc1 >= 0) SK[rc1] = val.y;
             if (rmulti) {
-                if (xin0) for (int j = rs0 + 1; j < re0; ++j) SK[g.rcv_list[j]] = val.x;
-                if (xin1) for (int j = rs1 + 1; j < re1; ++j) SK[g.rcv_list[j]] = val.y;
+                if (xin0) for (int j = rs0 + 1; j < re0; ++j) SK[ka->g.rcv_list[j]] = val.x;
+                if (xin1) for (int j = rs1 + 1; j < re1; ++j) SK[ka->g.rcv_list[j]] = val.y;
             }
         }
     }
-    if (a.out_cur) {   // ring path: keep the last two levels
+    if (ka->out_cur) {   // ring path: keep the last two levels
         constexpr bool odd = (T & 1) != 0;      // after T steps the newest level is in P0 if odd
-        const __amdgpu_buffer_rsrc_t OC = rsrc_of(a.out_cur + so, sbytes), OP = rsrc_of(a.out_prev + so, sbytes);
+        const __amdgpu_buffer_rsrc_t OC = rsrc_of(ka->out_cur + soo, sbytes), OP = rsrc_of(ka->out_prev + soo, sbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (rin & (1u << r)) {
@@ -916,6 +936,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
                 st2<PAIR>(odd ? P1[r] : P0[r], OP, vi0, vi1, rofs[r] * 4);
             }
     }
+    }   // shots
 }
 
 // Adjoint on wide regions (k_adj_tb's per-cell arithmetic):
@@ -2478,7 +2499,8 @@ struct rdq_fwi_plan {
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int adj_Tw = 0;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT); 0 = auto, see wide_adj_depth
-    int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_adj_spw)
+    int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_spw)
+    int fwd_spw = 0;            // the wide chunked forward's, 0 = auto
     int chains = 1;             // independent shot groups launched as concurrent chains
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
@@ -2525,32 +2547,32 @@ int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, 
 constexpr int TW_ADJ_DEFAULT = 5;
 int wide_adj_depth(const rdq_fwi_plan *p) { return p->adj_Tw > 0 ? p->adj_Tw : TW_ADJ_DEFAULT; }
 
-// Shots per workgroup of a wide adjoint launch over `regions` (models x tiles) of `ns` shots.  A
-// workgroup generates its region's alpha / kappa once for all its shots, so more is cheaper per shot
-// (configs[4], 16 shots: 1 -> 8 per workgroup 122 -> 100.8 ms; profiles/r5/configs4_adj_spw.jsonl),
-// but a workgroup of many shots is a long indivisible unit: choose the largest count up to 8 whose
-// rounds of one workgroup per CU waste no more slots than the best count's (+2 %).
-int wide_adj_spw(const rdq_fwi_plan *p, int regions, int ns)
+// Shots per workgroup of a wide forward / adjoint launch over `regions` (models x tiles) of `ns` shots.  A
+// workgroup generates its region's coefficients once for all its shots and pays its fixed start-up
+// once, so more is cheaper per shot, but a workgroup of many shots is a long indivisible unit.  Cost
+// model: rounds of one workgroup per CU x (shots per workgroup + KAPPA), KAPPA = a workgroup's fixed
+// cost in shots (fitted at configs[4]: forward 0.6, adjoint 0.25; profiles/r5/configs4_adj_spw.jsonl,
+// configs4_fwd_spw.jsonl); the cheapest of 8 / 4 / 2 / 1 (ties: more shots).  configs[4] (16 shots, 203
+// forward / 510 adjoint regions): 8 for both; a small grid (20 regions) keeps 1 for parallelism.
+int wide_spw(int setting, int regions, int ns)
 {
-    if (p->adj_spw > 0) return std::max(1, std::min(p->adj_spw, ns));
+    if (setting > 0) return std::max(1, std::min(setting, ns));
     static int cus = 0;
     if (!cus) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
     }
-    double best = 0.0;
-    double eff[4];
-    const int cand[4] = {8, 4, 2, 1};
-    for (int i = 0; i < 4; ++i) {
-        const int spw = std::min(cand[i], ns), groups = (ns + spw - 1) / spw;
+    constexpr double KAPPA = 0.5;
+    int pick = 1;
+    double best = 1e300;
+    for (const int c : {8, 4, 2, 1}) {
+        const int spw = std::min(c, ns), groups = (ns + spw - 1) / spw;
         const long long wgs = (long long)regions * groups, rounds = (wgs + cus - 1) / cus;
-        eff[i] = (double)regions * ns / ((double)rounds * cus * spw);
-        best = std::max(best, eff[i]);
+        const double cost = (double)rounds * (spw + KAPPA);
+        if (cost < best - 1e-9) { best = cost; pick = spw; }
     }
-    for (int i = 0; i < 4; ++i)
-        if (eff[i] >= best - 0.02) return std::min(cand[i], ns);
-    return 1;
+    return pick;
 }
 
 int ensure_aux(rdq_fwi_plan *p, int S)
@@ -3016,6 +3038,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
     for (int c = 0; c < S; ++c) {
         a.g.s_off = c * ns / S;
         a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
+        a.ns_sh = a.g.ns_grp;            // wide kernels: a.spw shots of one region per workgroup
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
         for (int n0 = 0, i = 0; n0 < nt; n0 += T, ++i) {
             a.n0 = n0;
@@ -3024,6 +3047,8 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
             const int Tl = p->wide ? a.nsteps : T;
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, false) : tiles_y(p->Hp, Tl));
+            a.spw = p->wide ? wide_spw(p->fwd_spw, B * a.g.ntiles, a.ns_sh) : 1;
+            a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
             if (hist) {
@@ -3073,7 +3098,7 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
             const int Tl = p->wide ? a.nsteps : T;
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
-            a.spw = p->wide ? wide_adj_spw(p, B * a.g.ntiles, a.ns_sh) : 1;
+            a.spw = p->wide ? wide_spw(p->adj_spw, B * a.g.ntiles, a.ns_sh) : 1;
             a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < ADJ_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
@@ -3262,9 +3287,20 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     return 0;
 }
 
+int rdq_fwi_set_wide_fwd_shots(rdq_fwi_plan *p, int32_t shots)
+{
+    if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_spw)
+    if (p->fwd_spw != shots) {   // graphs encode the grids
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->fwd_spw = shots;
+    return 0;
+}
+
 int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *p, int32_t shots)
 {
-    if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_adj_spw)
+    if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_spw)
     if (p->adj_spw != shots) {   // graphs encode the grids
         drop_graphs(p);
         p->cache.clear();

@@ -112,6 +112,10 @@ class FwiPlan:
         them).  Results are identical for every setting."""
         _hip.check(self.lib.rdq_fwi_set_wide_adj_shots(self.handle, int(shots)), "rdq_fwi_set_wide_adj_shots")
 
+    def set_wide_fwd_shots(self, shots):
+        """Shots per workgroup of the wide chunked forward (as set_wide_adj_shots; 0 = auto)."""
+        _hip.check(self.lib.rdq_fwi_set_wide_fwd_shots(self.handle, int(shots)), "rdq_fwi_set_wide_fwd_shots")
+
     def set_rows_per_wave(self, fwd_rows, adj_rows):
         """Rows per wave of the 64 x 96-region persistent kernels (forward 6 / 8 / 12 / 24, adjoint
         6 / 8 / 12; 6 is the default for both); results are the same for every choice."""
