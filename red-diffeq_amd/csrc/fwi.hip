@@ -859,23 +859,34 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
     const int rc0 = xin0 && rs0 < re0 ? g.rcv_list[rs0] : -1, rc1 = xin1 && rs1 < re1 ? g.rcv_list[rs1] : -1;
     const bool rmulti = __any(re0 - rs0 > 1 || re1 - rs1 > 1);   // wave-uniform
     const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
-    for (int sh = 0; sh < nsh; ++sh) {
-    // kernel arguments re-read from the kernarg segment per shot (k_adj_tw)
-    const __attribute__((address_space(4))) FwdTBArgs *ka =
-        (const __attribute__((address_space(4))) FwdTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ka));
-    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
-    const size_t soo = (size_t)bss * ka->g.slice;
-    if (sh) __syncthreads();             // the previous shot's last exchange has been read
+    // kernel arguments re-read from the kernarg segment per shot (k_adj_tw); a shot's two input levels
+    // are loaded when the previous shot's last levels have been stored (k_adj_tw's pipelining)
+    auto kargs = [&]() {
+        const __attribute__((address_space(4))) FwdTBArgs *k_ =
+            (const __attribute__((address_space(4))) FwdTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(k_));
+        return k_;
+    };
     f32x2 P0[R], P1[R];
-    {
-        const __amdgpu_buffer_rsrc_t RPv = rsrc_of(ka->in_prev + soo, sbytes), RCu = rsrc_of(ka->in_cur + soo, sbytes);
+    auto load_shot = [&](int ss_) {
+        const auto *k_ = kargs();
+        const size_t so_ = (size_t)(b * k_->g.ns + ss_) * k_->g.slice;
+        const __amdgpu_buffer_rsrc_t RPv = rsrc_of(k_->in_prev + so_, sbytes), RCu = rsrc_of(k_->in_cur + so_, sbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             P0[r] = ld2<PAIR>(RPv, v0, v1, rofs[r] * 4);
             P1[r] = ld2<PAIR>(RCu, v0, v1, rofs[r] * 4);
         }
-    }
+    };
+    load_shot(s_first);
+    for (int sh = 0; sh < nsh; ++sh) {
+    const auto *ka = kargs();
+    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
+    const size_t soo = (size_t)bss * ka->g.slice;
+    // an odd T ends on exchange buffer 0, which the next shot's first step rewrites: wait for every
+    // wave's last halo reads (an even T ends on buffer 1, and buffer 0's last reads precede the last
+    // step's barrier)
+    if ((T & 1) && sh) __syncthreads();
     const int isx = ka->g.isx[ss];
     const bool sc0 = gx0 == isx, sc1 = gx1 == isx;
     const float bsrc = smask ? ka->coeffs[4 * ka->g.cstride + (size_t)b * ka->g.slice + (size_t)ka->g.isz * ka->g.ld + isx] : 0.0f;
@@ -936,6 +947,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_tw(FwdTBArgs a)
                 st2<PAIR>(odd ? P1[r] : P0[r], OP, vi0, vi1, rofs[r] * 4);
             }
     }
+    if (sh + 1 < nsh) load_shot(ss + 1);
     }   // shots
 }
 
@@ -987,20 +999,23 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
         for (int r = 0; r < R; ++r) { As[w][r][lane] = f32x2{c0[r].al, c1[r].al}; KP[r] = f32x2{c0[r].kp, c1[r].kp}; }
     }
     const int rcv0 = rmask ? g.rlane[gx0] : -1, rcv1 = rmask ? g.rlane[gx1] : -1;
-    for (int sh = 0; sh < nsh; ++sh) {
-    // kernel arguments re-read from the kernarg segment per shot (an opaque pointer): kept live across
-    // the shot loop they exhaust the SGPRs and spill
-    const __attribute__((address_space(4))) AdjTBArgs *ka =
-        (const __attribute__((address_space(4))) AdjTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ka));
-    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
-    const size_t soo = (size_t)bss * ka->g.slice;
-    if (sh) __syncthreads();             // the previous shot's gk reduction has read the exchange LDS
+    // a shot's launch-start loads (levels L_{k0+1}, L_{k0+2}, history P_{k0-1}, gA): shot 0's here,
+    // shot s+1's right after shot s's output stores, so they are in flight during shot s's gk
+    // reduction.  Kernel arguments are re-read from the kernarg segment (an opaque pointer) per
+    // shot: kept live across the shot loop they exhaust the SGPRs and spill.
     f32x2 L0[R], L1[R], GA[R], Pn[R];
-    {
-        const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(ka->in_l1 + soo, sbytes), RL2 = rsrc_of(ka->in_l2 + soo, sbytes);
-        const __amdgpu_buffer_rsrc_t RG = rsrc_of(ka->gA + soo, sbytes);
-        const __amdgpu_buffer_rsrc_t HR = rsrc_of(ka->hist + (size_t)ka->k0 * ka->g.level + soo, sbytes);
+    auto kargs = [&]() {
+        const __attribute__((address_space(4))) AdjTBArgs *k_ =
+            (const __attribute__((address_space(4))) AdjTBArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(k_));
+        return k_;
+    };
+    auto load_shot = [&](int ss_) {
+        const auto *k_ = kargs();
+        const size_t so_ = (size_t)(b * k_->g.ns + ss_) * k_->g.slice;
+        const __amdgpu_buffer_rsrc_t RL1 = rsrc_of(k_->in_l1 + so_, sbytes), RL2 = rsrc_of(k_->in_l2 + so_, sbytes);
+        const __amdgpu_buffer_rsrc_t RG = rsrc_of(k_->gA + so_, sbytes);
+        const __amdgpu_buffer_rsrc_t HR = rsrc_of(k_->hist + (size_t)k_->k0 * k_->g.level + so_, sbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r) L1[r] = ld2<PAIR>(RL1, v0, v1, rofs[r] * 4);   // L_{k+1}
 #pragma unroll
@@ -1009,7 +1024,15 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
         for (int r = 0; r < R; ++r) Pn[r] = (pmask & (1u << r)) ? ld2<PAIR>(HR, pv0, pv1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
 #pragma unroll
         for (int r = 0; r < R; ++r) GA[r] = (rin & (1u << r)) ? ld2<PAIR>(RG, vi0, vi1, rofs[r] * 4) : f32x2{0.0f, 0.0f};
-    }
+    };
+    load_shot(s_first);
+    for (int sh = 0; sh < nsh; ++sh) {
+    const auto *ka = kargs();
+    const int ss = s_first + sh, bss = b * ka->g.ns + ss;
+    const size_t soo = (size_t)bss * ka->g.slice;
+    // (no barrier between shots: the gk reduction's LDS words are wave 0's own exchange slot, which
+    //  only wave 0 rewrites, after its thread 0 has read them; the reduction's two barriers order the
+    //  last step's halo reads before the next shot's first exchange)
     const int isx = ka->g.isx[ss];
     const bool sc0 = xin0 && gx0 == isx, sc1 = xin1 && gx1 == isx;   // the source cell is an own cell
     const __amdgpu_buffer_rsrc_t DSR = rsrc_of(ka->dseis + (size_t)bss * ka->g.nrec * ka->g.dstride);
@@ -1111,6 +1134,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
                 st2<PAIR>(GA[r], RG, vi0, vi1, rofs[r] * 4);
             }
     }
+    if (sh + 1 < nsh) load_shot(ss + 1);
     if (gbl) ka->gbeta[bss] = gbacc;
     // deterministic workgroup reduction of the sponge-coefficient partial sum: a fixed xor tree per
     // wave, then the NW wave sums in wave order (LDS of the exchange)
@@ -1123,7 +1147,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_tw(AdjTBArgs a)
     if (threadIdx.x == 0) {
         double tot = red[0];
         for (int i = 1; i < NW; ++i) tot += red[i];
-        ka->gk_part[(size_t)bss * ka->nblk + ti.tile] += tot;
+        // one add per (slot, launch), launches in stream order: the same sum as a load-add-store, but
+        // without the load's round trip before the next shot's barrier
+        unsafeAtomicAdd(&ka->gk_part[(size_t)bss * ka->nblk + ti.tile], tot);
     }
     }   // shots
 }
