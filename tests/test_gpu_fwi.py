@@ -642,6 +642,65 @@ def test_wide_chunked_kernels_vs_oracle(cuda, nx, nbc, T, Tw):
     np.testing.assert_allclose(fma[3], oK, rtol=2e-5)
 
 
+@pytest.mark.parametrize("T", [4, 3])
+def test_wide_shots_per_workgroup_bitexact(cuda, T):
+    """The wide kernels' shot loop (several shots of one region per workgroup, the next shot's loads
+    issued during the previous shot's epilogue): every shots-per-workgroup setting, with a shot count
+    that does not divide the group (5 shots in 2 models), two concurrent chains (shot offsets) and
+    graph replays, gives the one-shot-per-workgroup results bit for bit (seismograms, gA, gbeta, gk),
+    and those equal the oracle's.  nt = 158: forward tails (T = 4: 2, T = 3: 2) and the adjoint's
+    (depth 5: 3) run their own instantiations."""
+    from red_diffeq.utils.synthetic import make_model
+    ctx = dict(n_grid=71, nt=158, dx=10.0, dt=0.001, nbc=20, f=15.0, sz=10, gz=10, ng=71, ns=5)
+    vn = vnorm(make_model("curvefault", 36, 71, seed=7, batch=2))
+    fwi = make_fwi(dict(ctx))
+    v = torch.from_numpy(vn).to(cuda)
+    plan = fwi._plan(36, 71, v.device)
+    B = 2
+    sz = plan.sizes(B)
+    rng = np.random.default_rng(17)
+    dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
+    dseis = torch.from_numpy(dseis_np).to(cuda)
+
+    def run(fspw, aspw, chains):
+        plan.set_persistent(False)
+        plan.set_variant(wide_chunked=True)
+        plan.set_tuning(T, T, chains)
+        plan.set_wide_adj_steps(0)
+        plan.set_wide_fwd_shots(fspw)
+        plan.set_wide_adj_shots(aspw)
+        outs = []
+        for _ in range(2):                       # capture, then a replay of the cached graphs
+            coeffs, _ = plan.coeffs(v, 0)
+            seis, hist = plan.forward(coeffs, B, keep_history=True)
+            gA, gk, gb = plan.adjoint(coeffs, hist, dseis, B)
+            plan.status()
+            outs.append((seis.cpu().numpy(), gA.view(B, plan.ns, sz.Hp, sz.ld)[..., :sz.Wp].cpu().numpy(),
+                         gb.view(B, -1).cpu().numpy(), gk.view(B, -1).sum(1).cpu().numpy()))
+        for a_, b_ in zip(outs[0][:3], outs[1][:3]):
+            assert bits_equal(a_, b_)
+        return outs[1]
+
+    try:
+        ref = run(1, 1, 1)
+        for fspw, aspw, chains in ((2, 2, 1), (3, 4, 1), (8, 8, 1), (2, 3, 2), (8, 8, 2), (0, 0, 1)):
+            got = run(fspw, aspw, chains)
+            for name, a_, b_ in zip(("seis", "gA", "gbeta"), got[:3], ref[:3]):
+                assert bits_equal(a_, b_), (fspw, aspw, chains, name)
+            np.testing.assert_allclose(got[3], ref[3], rtol=1e-12)
+    finally:
+        plan.set_wide_fwd_shots(0)
+        plan.set_wide_adj_shots(0)
+        plan.set_tuning(4, 4, 1)
+    f = O.OracleFWI(dict(ctx), B)
+    so, c = f.forward(vn, keep_history=True)
+    oA, oK, ob = f.adjoint(c, dseis_np)
+    assert bits_equal(ref[0], so)
+    assert bits_equal(_shot_sum(ref[1]), oA)
+    assert bits_equal(ref[2], ob)
+    np.testing.assert_allclose(ref[3], oK, rtol=1e-7)
+
+
 @pytest.mark.parametrize("wide", [True, False])
 def test_chunked_graph_replays_on_poisoned_buffers(cuda, wide):
     """Cached-graph REPLAYS of the chunked forward (history and ring forms) and adjoint on fixed
