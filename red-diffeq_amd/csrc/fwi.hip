@@ -55,35 +55,12 @@ constexpr float C3 = (float)(-1.0 / 12.0);         // pde.py:68
 // --------------------------------------------------------------------------------------- K3
 // vmin / first row-major argmin over the (unpadded) model; the padded field's first minimum
 // folds back to this cell (pde.py:41, torch.min tie rule = first index).
-__global__ __launch_bounds__(256) void k_vstat(const float *__restrict__ vn, int64_t s0, int64_t s2,
-                                               int64_t s3, int nz, int nx, int vel_mode, float lnk,
-                                               float two_a, float *vmin, int64_t *amin, float *ks)
+// vmin and its first argmin per model (torch.min's tie rule, pde.py:41), in two passes: gridDim.y parts
+// of each model reduce contiguous index ranges to (min, first index) partials, then one workgroup per
+// model combines them (a 1.5 M-cell configs[4] model took 630 us in one workgroup).  The comparison
+// (value, then index) is order-independent, so the result is the one-pass scan's bit for bit.
+__device__ __forceinline__ void vstat_reduce(float &best, int64_t &bi, float *sv, int64_t *si)
 {
-    const int b = blockIdx.x;
-    float best = INFINITY;
-    int64_t bi = INT64_MAX;
-    const int n = nz * nx;
-    // each thread's elements in its original order, loads issued 8 at a time (one dependent L2
-    // round trip per element had made this a 20-deep latency chain): same comparisons, same result
-    constexpr int CH = 8;
-    for (int base = threadIdx.x; base < n; base += CH * blockDim.x) {
-        float t[CH];
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int i = base + u * blockDim.x;
-            const int iz = i / nx, ix = i - iz * nx;
-            t[u] = i < n ? vn[b * s0 + iz * s2 + ix * s3] : INFINITY;
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int i = base + u * blockDim.x;
-            float v = t[u];
-            if (vel_mode == 0) { v = v + 1.0f; v = v / 2.0f; v = v * 3000.0f; v = v + 1500.0f; }
-            if (i < n && v < best) { best = v; bi = i; }
-        }
-    }
-    __shared__ float sv[256];
-    __shared__ int64_t si[256];
     sv[threadIdx.x] = best;
     si[threadIdx.x] = bi;
     __syncthreads();
@@ -98,10 +75,64 @@ __global__ __launch_bounds__(256) void k_vstat(const float *__restrict__ vn, int
         }
         __syncthreads();
     }
+    best = sv[0];
+    bi = si[0];
+}
+
+__global__ __launch_bounds__(256) void k_vstat_part(const float *__restrict__ vn, int64_t s0, int64_t s2,
+                                                    int64_t s3, int nz, int nx, int vel_mode, int chunk,
+                                                    float *pv, int64_t *pi)
+{
+    const int b = blockIdx.x, part = blockIdx.y;
+    const int n = nz * nx, i0 = part * chunk, i1 = min(n, i0 + chunk);
+    float best = INFINITY;
+    int64_t bi = INT64_MAX;
+    // each thread's elements in increasing order, loads issued 8 at a time
+    constexpr int CH = 8;
+    for (int base = i0 + threadIdx.x; base < i1; base += CH * blockDim.x) {
+        float t[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = base + u * blockDim.x;
+            const int iz = i / nx, ix = i - iz * nx;
+            t[u] = i < i1 ? vn[b * s0 + iz * s2 + ix * s3] : INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = base + u * blockDim.x;
+            float v = t[u];
+            if (vel_mode == 0) { v = v + 1.0f; v = v / 2.0f; v = v * 3000.0f; v = v + 1500.0f; }
+            if (i < i1 && v < best) { best = v; bi = i; }
+        }
+    }
+    __shared__ float sv[256];
+    __shared__ int64_t si[256];
+    vstat_reduce(best, bi, sv, si);
     if (threadIdx.x == 0) {
-        vmin[b] = sv[0];
-        amin[b] = si[0];
-        float k = 3.0f * sv[0]; k = k * lnk; k = k / two_a;   // kappa = 3*vmin*ln(1e7)/(2a), pde.py:43
+        pv[(size_t)b * gridDim.y + part] = best;
+        pi[(size_t)b * gridDim.y + part] = bi;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vstat_final(const float *__restrict__ pv, const int64_t *__restrict__ pi,
+                                                     int parts, float lnk, float two_a, float *vmin, int64_t *amin,
+                                                     float *ks)
+{
+    const int b = blockIdx.x;
+    float best = INFINITY;
+    int64_t bi = INT64_MAX;
+    for (int j = threadIdx.x; j < parts; j += blockDim.x) {
+        const float v = pv[(size_t)b * parts + j];
+        const int64_t i = pi[(size_t)b * parts + j];
+        if (v < best || (v == best && i < bi)) { best = v; bi = i; }
+    }
+    __shared__ float sv[256];
+    __shared__ int64_t si[256];
+    vstat_reduce(best, bi, sv, si);
+    if (threadIdx.x == 0) {
+        vmin[b] = best;
+        amin[b] = bi;
+        float k = 3.0f * best; k = k * lnk; k = k / two_a;   // kappa = 3*vmin*ln(1e7)/(2a), pde.py:43
         ks[b] = k;
     }
 }
@@ -3511,9 +3542,16 @@ int rdq_fwi_coeffs(const rdq_fwi_plan *p, int32_t B, const float *vn, const int6
     CoefArgs a;
     a.cg = coef_gen(p, B, coeffs);
     const double ad = (double)(p->g.nbc - 1) * (double)p->g.dx;   // a = (nbc-1)*dx, pde.py:42
-    hipLaunchKernelGGL(k_vstat, dim3(B), dim3(256), 0, st, vn, strides[0], strides[2], strides[3],
-                       p->g.nz, p->g.nx, vel_mode, (float)std::log(10000000.0), (float)(2.0 * ad), vmin, amin,
-                       const_cast<float *>(a.cg.ks));
+    {   // partials in field 5 of `coeffs` (the model copy, written by k_coeff_fields afterwards)
+        const int n = p->g.nz * p->g.nx, parts = std::max(1, std::min(256, (n + 8191) / 8192));
+        const int chunk = (n + parts - 1) / parts;
+        float *pv = coeffs + 5 * (size_t)B * p->Hp * p->ld;
+        int64_t *pi = reinterpret_cast<int64_t *>(pv + (((size_t)B * parts + 3) / 4) * 4);
+        hipLaunchKernelGGL(k_vstat_part, dim3(B, parts), dim3(256), 0, st, vn, strides[0], strides[2], strides[3],
+                           p->g.nz, p->g.nx, vel_mode, chunk, pv, pi);
+        hipLaunchKernelGGL(k_vstat_final, dim3(B), dim3(256), 0, st, pv, pi, parts, (float)std::log(10000000.0),
+                           (float)(2.0 * ad), vmin, amin, const_cast<float *>(a.cg.ks));
+    }
     a.vn = vn; a.s0 = strides[0]; a.s2 = strides[2]; a.s3 = strides[3];
     a.vel_mode = vel_mode; a.ld = p->ld;
     a.vmod_out = const_cast<float *>(a.cg.vmod);
