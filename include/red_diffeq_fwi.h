@@ -121,6 +121,9 @@ int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *plan, int32_t steps);
 int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *plan, int32_t shots);
 /* The same for the WIDE chunked forward (k_fwd_tw; 0 = auto, the default). */
 int rdq_fwi_set_wide_fwd_shots(rdq_fwi_plan *plan, int32_t shots);
+/* Time steps per launch of the WIDE chunked forward (k_fwd_tw, 1..6, or 0 = rdq_fwi_set_tuning's
+ * fwd_steps, the default).  Results are identical for every depth. */
+int rdq_fwi_set_wide_fwd_steps(rdq_fwi_plan *plan, int32_t steps);
 /* Rows per wave of the 64 x 96-region persistent kernels: forward 6, 8, 12 or 24 (16, 12, 8 or 4
  * waves per workgroup), adjoint (FMA build) 6, 8 or 12.  Same region geometry and results.  The time
  * step is latency-bound, so more resident waves win (configs[1], tools/ab_rw.sh, tools/ab_adj_nb6.sh):

@@ -255,6 +255,8 @@ constexpr int TB_NW = 8;                 // waves per workgroup
 constexpr int TB_R = 8;                  // rows per wave
 constexpr int TB_RH = TB_NW * TB_R;      // region rows
 constexpr int TB_MAXT = 4;
+constexpr int TW_FWD_MAXT = 6;          // deepest wide chunked forward (k_fwd_tw instantiations 1 .. 6)
+constexpr int FWD_W_MAX = TW_FWD_MAXT > TB_MAXT ? TW_FWD_MAXT : TB_MAXT;   // wavelet samples per chunked forward launch
 
 __device__ __forceinline__ float dpp_shr1(float v)   // lane i <- lane i-1 (x-1); lane 0 reads 0
 {
@@ -286,7 +288,7 @@ struct FwdTBArgs {
     float *seis;
     int n0, nsteps;
     int spw, ns_sh;                      // wide kernels: shots per workgroup, shots of the launch's chain
-    float w[TB_MAXT];                    // wavelet samples w[n0 .. n0+nsteps-1]
+    float w[FWD_W_MAX];                  // wavelet samples w[n0 .. n0+nsteps-1]
 };
 
 // exchange two boundary rows each way between the NW waves of the workgroup
@@ -2556,6 +2558,7 @@ struct rdq_fwi_plan {
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
     int adj_Tw = 0;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT); 0 = auto, see wide_adj_depth
+    int fwd_Tw = 0;             // the wide chunked forward's depth (<= TW_FWD_MAXT); 0 = auto, see wide_fwd_depth
     int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_spw)
     int fwd_spw = 0;            // the wide chunked forward's, 0 = auto
     int chains = 1;             // independent shot groups launched as concurrent chains
@@ -2603,6 +2606,9 @@ int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, 
 // at 6; contracted 111.2 ms vs 115.1-115.7 at 6).
 constexpr int TW_ADJ_DEFAULT = 5;
 int wide_adj_depth(const rdq_fwi_plan *p) { return p->adj_Tw > 0 ? p->adj_Tw : TW_ADJ_DEFAULT; }
+// Default depth of the wide chunked forward: rdq_fwi_set_tuning's fwd_steps (the persistent kernels'
+// depth, <= 4) unless rdq_fwi_set_wide_fwd_steps chose one (<= TW_FWD_MAXT)
+int wide_fwd_depth(const rdq_fwi_plan *p) { return p->fwd_Tw > 0 ? p->fwd_Tw : p->fwd_T; }
 
 // Shots per workgroup of a wide forward / adjoint launch over `regions` (models x tiles) of `ns` shots.  A
 // workgroup generates its region's coefficients once for all its shots and pays its fixed start-up
@@ -2739,9 +2745,12 @@ void launch_fwd_w(int T, bool gen, bool pair, dim3 grid, hipStream_t st, const F
     case 1: launch_fwd_w_T<1>(gen, pair, grid, st, a); break;
     case 2: launch_fwd_w_T<2>(gen, pair, grid, st, a); break;
     case 3: launch_fwd_w_T<3>(gen, pair, grid, st, a); break;
-    default: launch_fwd_w_T<4>(gen, pair, grid, st, a); break;
+    case 4: launch_fwd_w_T<4>(gen, pair, grid, st, a); break;
+    case 5: launch_fwd_w_T<5>(gen, pair, grid, st, a); break;
+    default: launch_fwd_w_T<6>(gen, pair, grid, st, a); break;
     }
 }
+static_assert(FWD_W_MAX >= TW_FWD_MAXT && FWD_W_MAX >= TB_MAXT, "FwdTBArgs::w holds one sample per step of a launch");
 template <int TT, bool EX>
 void launch_adj_w_T(bool pair, dim3 grid, hipStream_t st, const AdjTBArgs &a)
 {
@@ -3082,7 +3091,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
     FwdTBArgs a{};
     a.g = tb_geo(p, B);
     const size_t L = a.g.level;
-    const int T = p->fwd_T, S = chain_count(p), ns = p->g.ns;
+    const int T = p->wide ? wide_fwd_depth(p) : p->fwd_T, S = chain_count(p), ns = p->g.ns;
     // (no hipMemsetAsync under graph capture: see zero_regions)
     if (hist) RDQ_TRY(zero_regions({{hist, 2 * L * sizeof(float)}}, st));
     else RDQ_TRY(zero_regions({{ring, 4 * L * sizeof(float)}}, st));
@@ -3107,7 +3116,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
             a.spw = p->wide ? wide_spw(p->fwd_spw, B * a.g.ntiles, a.ns_sh) : 1;
             a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
-            for (int t = 0; t < TB_MAXT; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
+            for (int t = 0; t < FWD_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
             if (hist) {
                 a.in_prev = hist + (size_t)n0 * L;          // slot n0   = P_{n0-1}
                 a.in_cur = hist + (size_t)(n0 + 1) * L;     // slot n0+1 = P_{n0}
@@ -3344,6 +3353,17 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     return 0;
 }
 
+int rdq_fwi_set_wide_fwd_steps(rdq_fwi_plan *p, int32_t steps)
+{
+    if (!p || steps < 0 || steps > TW_FWD_MAXT) return RDQ_E_INVALID;   // 0 = set_tuning's fwd_steps
+    if (p->fwd_Tw != steps) {   // graphs encode the launch sequence
+        drop_graphs(p);
+        p->cache.clear();
+    }
+    p->fwd_Tw = steps;
+    return 0;
+}
+
 int rdq_fwi_set_wide_fwd_shots(rdq_fwi_plan *p, int32_t shots)
 {
     if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_spw)
@@ -3428,11 +3448,12 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     int perf = 0, pera = 0;
     out[0] = persistent_nw(p, B, false, &perf);
     out[1] = persistent_nw(p, B, true, &pera);
-    out[2] = p->fwd_T;
+    const int fwdT = !out[0] && p->wide ? wide_fwd_depth(p) : p->fwd_T;   // chunked forward: the wide kernels' depth
+    out[2] = fwdT;
     const int adjT = !out[1] && p->wide ? wide_adj_depth(p) : p->adj_T;   // chunked adjoint: the wide kernels' depth
     out[3] = adjT;
     const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
-    out[4] = out[0] ? (ns + perf - 1) / perf : (nt + p->fwd_T - 1) / p->fwd_T;
+    out[4] = out[0] ? (ns + perf - 1) / perf : (nt + fwdT - 1) / fwdT;
     out[5] = out[1] ? (ns + pera - 1) / pera : (nt + adjT - 1) / adjT;
     return 0;
 }

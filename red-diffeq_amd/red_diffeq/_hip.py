@@ -50,6 +50,7 @@ SIGNATURES = {
     "rdq_fwi_set_wide_adj_steps": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_wide_adj_shots": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_wide_fwd_shots": (c_int32, [c_void_p, c_int32]),
+    "rdq_fwi_set_wide_fwd_steps": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_persistent": (c_int32, [c_void_p, c_int32]),
     "rdq_fwi_set_rows_per_wave": (c_int32, [c_void_p, c_int32, c_int32]),
     "rdq_fwi_status": (c_int32, [c_void_p, c_void_p]),

@@ -112,6 +112,11 @@ class FwiPlan:
         them).  Results are identical for every setting."""
         _hip.check(self.lib.rdq_fwi_set_wide_adj_shots(self.handle, int(shots)), "rdq_fwi_set_wide_adj_shots")
 
+    def set_wide_fwd_steps(self, steps):
+        """Time steps per launch of the wide chunked forward (1..6; 0 = set_tuning's fwd_steps).
+        Results are identical for every depth."""
+        _hip.check(self.lib.rdq_fwi_set_wide_fwd_steps(self.handle, int(steps)), "rdq_fwi_set_wide_fwd_steps")
+
     def set_wide_fwd_shots(self, shots):
         """Shots per workgroup of the wide chunked forward (as set_wide_adj_shots; 0 = auto)."""
         _hip.check(self.lib.rdq_fwi_set_wide_fwd_shots(self.handle, int(shots)), "rdq_fwi_set_wide_fwd_shots")

@@ -662,11 +662,12 @@ def test_wide_shots_per_workgroup_bitexact(cuda, T):
     dseis_np = rng.standard_normal((B, plan.ns, sz.nrec, plan.ng)).astype(np.float32)
     dseis = torch.from_numpy(dseis_np).to(cuda)
 
-    def run(fspw, aspw, chains):
+    def run(fspw, aspw, chains, fTw=0):
         plan.set_persistent(False)
         plan.set_variant(wide_chunked=True)
         plan.set_tuning(T, T, chains)
         plan.set_wide_adj_steps(0)
+        plan.set_wide_fwd_steps(fTw)
         plan.set_wide_fwd_shots(fspw)
         plan.set_wide_adj_shots(aspw)
         outs = []
@@ -683,12 +684,14 @@ def test_wide_shots_per_workgroup_bitexact(cuda, T):
 
     try:
         ref = run(1, 1, 1)
-        for fspw, aspw, chains in ((2, 2, 1), (3, 4, 1), (8, 8, 1), (2, 3, 2), (8, 8, 2), (0, 0, 1)):
-            got = run(fspw, aspw, chains)
+        for fspw, aspw, chains, fTw in ((2, 2, 1, 0), (3, 4, 1, 0), (8, 8, 1, 0), (2, 3, 2, 0), (8, 8, 2, 0),
+                                        (0, 0, 1, 0), (4, 0, 1, 5), (0, 0, 2, 6)):
+            got = run(fspw, aspw, chains, fTw)      # (fTw: the wide forward's own depth 5 / 6, tails 3 / 2)
             for name, a_, b_ in zip(("seis", "gA", "gbeta"), got[:3], ref[:3]):
-                assert bits_equal(a_, b_), (fspw, aspw, chains, name)
+                assert bits_equal(a_, b_), (fspw, aspw, chains, fTw, name)
             np.testing.assert_allclose(got[3], ref[3], rtol=1e-12)
     finally:
+        plan.set_wide_fwd_steps(0)
         plan.set_wide_fwd_shots(0)
         plan.set_wide_adj_shots(0)
         plan.set_tuning(4, 4, 1)

@@ -35,6 +35,7 @@ ap.add_argument("--chunked-adj-fma", action="store_true", help="contracted wide 
 ap.add_argument("--Tw", type=int, default=0, help="wide chunked adjoint depth (rdq_fwi_set_wide_adj_steps; 0 = auto)")
 ap.add_argument("--spw", type=int, default=0, help="wide adjoint shots per workgroup (0: the plan's default)")
 ap.add_argument("--fspw", type=int, default=0, help="wide forward shots per workgroup (0: the plan's default)")
+ap.add_argument("--fTw", type=int, default=0, help="wide forward depth (0: the --T depth)")
 ap.add_argument("--chains", type=int, default=1, help="concurrent shot-group launch chains")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
@@ -54,6 +55,7 @@ if a.spw:
     plan.set_wide_adj_shots(a.spw)
 if a.fspw:
     plan.set_wide_fwd_shots(a.fspw)
+plan.set_wide_fwd_steps(a.fTw)
 sz = plan.sizes(1)
 npad = sz.Hp * sz.Wp
 dseis = torch.randn(1, a.ns, sz.nrec, plan.ng, device=dev)
@@ -90,7 +92,7 @@ for T in [int(t) for t in a.T.split(",")]:
     plan.status()
     f, d = min(fw), min(ad)
     shot_steps = a.ns * a.nt
-    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chunked_adj_fma": a.chunked_adj_fma, "Tw": a.Tw, "spw": a.spw, "fspw": a.fspw, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
+    print(json.dumps({"T": T, "fwd_gen": not a.no_gen, "wide": not a.narrow, "exact": a.exact, "chunked_adj_fma": a.chunked_adj_fma, "Tw": a.Tw, "spw": a.spw, "fspw": a.fspw, "fTw": a.fTw, "chains": a.chains, "fwd_ms": round(f, 2), "adj_ms": round(d, 2),
                       "shot_ts_per_s": round(shot_steps / ((f + d) / 1e3)),
                       "fwd_GBps_alg": round(12 * npad * shot_steps / f / 1e6, 1),
                       "adj_GBps_alg": round(16 * npad * shot_steps / d / 1e6, 1),
