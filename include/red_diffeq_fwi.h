@@ -184,7 +184,9 @@ int rdq_fwi_forward(const rdq_fwi_plan *plan, int32_t B, const float *coeffs, fl
                     float *history, float *ring, hipStream_t stream);
 
 /* K2: discrete adjoint of the forward (the autograd backward of pde.py:74-86), given
- * dseis = d(loss)/d(seis).  Writes the accumulators gA, gk_part, gbeta (overwritten). */
+ * dseis = d(loss)/d(seis).  Writes the accumulators gA, gk_part, gbeta (overwritten).  All buffers
+ * are device memory (hipMalloc / torch CUDA tensors): the wide chunked kernels add into gk_part with
+ * hardware fp64 atomics, which fine-grained host memory does not support. */
 int rdq_fwi_adjoint(const rdq_fwi_plan *plan, int32_t B, const float *coeffs,
                     const float *history, const float *dseis, float *ring, float *gA,
                     double *gk_part, float *gbeta, hipStream_t stream);
