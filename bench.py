@@ -275,9 +275,9 @@ def configs4_rank_workload(dev, a, nsl=16, ns_total=128, nz=500, nx=3000, iters=
             "adj_frac_alg": round(16 * npad * shot_steps / d / 1e6 / HBM_PEAK_GBS, 4),
             # the wide kernels keep T steps of a region on chip, so their counter traffic is below the
             # algorithmic bytes (adjoint 0.81x, forward 0.63x: profiles/r5/pmc_traffic_k_*_tw_ns16.json)
-            # and frac_alg can pass 1.0; the per-cell-step time is the figure of merit then
-            "fwd_ns_per_cell_step": round(f * 1e6 / (npad * shot_steps), 5),
-            "adj_ns_per_cell_step": round(d * 1e6 / (npad * shot_steps), 5),
+            # and frac_alg can pass 1.0; the cell-step rate is the figure of merit then
+            "fwd_gcell_steps_per_s": round(npad * shot_steps / f / 1e6, 1),
+            "adj_gcell_steps_per_s": round(npad * shot_steps / d / 1e6, 1),
             "frac_alg_note": "algorithmic fraction (12 / 16 B per cell-step at 8 TB/s); saturates above 1.0",
             "peak_hbm_allocated_GB": round(peak_gb, 1), "kernels": info}
 
