@@ -114,8 +114,8 @@ int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
  * narrow chunked adjoints' depth only.  A time loop whose nt is not a multiple of the depth ends with
  * one shorter launch of its own depth.  Results are identical for every depth. */
 int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *plan, int32_t steps);
-/* Shots per workgroup of the WIDE chunked adjoint (1..64, or 0 = auto, the default: the largest of
- * 8 / 4 / 2 / 1 whose launch rounds fill the CUs as well as the best): a workgroup runs that many
+/* Shots per workgroup of the WIDE chunked adjoint (1..64, or 0 = auto, the default: the cheapest of
+ * 16 / 8 / 4 / 2 / 1 under rounds of one workgroup per CU x (shots + a workgroup's fixed cost)): a workgroup runs that many
  * shots of one region in turn and generates the region's alpha / kappa once for all of them.
  * Results are identical for every setting. */
 int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *plan, int32_t shots);

@@ -2615,8 +2615,9 @@ int wide_fwd_depth(const rdq_fwi_plan *p) { return p->fwd_Tw > 0 ? p->fwd_Tw : p
 // once, so more is cheaper per shot, but a workgroup of many shots is a long indivisible unit.  Cost
 // model: rounds of one workgroup per CU x (shots per workgroup + KAPPA), KAPPA = a workgroup's fixed
 // cost in shots (fitted at configs[4]: forward 0.6, adjoint 0.25; profiles/r5/configs4_adj_spw.jsonl,
-// configs4_fwd_spw.jsonl); the cheapest of 8 / 4 / 2 / 1 (ties: more shots).  configs[4] (16 shots, 203
-// forward / 510 adjoint regions): 8 for both; a small grid (20 regions) keeps 1 for parallelism.
+// configs4_fwd_spw.jsonl); the cheapest of 16 / 8 / 4 / 2 / 1 (ties: more shots).  configs[4] (16
+// shots, 203 forward / 510 adjoint regions): 16 for both (forward 57.5 -> 54.9 ms, adjoint 94.9 -> 94.1
+// against 8: configs4_spw16.jsonl); a small grid (20 regions) keeps 1 for parallelism.
 int wide_spw(int setting, int regions, int ns)
 {
     if (setting > 0) return std::max(1, std::min(setting, ns));
@@ -2629,7 +2630,7 @@ int wide_spw(int setting, int regions, int ns)
     constexpr double KAPPA = 0.5;
     int pick = 1;
     double best = 1e300;
-    for (const int c : {8, 4, 2, 1}) {
+    for (const int c : {16, 8, 4, 2, 1}) {
         const int spw = std::min(c, ns), groups = (ns + spw - 1) / spw;
         const long long wgs = (long long)regions * groups, rounds = (wgs + cus - 1) / cus;
         const double cost = (double)rounds * (spw + KAPPA);

@@ -107,9 +107,9 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_set_wide_adj_steps(self.handle, int(steps)), "rdq_fwi_set_wide_adj_steps")
 
     def set_wide_adj_shots(self, shots):
-        """Shots per workgroup of the wide chunked adjoint (1..64; 0 = auto, the default: up to 8, chosen
-        so the launch's rounds fill the CUs; the region's alpha / kappa are generated once for all of
-        them).  Results are identical for every setting."""
+        """Shots per workgroup of the wide chunked adjoint (1..64; 0 = auto, the default: up to 16, from a
+        cost model of launch rounds x (shots + a workgroup's fixed cost); the region's alpha / kappa are
+        generated once for all of them).  Results are identical for every setting."""
         _hip.check(self.lib.rdq_fwi_set_wide_adj_shots(self.handle, int(shots)), "rdq_fwi_set_wide_adj_shots")
 
     def set_wide_fwd_steps(self, steps):
