@@ -75,7 +75,8 @@ int rdq_fwi_sizes(const rdq_fwi_plan *plan, int32_t B, rdq_fwi_sizes_t *out);
 int rdq_fwi_set_graphs(rdq_fwi_plan *plan, int32_t enable);
 /* Time steps advanced per launch by the forward / adjoint kernels (temporal blocking depth,
  * 1..4; the wide chunked adjoint has its own depth, rdq_fwi_set_wide_adj_steps) and the number of
- * concurrent shot-group launch chains (1..16).  Results are identical for every setting; only speed
+ * concurrent shot-group launch chains of the chunked kernels (1..16, or 0 = auto, the default: 2 for
+ * the wide kernels, 1 for the 64-column ones).  Results are identical for every setting; only speed
  * changes. */
 int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps, int32_t chains);
 /* Kernel variant flags (a new plan starts at RDQ_VARIANT_FWD_GEN):

@@ -2561,7 +2561,7 @@ struct rdq_fwi_plan {
     int fwd_Tw = 0;             // the wide chunked forward's depth (<= TW_FWD_MAXT); 0 = auto, see wide_fwd_depth
     int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_spw)
     int fwd_spw = 0;            // the wide chunked forward's, 0 = auto
-    int chains = 1;             // independent shot groups launched as concurrent chains
+    int chains = 0;             // independent shot groups launched as concurrent chains; 0 = auto (chain_count)
     bool fwd_gen = true;        // chunked forward regenerates coefficients from the model (vs loading K3)
     bool adj_fma = true;        // persistent adjoint with FMA contraction (vs the oracle's exact op order)
     bool adj_tw_fma = false;    // wide chunked adjoint with FMA contraction (RDQ_VARIANT_CHUNKED_ADJ_FMA; default:
@@ -2599,7 +2599,15 @@ TBGeo tb_geo(const rdq_fwi_plan *p, int B)
 // from and joined back into `st` with events (inside graph capture this records parallel graph
 // branches).  Concurrent chains overlap each launch's fixed latency (prologue loads, store
 // drain, dispatch) with the other chains' compute.
-int chain_count(const rdq_fwi_plan *p) { return std::max(1, std::min(p->chains, p->g.ns)); }
+// Concurrent launch chains of a chunked time loop.  Auto: two for the wide kernels (each chain's
+// launches fill the other's tail rounds: configs[4] forward 54.7 -> 49.0-50.0 ms, adjoint 93.8 ->
+// 91.0-91.6; 3 / 4 / 8 chains 51.7 / 53.9 / 58.0 and 93.1 / 95.1 / 101.2; profiles/r5/configs4_chains.jsonl),
+// one for the 64-column kernels.
+int chain_count(const rdq_fwi_plan *p)
+{
+    const int c = p->chains > 0 ? p->chains : (p->wide ? 2 : 1);
+    return std::max(1, std::min(c, p->g.ns));
+}
 
 // Default depth of the wide chunked adjoint, measured at configs[4] (profiles/r5/configs4_wide_adj_depth.jsonl):
 // 5 steps per launch is the fastest for both forms (exact order 116.1-116.3 ms vs 120.4 at 4 and 120.6
@@ -3341,7 +3349,7 @@ int rdq_fwi_set_graphs(rdq_fwi_plan *p, int32_t enable)
 
 int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, int32_t chains)
 {
-    if (!p || fwd_steps < 1 || fwd_steps > TB_MAXT || adj_steps < 1 || adj_steps > TB_MAXT || chains < 1 ||
+    if (!p || fwd_steps < 1 || fwd_steps > TB_MAXT || adj_steps < 1 || adj_steps > TB_MAXT || chains < 0 ||
         chains > 16)
         return RDQ_E_INVALID;
     if (p->fwd_T != fwd_steps || p->adj_T != adj_steps || p->chains != chains) {   // graphs encode these

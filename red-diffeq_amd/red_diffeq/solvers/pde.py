@@ -187,7 +187,8 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_profile_waves(self.handle, int(bool(adj)), out, n), "rdq_fwi_profile_waves")
         return np.frombuffer(out, dtype=np.uint64).reshape(-1, 3).astype(np.float64) / 100.0
 
-    def set_tuning(self, fwd_steps, adj_steps, chains=1):
+    def set_tuning(self, fwd_steps, adj_steps, chains=0):
+        """Blocking depths (1..4) and concurrent launch chains of the chunked kernels (0 = auto)."""
         _hip.check(self.lib.rdq_fwi_set_tuning(self.handle, int(fwd_steps), int(adj_steps), int(chains)),
                    "rdq_fwi_set_tuning")
 

@@ -36,7 +36,7 @@ ap.add_argument("--Tw", type=int, default=0, help="wide chunked adjoint depth (r
 ap.add_argument("--spw", type=int, default=0, help="wide adjoint shots per workgroup (0: the plan's default)")
 ap.add_argument("--fspw", type=int, default=0, help="wide forward shots per workgroup (0: the plan's default)")
 ap.add_argument("--fTw", type=int, default=0, help="wide forward depth (0: the --T depth)")
-ap.add_argument("--chains", type=int, default=1, help="concurrent shot-group launch chains")
+ap.add_argument("--chains", type=int, default=0, help="concurrent shot-group launch chains")
 ap.add_argument("--no-gen", action="store_true",
                 help="chunked forward loads the K3 coefficient fields instead of regenerating them (the default)")
 ap.add_argument("--phase", action="store_true",
