@@ -2629,12 +2629,12 @@ int wide_fwd_depth(const rdq_fwi_plan *p) { return p->fwd_Tw > 0 ? p->fwd_Tw : p
 int wide_spw(int setting, int regions, int ns)
 {
     if (setting > 0) return std::max(1, std::min(setting, ns));
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-    }
+    static const int cus = [] {          // (thread-safe one-time initialisation)
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+            n = 256;
+        return n;
+    }();
     constexpr double KAPPA = 0.5;
     int pick = 1;
     double best = 1e300;
