@@ -400,7 +400,11 @@ def main():
     backend = os.environ.get("RDQ_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    # under a torch.distributed launcher the process group is started at every world size, so a
+    # world-size-1 torchrun exercises the same init_process_group("nccl", device_id=...) and gradient
+    # all-reduce as the N-GPU runs (the driver's plain `python bench.py` N = 1 run has no group)
+    distributed = "WORLD_SIZE" in os.environ and "RANK" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -438,12 +442,12 @@ def main():
     mu = torch.nn.functional.pad(mu0, (1, 1, 1, 1)).to(dev).requires_grad_(True)
     opt = FusedAdamClamp(mu, lr=0.03, clamp=(-1.0, 1.0))       # K11: Adam + clamp, one pass
     sched = CosineLR(0.03, T_max=300, eta_min=0.0)
-    nobs = torch.full((B,), float(ns_tot * nt * 70), device=dev) if world > 1 else None
+    nobs = torch.full((B,), float(ns_tot * nt * 70), device=dev) if distributed else None
     lam = 0.01
 
     def step():
         v_in = mu[:, :, 1:-1, 1:-1]
-        if world > 1:
+        if distributed:
             v_in = grad_all_reduce(v_in)
         loss = l1_misfit(fwi(v_in), y, None, nobs) + lam * total_variation_loss(mu)
         opt.zero_grad()
@@ -453,17 +457,17 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    if world > 1:
+    if distributed:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     t_step = el.item() / a.steps
     dbg = os.environ.get("RDQ_DEBUG_STATUS")
@@ -496,7 +500,7 @@ def main():
     fwi.check()
     fw_ms, adj_ms = float(np.median(fw_ms)), float(np.median(adj_ms))
     allreduce_us = None
-    if world > 1:   # the one exchange per iteration: all-reduce of the B x 70 x 70 model gradient
+    if distributed:   # the one exchange per iteration: all-reduce of the B x 70 x 70 model gradient
         g = torch.randn(B, 1, 70, 70, device=dev)
         ts_ = []
         for _ in range(25):
@@ -538,7 +542,8 @@ def main():
                                        else f"OpenFWI {family}")) +
                                 f" 70x70 (310x310 padded), {nsl} shots/GPU ({ns_tot} total), nt={nt}, "
                                 "fwd+adj gradient + TV + Adam step" +
-                                (" + one RCCL all-reduce of the model gradient" if world > 1 else "")),
+                                (f" + one {'RCCL' if backend == 'nccl' else backend} all-reduce of the model gradient"
+                                 if distributed else "")),
                    "global_batch": B, "shots_per_gpu": nsl, "shots_total": ns_tot, "nt": nt,
                    "parallelism": f"shot-parallel x{world}"},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -552,12 +557,16 @@ def main():
                                        if traffic else None),
                      "algorithmic_bytes_per_launch": adj_bytes, "avg_launch_us": round(adj_launch_us, 3),
                      "steps_per_launch": steps_per_launch,
+                     # the figure of merit once frac saturates: the adjoint's device time per time step
+                     # (all nsl x B shots), and the forward's (coefficients + forward phase)
+                     "adj_us_per_timestep": round(adj_launch_us / steps_per_launch, 4),
+                     "fwd_us_per_timestep": round(fw_ms * 1e3 / nt, 4),
                      "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None},
         "kernels": info,
         "phases_ms": {"coeffs+forward": round(fw_ms, 3), "adjoint": round(adj_ms, 3),
                       "fwd_GBps_alg": round(fwd_bytes * nt / (fw_ms * 1e-3) / 1e9, 1)},
         "fwd_adj_only_shot_ts_per_s": round(nsl * nt * B / ((fw_ms + adj_ms) * 1e-3), 1),
-        "per_rank": {"shots": nsl, "allreduce_us": allreduce_us,
+        "per_rank": {"shots": nsl, "allreduce_us": allreduce_us, "backend": backend if distributed else None,
                      # step time minus the two time-loop phases; the phases are timed in separate
                      # runs after the timed loop, so this can dip below 0 by the kernels' own
                      # launch-to-launch spread (about +-5 %)
@@ -602,7 +611,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(ctx, vtrue[:1], a.cpu_sample_shots, a.cpu_sample_reps)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

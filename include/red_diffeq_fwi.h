@@ -11,9 +11,18 @@
  *   - Plain pointers and sizes; device pointers unless stated "host".  No torch types.
  *   - Every call is stream-ordered on the given hipStream_t (NULL = legacy default stream) and
  *     returns 0 or a negative error code (-hipError_t, or RDQ_E_* below).
+ *   - One call in flight per plan, enforced by the plan: its host state (graph cache, chain streams)
+ *     is mutex-guarded, so any host thread may call it, and a forward / adjoint call on a different
+ *     stream than the plan's previous one first waits (an event, no host sync) for the work that
+ *     stream had queued, so calls on one plan never overlap on the device.  The previous call's
+ *     stream must still exist at that point.  Different plans are independent.
  *   - The caller owns every buffer; sizes come from rdq_fwi_sizes().  The plan owns only the
  *     uploaded geometry (a few KB) and its cached hipGraphs.
- *   - Results are deterministic: no float atomics; every reduction has a fixed order.
+ *   - Results are deterministic: every reduction has a fixed order.  The one float atomic, the wide
+ *     chunked adjoint's fp64 add of a workgroup's sponge partial into its gk_part slot, has exactly
+ *     one writer per slot and launch and no slot shared between concurrent launch chains (checked on
+ *     the host for every launch of a time loop before it is enqueued; RDQ_E_INVALID otherwise), so
+ *     each slot's adds arrive one launch after another in stream order: a fixed order.
  *   - Layout: padded grid Hp = nz + 2*nbc rows, Wp = nx + 2*nbc columns, row pitch `ld`
  *     floats (Wp rounded up to 64).  fp32 throughout, as the reference.
  */
@@ -158,6 +167,10 @@ int rdq_fwi_set_status_buffer(rdq_fwi_plan *plan, uint32_t *words);
  * adjoint steps per epoch/launch, forward time-loop launches per call, adjoint time-loop launches
  * per call} (persistent: one per resident shot group; chunked: ceil(nt / T)). */
 int rdq_fwi_launch_info(rdq_fwi_plan *plan, int32_t B, int32_t out[6]);
+/* The wide chunked kernels' launch shape for batch B: out = {concurrent launch chains, shots per
+ * workgroup of the forward's and of the adjoint's full-depth launches of chain 0 (the automatic choice
+ * unless rdq_fwi_set_wide_*_shots fixed one), shots in chain 0}. */
+int rdq_fwi_wide_info(rdq_fwi_plan *plan, int32_t B, int32_t out[4]);
 /* Diagnostics: 1 = the persistent kernels accumulate per-wave phase times (s_memrealtime, 10 ns
  * ticks); read_profile synchronises the device, returns and clears them:
  * out[0..5] forward {hand-off wait, time steps, publish, waves, first sweep pass, sweep passes},

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -28,6 +29,7 @@
 #include <new>
 #include <vector>
 #include <initializer_list>
+#include <mutex>
 #include <utility>
 
 #include "red_diffeq_fwi.h"
@@ -447,7 +449,7 @@ __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)
 // shots of the group.  A placement guess only changes speed, never results.
 struct TileId { int tx, ty, tile, sl; bool valid; };
 
-__device__ __forceinline__ TileId decode_tile(int L, int tiles_x, int ntiles, int nsg)
+__host__ __device__ __forceinline__ TileId decode_tile(int L, int tiles_x, int ntiles, int nsg)
 {
     TileId t;
     t.tile = (L / (8 * nsg)) * 8 + (L & 7);
@@ -2569,9 +2571,18 @@ struct rdq_fwi_plan {
     bool wide = true;           // chunked kernels on 128-column regions (k_fwd_tw / k_adj_tw) vs 64-column
     hipStream_t cap = nullptr;
     std::vector<hipStream_t> aux;
-    std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins
+    std::vector<hipEvent_t> evs;   // [0] fork, [1..] joins (inside graph capture: graph edges)
     std::vector<GraphEntry> cache;
     uint64_t tick = 0;
+    // One call in flight per plan: the host state above (graph cache, chain streams and events) is
+    // guarded by `mu`, and a time-loop call on another stream than the previous one first waits on an
+    // event recorded on that stream at this point (`handover`), so calls on one plan from several
+    // streams run one after the other on the device (the persistent launches share the plan's arrival
+    // counters and each needs the whole chip; the chunked launches share the chain streams).
+    std::mutex mu;
+    hipStream_t last = nullptr;
+    bool have_last = false;
+    hipEvent_t handover = nullptr;
 };
 
 namespace {
@@ -2618,34 +2629,105 @@ int wide_adj_depth(const rdq_fwi_plan *p) { return p->adj_Tw > 0 ? p->adj_Tw : T
 // depth, <= 4) unless rdq_fwi_set_wide_fwd_steps chose one (<= TW_FWD_MAXT)
 int wide_fwd_depth(const rdq_fwi_plan *p) { return p->fwd_Tw > 0 ? p->fwd_Tw : p->fwd_T; }
 
+// Compute units of the device the plan's launches run on, cached per device (a process may drive
+// several GPUs; the count is queried once per device id).
+int device_cus()
+{
+    constexpr int MAXDEV = 64;
+    static std::atomic<int> cache[MAXDEV];               // 0 = not queried yet
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev >= 0 && dev < MAXDEV && (n = cache[dev].load(std::memory_order_relaxed)) > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    if (dev >= 0 && dev < MAXDEV) cache[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+
 // Shots per workgroup of a wide forward / adjoint launch over `regions` (models x tiles) of `ns` shots.  A
 // workgroup generates its region's coefficients once for all its shots and pays its fixed start-up
 // once, so more is cheaper per shot, but a workgroup of many shots is a long indivisible unit.  Cost
-// model: rounds of one workgroup per CU x (shots per workgroup + KAPPA), KAPPA = a workgroup's fixed
-// cost in shots (fitted at configs[4]: forward 0.6, adjoint 0.25; profiles/r5/configs4_adj_spw.jsonl,
-// configs4_fwd_spw.jsonl); the cheapest of 16 / 8 / 4 / 2 / 1 (ties: more shots).  configs[4] (16
-// shots, 203 forward / 510 adjoint regions): 16 for both (forward 57.5 -> 54.9 ms, adjoint 94.9 -> 94.1
-// against 8: configs4_spw16.jsonl); a small grid (20 regions) keeps 1 for parallelism.
-int wide_spw(int setting, int regions, int ns)
+// model: rounds of one workgroup per CU x (shots per workgroup + kappa), kappa = a workgroup's fixed
+// cost in shots, fitted at configs[4] (profiles/r5/configs4_adj_spw.jsonl, configs4_fwd_spw.jsonl):
+// forward 0.6, adjoint 0.25; the cheapest of 16 / 8 / 4 / 2 / 1 (ties: more shots).  `chains` launch
+// chains run concurrently and share the CUs, so one chain's launch gets cus / chains of them.
+// configs[4] (16 shots in two chains of 8, 203 forward / 510 adjoint regions): 8 for both; with one
+// chain, 16 for both (forward 57.5 -> 54.9 ms, adjoint 94.9 -> 94.1 against 8: configs4_spw16.jsonl); a
+// small grid (20 regions) keeps 1 for parallelism.
+int wide_spw(int setting, int regions, int ns, bool adj, int chains)
 {
     if (setting > 0) return std::max(1, std::min(setting, ns));
-    static const int cus = [] {          // (thread-safe one-time initialisation)
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
-            n = 256;
-        return n;
-    }();
-    constexpr double KAPPA = 0.5;
+    const int cus = std::max(1, device_cus() / std::max(1, chains));
+    const double kappa = adj ? 0.25 : 0.6;
     int pick = 1;
     double best = 1e300;
     for (const int c : {16, 8, 4, 2, 1}) {
         const int spw = std::min(c, ns), groups = (ns + spw - 1) / spw;
         const long long wgs = (long long)regions * groups, rounds = (wgs + cus - 1) / cus;
-        const double cost = (double)rounds * (spw + KAPPA);
+        const double cost = (double)rounds * (spw + kappa);
         if (cost < best - 1e-9) { best = cost; pick = spw; }
     }
     return pick;
 }
+
+// A time-loop call on `st` (caller holds p->mu): when the plan's previous call went to another
+// stream, `st` first waits for everything that stream had queued by now (which includes that call),
+// so calls on one plan never overlap on the device whatever streams they come on.  A steady caller
+// (one stream) pays nothing.  Skipped while either stream is being captured into a graph: a captured
+// stream cannot wait on an event recorded outside the capture (the caller orders captured work).
+int plan_enter(rdq_fwi_plan *p, hipStream_t st)
+{
+    if (p->have_last && p->last != st) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone, cl = hipStreamCaptureStatusNone;
+        RDQ_CHECK(hipStreamIsCapturing(st, &cs));
+        RDQ_CHECK(hipStreamIsCapturing(p->last, &cl));
+        if (cs == hipStreamCaptureStatusNone && cl == hipStreamCaptureStatusNone) {
+            if (!p->handover) RDQ_CHECK(hipEventCreateWithFlags(&p->handover, hipEventDisableTiming));
+            RDQ_CHECK(hipEventRecord(p->handover, p->last));
+            RDQ_CHECK(hipStreamWaitEvent(st, p->handover, 0));
+        }
+    }
+    p->last = st;
+    p->have_last = true;
+    return 0;
+}
+
+// The chunked adjoints accumulate each workgroup's sponge partial into gk_part[(b * ns + shot) * nblk
+// + tile]: the narrow kernel with a load-add-store, the wide one with a no-return fp64 atomic add.  Both
+// are deterministic (and the load-add-store race-free) only if every slot has ONE writer per launch
+// (the adds of a slot then arrive launch after launch, in stream order) and no slot is written by two
+// concurrent launch chains.  GkWriters replays the kernels' own block decode (decode_tile, the
+// shot-group split of k_adj_tw / k_adj_tb) for every launch of a time loop on the host, when the loop
+// is enqueued (once per captured graph), and refuses the call (RDQ_E_INVALID) on a violation or on a
+// slot outside the caller's gk_part buffer.
+struct GkWriters {
+    std::vector<int> chain;          // chain that owns the slot (-1: none yet)
+    std::vector<unsigned> stamp;     // last launch that wrote it
+    unsigned launch = 0;
+    int nblk;
+    GkWriters(size_t slices, int nblk_) : chain(slices * nblk_, -1), stamp(slices * nblk_, 0u), nblk(nblk_) {}
+    // one launch of chain c: grid blocks, tile grid, B models x ns shots, shot group [s_off, s_off + ns_sh)
+    // split in groups of spw shots (ns_grp groups)
+    bool add(int c, unsigned grid, int tiles_x, int ntiles, int B, int ns, int ns_grp, int s_off, int spw, int ns_sh)
+    {
+        ++launch;
+        const int nsg = B * ns_grp;
+        for (unsigned L = 0; L < grid; ++L) {
+            const TileId ti = decode_tile((int)L, tiles_x, ntiles, nsg);
+            if (!ti.valid) continue;
+            if (ti.tile >= nblk) return false;
+            const int b = ti.sl / ns_grp, jg = ti.sl - b * ns_grp;
+            const int s_first = s_off + jg * spw, nsh = std::min(spw, ns_sh - jg * spw);
+            for (int sh = 0; sh < nsh; ++sh) {
+                const size_t slot = (size_t)(b * ns + s_first + sh) * nblk + ti.tile;
+                if (s_first + sh >= ns || slot >= chain.size()) return false;
+                if (stamp[slot] == launch || (chain[slot] >= 0 && chain[slot] != c)) return false;
+                stamp[slot] = launch;
+                chain[slot] = c;
+            }
+        }
+        return true;
+    }
+};
 
 int ensure_aux(rdq_fwi_plan *p, int S)
 {
@@ -3021,9 +3103,10 @@ static int zero_regions(std::initializer_list<std::pair<void *, size_t>> regs, h
         tot = 0;
         return 0;
     };
+    for (const auto &r : regs)                   // every region is 4-byte words: checked before any launch
+        if (r.first && (r.second & 3)) return RDQ_E_INVALID;
     for (const auto &r : regs) {
         if (!r.first || !r.second) continue;
-        if (r.second & 3) return RDQ_E_INVALID;                      // every region is 4-byte words
         if (z.nr == ZERO_MAXR) RDQ_TRY(flush());
         z.p[z.nr] = r.first;
         z.n[z.nr++] = r.second;
@@ -3122,7 +3205,7 @@ int launch_forward(rdq_fwi_plan *p, int B, const float *coeffs, float *seis, flo
             const int Tl = p->wide ? a.nsteps : T;
             a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
             a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, false) : tiles_y(p->Hp, Tl));
-            a.spw = p->wide ? wide_spw(p->fwd_spw, B * a.g.ntiles, a.ns_sh) : 1;
+            a.spw = p->wide ? wide_spw(p->fwd_spw, B * a.g.ntiles, a.ns_sh, false, S) : 1;
             a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
             const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
             for (int t = 0; t < FWD_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[n0 + t] : 0.0f;
@@ -3153,29 +3236,40 @@ int launch_adjoint(rdq_fwi_plan *p, int B, const float *coeffs, const float *his
     const size_t L = a.g.level;
     const int T = p->wide ? wide_adj_depth(p) : p->adj_T, S = chain_count(p), ns = p->g.ns;
     const int nblk_alloc = gk_blocks(p);
-    RDQ_TRY(zero_regions({{ring, 4 * L * sizeof(float)}, {gA, L * sizeof(float)},
-                          {gk, (size_t)B * ns * nblk_alloc * sizeof(double)}, {gbeta, (size_t)B * ns * sizeof(float)}},
-                         st));   // (no hipMemsetAsync under graph capture: see zero_regions)
     a.coeffs = coeffs; a.hist = hist; a.dseis = dseis; a.gA = gA; a.gk_part = gk; a.gbeta = gbeta;
     a.cg = coef_gen(p, B, coeffs);
     a.nblk = nblk_alloc;
+    // launch geometry of chain c's launch of depth nsteps: sets a.g.{s_off, tiles_x, ntiles, ns_grp},
+    // a.ns_sh, a.spw; returns the grid size
+    auto geometry = [&](int c, int nsteps) -> unsigned {
+        a.g.s_off = c * ns / S;
+        a.ns_sh = (c + 1) * ns / S - a.g.s_off;   // wide kernels: a.spw shots of one region per workgroup
+        const int Tl = p->wide ? nsteps : T;
+        a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
+        a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
+        a.spw = p->wide ? wide_spw(p->adj_spw, B * a.g.ntiles, a.ns_sh, true, S) : 1;
+        a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;   // (the decode's slice groups are shot groups)
+        return (unsigned)((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
+    };
+    {   // the gk_part one-writer invariant, on every launch, before anything is enqueued
+        GkWriters writers((size_t)B * ns, nblk_alloc);
+        for (int c = 0; c < S; ++c)
+            for (int k0 = p->g.nt; k0 >= 1; k0 -= T) {
+                const unsigned grid = geometry(c, std::min(T, k0));
+                if (!writers.add(c, grid, a.g.tiles_x, a.g.ntiles, B, ns, a.g.ns_grp, a.g.s_off, a.spw, a.ns_sh))
+                    return RDQ_E_INVALID;
+            }
+    }
+    RDQ_TRY(zero_regions({{ring, 4 * L * sizeof(float)}, {gA, L * sizeof(float)},
+                          {gk, (size_t)B * ns * nblk_alloc * sizeof(double)}, {gbeta, (size_t)B * ns * sizeof(float)}},
+                         st));   // (no hipMemsetAsync under graph capture: see zero_regions)
     RDQ_TRY(fork_chains(p, st, S));
     for (int c = 0; c < S; ++c) {
-        a.g.s_off = c * ns / S;
-        a.g.ns_grp = (c + 1) * ns / S - a.g.s_off;
-        // wide kernels: a workgroup runs a.spw shots of one region in turn (the decode's slice groups
-        // are then shot groups)
-        a.ns_sh = a.g.ns_grp;
         const hipStream_t cs = c == 0 ? st : p->aux[c - 1];
         for (int k0 = p->g.nt, i = 0; k0 >= 1; k0 -= T, ++i) {
             a.k0 = k0;
             a.nsteps = std::min(T, k0);
-            const int Tl = p->wide ? a.nsteps : T;
-            a.g.tiles_x = p->wide ? tw_tiles_x(p->Wp, Tl) : tiles_x(p->Wp, Tl);
-            a.g.ntiles = a.g.tiles_x * (p->wide ? tw_tiles_y(p->Hp, Tl, true) : tiles_y(p->Hp, Tl));
-            a.spw = p->wide ? wide_spw(p->adj_spw, B * a.g.ntiles, a.ns_sh) : 1;
-            a.g.ns_grp = (a.ns_sh + a.spw - 1) / a.spw;
-            const dim3 grid((a.g.ntiles + 7) / 8 * 8 * B * a.g.ns_grp);
+            const dim3 grid(geometry(c, a.nsteps));
             for (int t = 0; t < ADJ_W_MAX; ++t) a.w[t] = t < a.nsteps ? p->wavf[k0 - 1 - t] : 0.0f;
             const int pin = i & 1, pout = pin ^ 1;
             a.in_l1 = ring + (size_t)(2 * pin) * L;
@@ -3328,6 +3422,7 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
     if (p->cap) (void)hipStreamDestroy(p->cap);
     for (auto st : p->aux) (void)hipStreamDestroy(st);
     for (auto e : p->evs) (void)hipEventDestroy(e);
+    if (p->handover) (void)hipEventDestroy(p->handover);
     if (p->d_isx) (void)hipFree(p->d_isx);
     if (p->d_rcv_start) (void)hipFree(p->d_rcv_start);
     if (p->d_rcv_list) (void)hipFree(p->d_rcv_list);
@@ -3343,6 +3438,7 @@ int rdq_fwi_plan_destroy(rdq_fwi_plan *p)
 int rdq_fwi_set_graphs(rdq_fwi_plan *p, int32_t enable)
 {
     if (!p) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     p->graphs = enable != 0;
     return 0;
 }
@@ -3352,6 +3448,7 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
     if (!p || fwd_steps < 1 || fwd_steps > TB_MAXT || adj_steps < 1 || adj_steps > TB_MAXT || chains < 0 ||
         chains > 16)
         return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->fwd_T != fwd_steps || p->adj_T != adj_steps || p->chains != chains) {   // graphs encode these
         drop_graphs(p);
         p->cache.clear();
@@ -3365,6 +3462,7 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *p, int32_t fwd_steps, int32_t adj_steps, in
 int rdq_fwi_set_wide_fwd_steps(rdq_fwi_plan *p, int32_t steps)
 {
     if (!p || steps < 0 || steps > TW_FWD_MAXT) return RDQ_E_INVALID;   // 0 = set_tuning's fwd_steps
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->fwd_Tw != steps) {   // graphs encode the launch sequence
         drop_graphs(p);
         p->cache.clear();
@@ -3376,6 +3474,7 @@ int rdq_fwi_set_wide_fwd_steps(rdq_fwi_plan *p, int32_t steps)
 int rdq_fwi_set_wide_fwd_shots(rdq_fwi_plan *p, int32_t shots)
 {
     if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_spw)
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->fwd_spw != shots) {   // graphs encode the grids
         drop_graphs(p);
         p->cache.clear();
@@ -3387,6 +3486,7 @@ int rdq_fwi_set_wide_fwd_shots(rdq_fwi_plan *p, int32_t shots)
 int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *p, int32_t shots)
 {
     if (!p || shots < 0 || shots > 64) return RDQ_E_INVALID;   // 0 = auto (wide_spw)
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->adj_spw != shots) {   // graphs encode the grids
         drop_graphs(p);
         p->cache.clear();
@@ -3398,6 +3498,7 @@ int rdq_fwi_set_wide_adj_shots(rdq_fwi_plan *p, int32_t shots)
 int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *p, int32_t steps)
 {
     if (!p || steps < 0 || steps > TW_ADJ_MAXT) return RDQ_E_INVALID;   // 0 = auto (wide_adj_depth)
+    std::lock_guard<std::mutex> lk(p->mu);
     if (wide_adj_depth(p) != (steps ? steps : TW_ADJ_DEFAULT)) {   // graphs encode the launch sequence
         drop_graphs(p);
         p->cache.clear();
@@ -3409,6 +3510,7 @@ int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *p, int32_t steps)
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
     if (!p || (flags & ~31)) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0;
     const bool fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0 && recurrence_ok(p);
     const bool twfma = (flags & RDQ_VARIANT_CHUNKED_ADJ_FMA) != 0 && (flags & RDQ_VARIANT_ADJ_EXACT) == 0 &&
@@ -3432,6 +3534,7 @@ int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *p, int32_t fwd_rows, int32_t adj_row
     if (!p || (fwd_rows != 6 && fwd_rows != 8 && fwd_rows != 12 && fwd_rows != 24) ||
         (adj_rows != 6 && adj_rows != 8 && adj_rows != 12))
         return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->fwd_rw != fwd_rows || p->adj_rw != adj_rows) {
         drop_graphs(p);
         p->cache.clear();
@@ -3443,6 +3546,7 @@ int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *p, int32_t fwd_rows, int32_t adj_row
 int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 {
     if (!p || (mode != 0 && mode != 1 && mode != 8 && mode != 12 && mode != 16 && mode != -1)) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->persist != mode) {
         drop_graphs(p);
         p->cache.clear();
@@ -3454,6 +3558,7 @@ int rdq_fwi_set_persistent(rdq_fwi_plan *p, int32_t mode)
 int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
 {
     if (!p || !out || B < 1) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     int perf = 0, pera = 0;
     out[0] = persistent_nw(p, B, false, &perf);
     out[1] = persistent_nw(p, B, true, &pera);
@@ -3467,9 +3572,23 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     return 0;
 }
 
+int rdq_fwi_wide_info(rdq_fwi_plan *p, int32_t B, int32_t out[4])
+{
+    if (!p || !out || B < 1) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
+    const int S = chain_count(p), ns0 = p->g.ns / S;   // chain 0: shots [0, ns / S), the smallest group
+    const int Tf = wide_fwd_depth(p), Ta = wide_adj_depth(p);
+    out[0] = S;
+    out[1] = p->wide ? wide_spw(p->fwd_spw, B * tw_tiles_x(p->Wp, Tf) * tw_tiles_y(p->Hp, Tf, false), ns0, false, S) : 1;
+    out[2] = p->wide ? wide_spw(p->adj_spw, B * tw_tiles_x(p->Wp, Ta) * tw_tiles_y(p->Hp, Ta, true), ns0, true, S) : 1;
+    out[3] = ns0;
+    return 0;
+}
+
 int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
 {
     if (!p) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     drop_graphs(p);   // graphs bake the pointer in
     p->cache.clear();
     if (enable && !p->d_prof) {
@@ -3485,6 +3604,7 @@ int rdq_fwi_set_profile(rdq_fwi_plan *p, int32_t enable)
 int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[12])
 {
     if (!p || !out) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     if (!p->d_prof) { for (int i = 0; i < 8; ++i) out[i] = 0; return 0; }
     RDQ_CHECK(hipDeviceSynchronize());
     p->prof_host.resize(2 * PROF_WORDS);
@@ -3498,6 +3618,7 @@ int rdq_fwi_read_profile(rdq_fwi_plan *p, uint64_t out[12])
 int rdq_fwi_profile_waves(rdq_fwi_plan *p, int32_t adj, uint64_t *out, size_t count)
 {
     if (!p || !out || (adj != 0 && adj != 1)) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     const size_t n = std::min(count, PROF_WAVES * 3);
     for (size_t i = 0; i < n; ++i)
         out[i] = p->prof_host.empty() ? 0 : p->prof_host[(adj ? PROF_WORDS : 0) + PROF_RAW + i];
@@ -3507,6 +3628,7 @@ int rdq_fwi_profile_waves(rdq_fwi_plan *p, int32_t adj, uint64_t *out, size_t co
 int rdq_fwi_status(rdq_fwi_plan *p, hipStream_t st)
 {
     if (!p) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     unsigned v = 0;
     RDQ_CHECK(hipMemcpyAsync(&v, p->d_status, sizeof(v), hipMemcpyDeviceToHost, st));
     RDQ_CHECK(hipStreamSynchronize(st));
@@ -3521,6 +3643,7 @@ int rdq_fwi_status(rdq_fwi_plan *p, hipStream_t st)
 int rdq_fwi_set_status_buffer(rdq_fwi_plan *p, uint32_t *words)
 {
     if (!p) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     if (p->d_status != (words ? words : p->d_status_own)) {
         drop_graphs(p);
         p->cache.clear();
@@ -3532,6 +3655,7 @@ int rdq_fwi_set_status_buffer(rdq_fwi_plan *p, uint32_t *words)
 int rdq_fwi_debug_words(rdq_fwi_plan *p, uint32_t out[32])
 {
     if (!p || !out) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
     RDQ_CHECK(hipDeviceSynchronize());
     RDQ_CHECK(hipMemcpy(out, p->d_status, 32 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return 0;
@@ -3598,6 +3722,8 @@ int rdq_fwi_forward(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, floa
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !seis || (!hist && !ring) || B < 1) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
+    RDQ_TRY(plan_enter(p, st));
     int per = 0;
     if (const int nw = persistent_nw(p, B, false, &per)) {
         if (!ring) return RDQ_E_INVALID;   // the persistent kernel's hand-off granules live in `ring`
@@ -3614,6 +3740,8 @@ int rdq_fwi_adjoint(const rdq_fwi_plan *pc, int32_t B, const float *coeffs, cons
 {
     rdq_fwi_plan *p = const_cast<rdq_fwi_plan *>(pc);
     if (!p || !coeffs || !hist || !dseis || !ring || !gA || !gk || !gbeta || B < 1) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
+    RDQ_TRY(plan_enter(p, st));
     if (p->rmulti) {   // several receivers in a column: fold the residuals per column (ring tail)
         float *fold = ring + 8 * (size_t)B * p->g.ns * p->Hp * p->ld;
         const size_t rows = (size_t)B * p->g.ns * p->nrec, n = rows * p->ncolr;

@@ -18,7 +18,9 @@ import torch.nn.functional as F
 from tqdm.auto import tqdm
 
 from red_diffeq.core.fused import FusedAdamClamp, metrics as fused_metrics
+from red_diffeq.core.inversion import k12_covers
 from red_diffeq.core.losses import LossCalculator
+from red_diffeq.core.metrics import MetricsCalculator
 from red_diffeq.utils.data_trans import add_noise_to_seismic, missing_trace, v_normalize
 from red_diffeq.utils.diffusion_utils import diffusion_crop, diffusion_pad
 
@@ -131,6 +133,8 @@ class DiffusionFWI:
         y = y.to(self.device)
         mask = mask.to(self.device) if missing_number else None
         loss_calc = LossCalculator(None)
+        # K12 when ssim_loss is the reference's SSIM, else the module itself (reference MetricsCalculator)
+        metrics_calc = None if k12_covers(self.ssim_loss) else MetricsCalculator(self.ssim_loss)
         keys = ("total_losses", "obs_losses", "ssim", "mae", "rmse")
         hist = torch.zeros(diffusion_ts, len(keys), B, dtype=torch.float32, device=self.device)
 
@@ -174,7 +178,10 @@ class DiffusionFWI:
                 current = denoised.detach()
             with torch.no_grad():
                 obs = loss_calc.observation_loss(fwi_forward(current), y, mask=mask)
-                m = fused_metrics(current, true_norm)                     # (mae, rmse, ssim)
+                if metrics_calc is None:
+                    m = fused_metrics(current, true_norm)                 # (mae, rmse, ssim)
+                else:                                                     # the caller's own SSIM module
+                    m = metrics_calc.calculate(current, mu_true.float().to(self.device))
                 hist[row, 0] = obs
                 hist[row, 1] = obs
                 hist[row, 2] = m[2]

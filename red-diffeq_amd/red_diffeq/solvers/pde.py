@@ -165,6 +165,14 @@ class FwiPlan:
                 "fwd_class": int(out[0]), "adj_class": int(out[1]), "fwd_T": int(out[2]),
                 "adj_T": int(out[3]), "fwd_launches": int(out[4]), "adj_launches": int(out[5])}
 
+    def wide_info(self, B):
+        """{'chains', 'fwd_spw', 'adj_spw', 'chain0_shots'}: the wide chunked kernels' concurrent launch
+        chains and shots per workgroup of chain 0's full-depth forward / adjoint launches for batch B
+        (the automatic choice unless set_wide_*_shots fixed one)."""
+        out = (ctypes.c_int32 * 4)()
+        _hip.check(self.lib.rdq_fwi_wide_info(self.handle, int(B), out), "rdq_fwi_wide_info")
+        return {"chains": int(out[0]), "fwd_spw": int(out[1]), "adj_spw": int(out[2]), "chain0_shots": int(out[3])}
+
     def set_profile(self, enable):
         _hip.check(self.lib.rdq_fwi_set_profile(self.handle, int(bool(enable))), "rdq_fwi_set_profile")
 

@@ -123,6 +123,9 @@ def test_red_loop_configs2_at_its_size(cuda):
                                    err_msg=k)
 
 
+SSIM_B25_BAR = 2 * 1.85e-4   # 2 x K12's SSIM vs the reference's own on its final models (profiles/r5)
+
+
 @pytest.mark.parametrize("adjoint", ["exact", "default"])
 def test_red_loop_openfwi_yaml_b25(cuda, adjoint):
     """The reference's shipped OpenFWI config at its own batch (configs/openfwi/red-diffeq.yaml:43,
@@ -138,7 +141,8 @@ def test_red_loop_openfwi_yaml_b25(cuda, adjoint):
     SSIM's own floor is measured here: the metric (K12, its SSIM map in fp64) of the reference's OWN final
     25 models against the reference's value for them differs by ~1.9e-4 (the reference evaluates the
     variances E[x^2] - mu^2 in fp32; a GPU torch run of the reference SSIM module on the same models
-    differs from it by 1.5e-4), so SSIM is held to max(2e-4, 2 x that floor)."""
+    differs from it by 1.5e-4), so SSIM is held to a fixed 3.7e-4 = 2 x the committed floor
+    (profiles/r5/ssim_metric_floor_b25.txt), and the floor itself is re-measured and held below 2e-4."""
     from red_diffeq.core.inversion import InversionEngine
     from red_diffeq.utils.data_trans import v_normalize
     from red_diffeq.utils.ssim import SSIM
@@ -166,17 +170,63 @@ def test_red_loop_openfwi_yaml_b25(cuda, adjoint):
         m_ref = metrics(torch.from_numpy(z["mu"]).to(cuda).contiguous(),
                         v_normalize(torch.from_numpy(z["v_true"]).to(cuda)).contiguous()).cpu().numpy()
     floor = float(np.max(np.abs(m_ref[2] - z["ssim"][:, -1]) / np.abs(z["ssim"][:, -1])))
-    record_margin("loop_red_b25_ssim_metric_floor", "K12 on the reference's final models", floor, 2.5e-4)
-    assert floor < 2.5e-4
+    # the floor measured here must stay the committed one (profiles/r5/ssim_metric_floor_b25.txt:
+    # 1.85e-4): the SSIM bar below is a constant, so a drift of the metric cannot loosen it
+    record_margin("loop_red_b25_ssim_metric_floor", "K12 on the reference's final models", floor, 2.0e-4)
+    assert floor < 2.0e-4
     bar = 2e-4 if adjoint == "exact" else 5e-4
     for k in ("total_losses", "obs_losses", "reg_losses", "mae", "rmse", "ssim"):
         got = np.array([h[k] for h in hist], np.float64)
         ref = z[k].astype(np.float64)
         rel = float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-6)))
-        b = max(bar, 2 * floor) if k == "ssim" else bar
+        # SSIM: K12 (its map in fp64, a deliberate departure from the reference's fp32 E[x^2] - mu^2)
+        # differs from the reference's own value on identical models by 1.85e-4 (committed floor):
+        # a fixed bar of 2 x that, 3.7e-4
+        b = max(bar, SSIM_B25_BAR) if k == "ssim" else bar
         print(f"  {adjoint} {k}: max rel {rel:.3e} (bar {b:.2e})")
         record_margin("loop_red_b25_rel_" + adjoint, k, rel, b)
+        # the assertion's own criterion |d| <= atol + b |ref|, as a fraction of its right-hand side
+        record_margin("loop_red_b25_crit_" + adjoint, k, float(np.max(np.abs(got - ref) / (1e-6 + b * np.abs(ref)))), 1.0)
         np.testing.assert_allclose(got, ref, rtol=b, atol=1e-6, err_msg=k)
+
+
+def test_engine_calls_a_non_reference_ssim_module(cuda):
+    """with ssim_loss = SSIM(window_size=7) the engine's SSIM history is the caller's
+    module evaluated on each iteration's model as the reference's MetricsCalculator does (reference
+    core/inversion.py:55,94, core/metrics.py:13-46): equal, bit for bit, to MetricsCalculator(SSIM(7))
+    on the traced models; with the reference's SSIM(11) the same run reports K12's (different) values,
+    and MAE / RMSE / the losses are unchanged."""
+    from red_diffeq.core.inversion import InversionEngine
+    from red_diffeq.core.metrics import MetricsCalculator
+    from red_diffeq.utils.ssim import SSIM
+    z = load_golden("loop_tv_openfwi")
+    fwi = make_fwi(ctx_of(z))
+
+    class _NoDiffusion:
+        device = cuda
+
+    runs = {}
+    for w in (7, 11):
+        eng = InversionEngine(_NoDiffusion(), SSIM(window_size=w), "tv", show_progress=False)
+        eng.model_trace = []
+        mu, hist = eng.optimize(torch.from_numpy(z["mu0"]), torch.from_numpy(z["v_true"]),
+                                torch.from_numpy(z["y"]).to(cuda), fwi, ts=4, lr=0.03, reg_lambda=0.01,
+                                regularization="tv")
+        runs[w] = (hist, eng.model_trace)
+    hist7, trace7 = runs[7]
+    calc = MetricsCalculator(SSIM(window_size=7))
+    mu_true = torch.from_numpy(z["v_true"]).float().to(cuda)
+    for it, m in enumerate(trace7):
+        mae, rmse, ssim = calc.calculate(m, mu_true)
+        for b in range(m.shape[0]):
+            assert np.float32(hist7[b]["ssim"][it]) == np.float32(float(ssim[b])), (it, b)
+            assert np.float32(hist7[b]["mae"][it]) == np.float32(float(mae[b]))
+            assert np.float32(hist7[b]["rmse"][it]) == np.float32(float(rmse[b]))
+    hist11 = runs[11][0]
+    for k in ("total_losses", "obs_losses", "reg_losses"):
+        assert np.array_equal(np.array(hist7[0][k]), np.array(hist11[0][k])), k
+    np.testing.assert_allclose(np.array(hist7[0]["mae"]), np.array(hist11[0]["mae"]), rtol=1e-5)
+    assert np.abs(np.array(hist7[0]["ssim"]) - np.array(hist11[0]["ssim"])).max() > 1e-4
 
 
 def test_tv_long_trajectory_floor(cuda):

@@ -233,6 +233,10 @@ def test_reference_configs_run_unchanged_through_cli(cuda, tmp_path, monkeypatch
         mu = mu.detach().cpu().numpy()
         for i in range(s1 - s0):
             z = np.load(files[s0 + i])
+            # (assert_array_equal treats NaN == NaN: the model's range is checked on its own)
+            assert np.isfinite(z["result"]).all() and np.abs(z["result"]).max() <= 1.0
+            for k in ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse"):
+                assert np.isfinite(z[k]).all(), k
             np.testing.assert_array_equal(z["result"], mu[i, 0])
             np.testing.assert_array_equal(z["initial_velocity"], init[i, 0, 1:-1, 1:-1].numpy())
             for k in ("total_losses", "obs_losses", "reg_losses", "ssim", "mae", "rmse"):

@@ -417,3 +417,23 @@ def test_unet_options_are_atomic_and_versioned():
     finally:
         assert lib.rdq_unet_set_option(6, old) == 5
     assert lib.rdq_unet_options_generation() == g0 + 2
+
+
+def test_k12_covers_only_the_reference_ssim():
+    """the engine evaluates SSIM with the fused K12 kernel only when the caller's
+    ssim_loss is the reference's 11 x 11, sigma 1.5 SSIM module (either size_average); any other
+    module -- another window, a subclass, a modified window -- is called as the reference's
+    MetricsCalculator calls it (reference core/metrics.py:13-46)."""
+    from red_diffeq.core.inversion import k12_covers
+    from red_diffeq.utils.ssim import SSIM
+    assert k12_covers(SSIM(window_size=11))
+    assert k12_covers(SSIM(window_size=11, size_average=False))
+    assert not k12_covers(SSIM(window_size=7))
+    assert not k12_covers(None)
+
+    class MySSIM(SSIM):
+        pass
+    assert not k12_covers(MySSIM(window_size=11))
+    s = SSIM(window_size=11)
+    s.window = s.window * 1.01
+    assert not k12_covers(s)
