@@ -1453,6 +1453,19 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
         }                                                                                           \
     }
 
+// The first hand-off pass of an epoch is issued `a.sweep_delay` ticks after the wave's publish: a pass
+// issued at once mostly finds the neighbours' granules not yet there (1.9 passes per epoch, each an L2
+// round trip of ~0.7 us) and a failed pass's loads sit in the CU's memory queue ahead of the next
+// pass's.  Measured at configs[1] (profiles/r6/sweep_delay_*): 0.25 us takes the forward 1.371 ->
+// 1.321 ms and the adjoint 1.688 -> 1.647 ms; 1 us is flat, 2 us slower.  Timing only: results are
+// identical for every delay.
+#define PT_SWEEP_DELAY()                                                                            \
+    if (a.sweep_delay > 0) {                                                                        \
+        const unsigned long long d0_ = __builtin_amdgcn_s_memrealtime();                            \
+        while (__builtin_amdgcn_s_memrealtime() - d0_ < (unsigned long long)a.sweep_delay)          \
+            __builtin_amdgcn_s_sleep(1);                                                            \
+    }
+
 #define PT_PROF(ACC)                                                                                \
     if (prof) { const unsigned long long now_ = __builtin_amdgcn_s_memrealtime(); ACC += now_ - tm; tm = now_; }
 
@@ -1476,6 +1489,7 @@ struct FwdPtArgs {
     unsigned long long *prof;            // nullable: [0] hand-off, [1] steps, [2] publish (10 ns ticks), [3] waves
     int nt;
     int xcd_mode;                        // 1: XCD-local slices (pt_assign), 0: all hand-offs write-through
+    int sweep_delay;                     // s_memrealtime ticks (10 ns) between an epoch's publish and its first sweep pass
 };
 
 // One forward step P_{n+1} = temp1 P_n - temp2 P_{n-1} + alpha N(P_n) (+ source), pde.py:79-81, on
@@ -1670,6 +1684,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, P0, P1)
             PT_PROF(tpb)
+            PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, P0, P1, R)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
@@ -1710,6 +1725,7 @@ struct AdjPtArgs {
     unsigned long long *prof;            // nullable, as FwdPtArgs
     int nt, nblk;
     int xcd_mode;
+    int sweep_delay;                     // as FwdPtArgs
 };
 
 __device__ __forceinline__ float bload_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff)
@@ -1926,6 +1942,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             ADJ_GRAD(L0, L1, PB, PHB, wv[T - 1])          // the deferred last step (no neighbour data)
             const int kn = ke - T;                        // first step k of the next epoch
             PT_PROF(tpb)
+            PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             ADJ_ISSUE
             PT_PROF(tsw)
@@ -2161,6 +2178,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             ADJR_GRAD(L0, L1, wv[T - 1], QW(0), QW(1), QW(2))   // the deferred last step (no neighbour data)
             const int kn = ke - T;                        // first step k of the next epoch
             PT_PROF(tpb)
+            PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             ADJ_ISSUE
             PT_PROF(tsw)
@@ -2223,6 +2241,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 #undef PT_SWEEP
 #undef PT_PUBLISH
 #undef PT_PROF
+#undef PT_SWEEP_DELAY
 #undef PT_ROFS
 #undef PT_REGION_INIT
 #undef LAUNDER
@@ -2531,6 +2550,9 @@ struct GraphEntry {
     uint64_t last_use;
 };
 
+// default pre-sweep delays of the persistent forward / adjoint, 10 ns ticks (PT_SWEEP_DELAY)
+constexpr int RDQ_SWEEP_DELAY_FWD = 25, RDQ_SWEEP_DELAY_ADJ = 25;
+
 struct rdq_fwi_plan {
     rdq_fwi_geom g;
     std::vector<int32_t> isx, igx;
@@ -2559,6 +2581,7 @@ struct rdq_fwi_plan {
     int fwd_rw = 6, adj_rw = 6;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave;
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
+    int fwd_delay = RDQ_SWEEP_DELAY_FWD, adj_delay = RDQ_SWEEP_DELAY_ADJ;   // persistent kernels' pre-sweep delay (ticks)
     int adj_Tw = 0;             // the wide chunked adjoint's depth (<= TW_ADJ_MAXT); 0 = auto, see wide_adj_depth
     int fwd_Tw = 0;             // the wide chunked forward's depth (<= TW_FWD_MAXT); 0 = auto, see wide_fwd_depth
     int adj_spw = 0;            // the wide chunked adjoint's shots per workgroup, 0 = auto (wide_spw)
@@ -3132,6 +3155,7 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.coeffs = coeffs; a.wav = p->d_wav; a.hist = hist; a.seis = seis;
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof; a.xcd_mode = p->xcd_mode;
+    a.sweep_delay = p->fwd_delay;
     // consecutive slice groups, one resident launch each (granules live at per-slice offsets, so
     // one zeroing serves every group)
     for (int s0 = 0; s0 < B * p->g.ns; s0 += per) {
@@ -3166,6 +3190,7 @@ int launch_adjoint_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.nblk = nblk_alloc; a.prof = p->d_prof ? p->d_prof + PROF_WORDS : nullptr;
     a.xcd_mode = p->xcd_mode;
+    a.sweep_delay = p->adj_delay;
     for (int s0 = 0; s0 < B * p->g.ns; s0 += per) {
         a.g.sl_off = s0;
         a.g.nsl = std::min(per, B * p->g.ns - s0);
@@ -3569,6 +3594,15 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
     out[4] = out[0] ? (ns + perf - 1) / perf : (nt + fwdT - 1) / fwdT;
     out[5] = out[1] ? (ns + pera - 1) / pera : (nt + adjT - 1) / adjT;
+    return 0;
+}
+
+int rdq_fwi_set_sweep_delay(rdq_fwi_plan *p, int32_t fwd_ticks, int32_t adj_ticks)
+{
+    if (!p || fwd_ticks < 0 || fwd_ticks > 100000 || adj_ticks < 0 || adj_ticks > 100000) return RDQ_E_INVALID;
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->fwd_delay = fwd_ticks;   // (persistent launches are direct, not graphs: nothing cached to drop)
+    p->adj_delay = adj_ticks;
     return 0;
 }
 

@@ -60,6 +60,7 @@ SIGNATURES = {
     "rdq_fwi_profile_waves": (c_int32, [c_void_p, c_int32, ctypes.POINTER(ctypes.c_uint64), c_size_t]),
     "rdq_fwi_launch_info": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_int32)]),
     "rdq_fwi_wide_info": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_int32)]),
+    "rdq_fwi_set_sweep_delay": (c_int32, [c_void_p, c_int32, c_int32]),
     "rdq_fwi_read_profile": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "rdq_fwi_coeffs": (c_int32, [c_void_p, c_int32, c_void_p, ctypes.POINTER(c_int64), c_int32,
                                  c_void_p, c_void_p, c_void_p]),

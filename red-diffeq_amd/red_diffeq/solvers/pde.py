@@ -165,6 +165,11 @@ class FwiPlan:
                 "fwd_class": int(out[0]), "adj_class": int(out[1]), "fwd_T": int(out[2]),
                 "adj_T": int(out[3]), "fwd_launches": int(out[4]), "adj_launches": int(out[5])}
 
+    def set_sweep_delay(self, fwd_ticks, adj_ticks):
+        """Persistent kernels: 10 ns ticks between an epoch's publish and its first hand-off pass."""
+        _hip.check(self.lib.rdq_fwi_set_sweep_delay(self.handle, int(fwd_ticks), int(adj_ticks)),
+                   "rdq_fwi_set_sweep_delay")
+
     def wide_info(self, B):
         """{'chains', 'fwd_spw', 'adj_spw', 'chain0_shots'}: the wide chunked kernels' concurrent launch
         chains and shots per workgroup of chain 0's full-depth forward / adjoint launches for batch B
