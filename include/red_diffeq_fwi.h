@@ -111,18 +111,12 @@ int rdq_fwi_set_tuning(rdq_fwi_plan *plan, int32_t fwd_steps, int32_t adj_steps,
  *                          a difference of nearly equal adjoint levels, within ~1.3e-4).  Without it
  *                          (default) the chunked adjoint keeps the oracle's exact order: gA / gbeta
  *                          bit-identical, gk to fp64 summation order.  Ignored when
- *                          RDQ_VARIANT_ADJ_EXACT is set or nbc < 20;
- *   RDQ_VARIANT_NO_SHOT_PAIRS a persistent forward that needs several resident launches (more shots
- *                          than the chip holds at one workgroup per region) runs one shot per
- *                          workgroup instead of two shots of one model per workgroup, each shot's
- *                          hand-off in flight while the other's epoch computes (identical results;
- *                          slower). */
+ *                          RDQ_VARIANT_ADJ_EXACT is set or nbc < 20. */
 #define RDQ_VARIANT_FWD_GEN 1
 #define RDQ_VARIANT_ADJ_EXACT 2
 #define RDQ_VARIANT_NO_XCD_LOCAL 4
 #define RDQ_VARIANT_NARROW_CHUNKED 8
 #define RDQ_VARIANT_CHUNKED_ADJ_FMA 16
-#define RDQ_VARIANT_NO_SHOT_PAIRS 32
 int rdq_fwi_set_variant(rdq_fwi_plan *plan, int32_t flags);
 /* Time steps per launch of the WIDE chunked adjoint (k_adj_tw, 1..6, or 0 = the default, 5: the
  * fastest depth measured at configs[4] for both the exact-order and the contracted kernels,

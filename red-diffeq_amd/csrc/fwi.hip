@@ -1249,6 +1249,15 @@ __device__ __forceinline__ u32x4 gran_get(__amdgpu_buffer_rsrc_t r, int voff, in
     return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CP_SC1);
 }
 
+// A wavelet sample at a wave-uniform step, read through the scalar cache (s_load into an SGPR): out of
+// the vector memory queue, where, with gfx9's in-order vmcnt, the forward's source row waited for its
+// next epoch's samples behind the deferred history stores.  Forward: issued right after the publish,
+// 1.362 -> 1.334 ms at configs[1] (profiles/r6/wav_scalar_ab.txt); the adjoint keeps vector loads.
+__device__ __forceinline__ float wav_s(const float *w, int i)
+{
+    return ((const __attribute__((address_space(4))) float *)w)[i];
+}
+
 // padded-grid row of region row uz (periodic wrap, pde.py:79); |uz| < 2 Hp
 __device__ __forceinline__ int wrap_row(int uz, int Hp)
 {
@@ -1661,13 +1670,13 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
-    // The next epoch's wavelet samples are loaded right after the hand-off sweep (FWD_ISSUE), not
-    // before it, so the granule loads do not queue behind them.
+    // The next epoch's wavelet samples (FWD_ISSUE) are scalar loads issued right after the publish: the
+    // source row's first step no longer waits for them behind the deferred history stores.
     float wv[T];
 #pragma unroll
-    for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
+    for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(t, a.nt - 1));
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
-#define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = a.wav[min(n0 + T + t, a.nt - 1)];
+#define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(n0 + T + t, a.nt - 1));
     xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
     __syncthreads();
     xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // P_0 = 0, step 0's tag
@@ -1692,11 +1701,12 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so);
             PT_PUBLISH(GR, tag, P0, P1)
             PT_PROF(tpb)
+            FWD_ISSUE                                     // scalar loads (wav_s): their latency hides in the
+                                                          // delay and the sweep, and no vector op waits on them
             PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, P0, P1, R)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
-            FWD_ISSUE                                     // (before the stores: 1.32 -> 1.375 ms, not used)
             // the next step's boundary rows, with the halo cells the sweep reloaded
             xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
         }
@@ -1715,133 +1725,6 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     }
 }
 
-// ---- Two shots per workgroup (k_fwd_p2): the persistent forward for surveys that need several
-// resident launches (configs[2] / configs[3]: 32 shots = 4 launches of 8 slices; the reference's
-// OpenFWI yaml: 25 models x 5 shots).  A workgroup holds the same region of TWO shots of one model
-// (they share alpha / temp1 / temp2) and alternates between them:
-//     sweep A (epoch e's halo) -> T steps of A -> publish A -> sweep B -> T steps of B -> publish B
-// so shot A's hand-off is in flight while the workgroup computes shot B's epoch, and the other way
-// round.  With one shot per workgroup an epoch costs compute + hand-off latency (configs[1]: 3.25 +
-// 2.06 us); here two shots' epochs cost max(2 x compute, compute + latency), and the probe in
-// profiles/r6/presweep_busy_probe.txt (up to ~1 us of other work between publish and sweep costs the
-// forward nothing) says the latency is in flight, not queued.  Shot pairs are (2j, 2j + 1) of each
-// model (an odd last shot runs alone in its workgroup); the launch's "slices" are these pair units,
-// placed XCD-locally by pt_assign as before.  Per-shot arithmetic, order and stores are k_fwd_pt's:
-// seismograms and history are bit-identical (tests/test_gpu_plan_contract.py).
-template <int T, int NW, int RW>
-__global__ __launch_bounds__(64 * NW) void k_fwd_p2(FwdPtArgs a)
-{
-    unsigned long long *const prof = nullptr;            // (no phase-profiled build)
-    constexpr bool PT_MIR = true;
-    __shared__ u32x4 xq2[2][2][NW][2][64];                // the barrier-free exchange of each shot
-    const TBGeo &g = a.g;
-    PT_REGION_HEAD(NW, RW)
-    // pair unit -> (model, first shot, second shot or -1); g.ns_grp = pair units per model
-    const int U = __builtin_amdgcn_readfirstlane(g.sl_off + ti.sl);
-    const int b = __builtin_amdgcn_readfirstlane(U / g.ns_grp);
-    const int s = __builtin_amdgcn_readfirstlane(2 * (U - b * g.ns_grp));
-    const bool two = s + 1 < g.ns;                        // uniform
-    const int bs = b * g.ns + s;
-    PT_REGION_GEOM()
-    const size_t soA = so, soB = so + g.slice;            // the two shots' slices bs, bs + 1
-    const int bsA = bs, bsB = bs + 1;
-    const float *AL = a.coeffs + (size_t)b * g.slice;
-    f32x2 A[RP], C1[RP], C2v[RP], PS0[2][RP], PS1[2][RP];   // per shot: PS1 = newest level
-    const f32x2 kC2 = {C2, C2}, kC3 = {C3, C3};
-    unsigned smask = 0;
-    int rrow = -1;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int gz = wrap_row(uz0 + r, g.Hp);
-        const int o = gz * g.ld + gx;
-        PT_AT(A, r) = AL[o]; PT_AT(C1, r) = AL[g.cstride + o]; PT_AT(C2v, r) = AL[2 * g.cstride + o];
-        PT_AT(PS0[0], r) = 0.0f; PT_AT(PS1[0], r) = 0.0f; PT_AT(PS0[1], r) = 0.0f; PT_AT(PS1[1], r) = 0.0f;
-        if (gz == g.isz) smask |= 1u << r;
-        if (gz == g.igz && ((rin >> r) & 1u)) rrow = r;
-    }
-    const int isxA = g.isx[s], isxB = two ? g.isx[s + 1] : -1;
-    const bool scolA = gx == isxA, scolB = gx == isxB;
-    const float bsrcA = (smask != 0) ? AL[4 * g.cstride + (size_t)g.isz * g.ld + isxA] : 0.0f;
-    const float bsrcB = (smask != 0 && two) ? AL[4 * g.cstride + (size_t)g.isz * g.ld + isxB] : 0.0f;
-    int rs = 0, re = 0, rcv0 = -1;
-    if (rrow >= 0) {
-        rs = g.rcv_start[gx]; re = g.rcv_start[gx + 1];
-        rcv0 = rs < re ? g.rcv_list[rs] : -1;
-    }
-    const bool rec = rrow >= 0 && xin && rcv0 >= 0;
-    const bool rmulti = __any(re - rs > 1);
-    const bool s1row = smask != 0 && (smask & (smask - 1u)) == 0;
-    const int sr1 = smask ? __builtin_ctz(smask) : 0;
-    const int spair = __builtin_amdgcn_readfirstlane(sr1 < RP ? sr1 : R - 1 - sr1);
-    const int rpair = __builtin_amdgcn_readfirstlane(rrow < 0 ? 0 : (rrow < RP ? rrow : R - 1 - rrow));
-    const bool shalf = sr1 >= RP, rhalf = rrow >= RP;
-    float rvs[2][T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) { rvs[0][t] = 0.0f; rvs[1][t] = 0.0f; }
-    const size_t L = g.level;
-    const int slice_bytes = (int)(g.slice * 4);
-    int hv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) hv[r] = (((rin >> r) & 1u) && xin) ? (PT_ROFS(r) + gx) * 4 : OOB;
-    const int nep = (a.nt + T - 1) / T;
-    bool live = true;
-    unsigned long long tfp = 0, npass = 0;
-    (void)tfp; (void)npass;
-    float wv[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) wv[t] = a.wav[min(t, a.nt - 1)];
-    __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) xq_init<NW>(xq2[k], w, lane);
-    __syncthreads();
-    xq_put<NW>(xq2[0], 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);
-    xq_put<NW>(xq2[1], 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);
-    // one shot's epoch e: its halo sweep (e > 0; the deferred history store of epoch e - 1's last step
-    // and the next step's boundary rows after it), T steps (k_fwd_pt's), its receiver records, and its
-    // publication for epoch e + 1.  The step / sweep / publish macros read the shot's state through the
-    // block-local names below (a macro, not a lambda: the per-shot arrays must stay registers).
-#define P2_EPOCH(K, SO, BS, SCOL, BSRC)                                                             \
-    {                                                                                               \
-        u32x4 (*xq)[NW][2][64] = xq2[K];                                                            \
-        float(&rv)[T] = rvs[K];                                                                     \
-        const size_t so = (SO);                                                                     \
-        const int bs = (BS);                                                                        \
-        const bool scol = (SCOL);                                                                   \
-        const float bsrc = (BSRC);                                                                  \
-        const int n0 = e * T;                                                                       \
-        if (e > 0) {                                                                                \
-            const unsigned tag = (unsigned)e;                                                       \
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * (e & 1)) * L + 2 * so); \
-            PT_SWEEP(GR, tag, PS0[K], PS1[K], R)                                                    \
-            if (a.hist) FWD_HIST(PS1[K], n0 - 1)                                                    \
-            xq_put<NW>(xq, n0 & 1, w, lane, (unsigned)n0 + 1u, PS1[K][0].x, PS1[K][1].x, PS1[K][1].y, \
-                       PS1[K][0].y);                                                                \
-        }                                                                                           \
-        _Pragma("unroll") for (int t = 0; t < T; ++t) {                                             \
-            const int n = n0 + t;                                                                   \
-            if (n >= a.nt) break;                                                                   \
-            if (t & 1) FWD_STEP_NB(PS0[K], PS1[K])                                                  \
-            else FWD_STEP_NB(PS1[K], PS0[K])                                                        \
-        }                                                                                           \
-        if (T & 1) {                                                                                \
-            _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                        \
-                const f32x2 tmp = PS0[K][i]; PS0[K][i] = PS1[K][i]; PS1[K][i] = tmp;                \
-            }                                                                                       \
-        }                                                                                           \
-        FWD_RECORD                                                                                  \
-        if (e + 1 < nep) {                                                                          \
-            const __amdgpu_buffer_rsrc_t GR = rsrc_of(a.gran + (size_t)(2 * ((e + 1) & 1)) * L + 2 * so); \
-            PT_PUBLISH(GR, (unsigned)(e + 1), PS0[K], PS1[K])                                       \
-        }                                                                                           \
-    }
-    for (int e = 0; e < nep; ++e) {
-        P2_EPOCH(0, soA, bsA, scolA, bsrcA)
-        if (two) P2_EPOCH(1, soB, bsB, scolB, bsrcB)
-#pragma unroll
-        for (int t = 0; t < T; ++t) wv[t] = a.wav[min((e + 1) * T + t, a.nt - 1)];   // the next epoch's
-    }
-#undef P2_EPOCH
-}
 #undef FWD_HIST
 #undef FWD_RECORD
 
@@ -2277,6 +2160,11 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
         dv[t] = DLOAD(a.nt - t);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+// the next epoch's wavelet samples and receiver residuals, issued after the sweep as vector loads:
+// ahead of it the residual loads make the sweep wait for their round trip (1.65 -> 1.78 ms), and the
+// wavelet as scalar loads (wav_s) is slower here too, before the sweep (1.64 -> 1.77 ms: an outstanding
+// s_load holds every lgkmcnt wait of the LDS exchange) or after it (1.66 ms; profiles/r6/
+// presweep_reorder_ab.txt, wav_scalar_ab.txt)
 #define ADJ_ISSUE                                                                                   \
     _Pragma("unroll") for (int t = 0; t < T; ++t) {                                                 \
         wv[t] = a.wav[max(kn - t - 1, 0)];                                                          \
@@ -2717,8 +2605,6 @@ struct rdq_fwi_plan {
     // 7..8 FMA adjoint 96-row with 8 / 12 rows per wave
     int capw[13][TB_MAXT + 1] = {};   // [9] fwd 96-row x 6 rows per wave, [10] FMA adjoint 96-row x 6,
                                       // [11] / [12] fwd / FMA adjoint 64-row x 4 rows per wave (class 16)
-    bool pairs = true;          // multi-launch persistent forwards run two shots per workgroup (k_fwd_p2)
-    int cap_p2 = 0, cap_p2_16 = 0;   // resident workgroups of k_fwd_p2, 96-row / 64-row regions (0 = not queried)
     int fwd_rw = 6, adj_rw = 6;   // rows per wave of the 96-row persistent kernels (rdq_fwi_set_rows_per_wave;
                                   // adjoint 6: 1.649 vs 1.672 ms for 8, profiles/r3/adj_rows_nb_ab.txt)
     int fwd_T = 4, adj_T = 4;   // time steps per launch (temporal blocking depth), <= TB_MAXT
@@ -3279,48 +3165,6 @@ static int zero_regions(std::initializer_list<std::pair<void *, size_t>> regs, h
     return flush();
 }
 
-// Pair units per launch of the two-shot persistent forward (k_fwd_p2) for this call, 0 = one shot per
-// workgroup.  Used when the survey needs more than one resident launch of single-shot workgroups (there
-// the hand-off latency of one shot can hide behind the other shot's epoch) and the call runs the
-// default 96-row class with 6 rows per wave at depth 4 (the instantiated kernel).  Units = shot pairs
-// (2j, 2j + 1) of each model, an odd last shot alone.
-int fwd_pair_units(rdq_fwi_plan *p, int B, int NW, int per)
-{
-    if (!p->pairs || (NW != 12 && NW != 16) || (NW == 12 && p->fwd_rw != 6) || p->fwd_T != 4 || p->persist == -1 ||
-        p->d_prof)
-        return 0;
-    if (B * p->g.ns <= per) return 0;
-    const int cap = NW == 12 ? resident_capacity(k_fwd_p2<4, 16, 6>, 1024, p->cap_p2)
-                             : resident_capacity(k_fwd_p2<4, 16, 4>, 1024, p->cap_p2_16);
-    const unsigned tp = pt_tiles_padded(p, 4, NW);
-    if (cap <= 0 || (unsigned)cap < tp) return 0;
-    const int units = B * ((p->g.ns + 1) / 2), perU = (int)((unsigned)cap / tp);
-    const int groups = (units + perU - 1) / perU;
-    return (units + groups - 1) / groups;
-}
-
-int launch_forward_p2(rdq_fwi_plan *p, int B, int NW, int perU, FwdPtArgs &a, hipStream_t st)
-{
-    const int upm = (p->g.ns + 1) / 2, units = B * upm;
-    a.g.ns_grp = upm;                                     // pair units per model (the kernel's decode)
-    const unsigned tp = pt_tiles_padded(p, 4, NW), Tt = (unsigned)a.g.ntiles;
-    const int cap = NW == 12 ? p->cap_p2 : p->cap_p2_16;
-    for (int u0 = 0; u0 < units; u0 += perU) {
-        a.g.sl_off = u0;
-        a.g.nsl = std::min(perU, units - u0);
-        unsigned grid = tp * (unsigned)a.g.nsl;
-        if (p->xcd_mode) {                                // every unit on an XCD of its own (pt_grid)
-            const unsigned want = 8u * Tt * (((unsigned)a.g.nsl + 7u) / 8u);
-            if (want > grid && (int)want <= cap) grid = want;
-        }
-        if (u0 > 0) RDQ_TRY(zero_regions({{p->d_status + 16, 8 * sizeof(unsigned)}}, st));   // pt_assign arrivals
-        if (NW == 12) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_p2<4, 16, 6>), dim3(grid), dim3(1024), 0, st, a);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fwd_p2<4, 16, 4>), dim3(grid), dim3(1024), 0, st, a);
-        RDQ_CHECK(hipGetLastError());
-    }
-    return 0;
-}
-
 int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coeffs, float *seis, float *hist, float *ring,
                       hipStream_t st)
 {
@@ -3339,7 +3183,6 @@ int launch_forward_pt(rdq_fwi_plan *p, int B, int NW, int per, const float *coef
     a.gran = reinterpret_cast<unsigned long long *>(ring);
     a.status = p->d_status; a.nt = p->g.nt; a.prof = p->d_prof; a.xcd_mode = p->xcd_mode;
     a.sweep_delay = p->fwd_delay;
-    if (const int perU = fwd_pair_units(p, B, NW, per)) return launch_forward_p2(p, B, NW, perU, a, st);
     // consecutive slice groups, one resident launch each (granules live at per-slice offsets, so
     // one zeroing serves every group)
     for (int s0 = 0; s0 < B * p->g.ns; s0 += per) {
@@ -3718,7 +3561,7 @@ int rdq_fwi_set_wide_adj_steps(rdq_fwi_plan *p, int32_t steps)
 
 int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
 {
-    if (!p || (flags & ~63)) return RDQ_E_INVALID;
+    if (!p || (flags & ~31)) return RDQ_E_INVALID;
     std::lock_guard<std::mutex> lk(p->mu);
     const bool gen = (flags & RDQ_VARIANT_FWD_GEN) != 0;
     const bool fma = (flags & RDQ_VARIANT_ADJ_EXACT) == 0 && recurrence_ok(p);
@@ -3726,7 +3569,6 @@ int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
                        recurrence_ok(p);
     const int xcd = (flags & RDQ_VARIANT_NO_XCD_LOCAL) ? 0 : 1;
     const bool wide = (flags & RDQ_VARIANT_NARROW_CHUNKED) == 0;
-    const bool pairs = (flags & RDQ_VARIANT_NO_SHOT_PAIRS) == 0;
     if (p->fwd_gen != gen || p->adj_fma != fma || p->adj_tw_fma != twfma || p->xcd_mode != xcd || p->wide != wide) {
         drop_graphs(p);
         p->cache.clear();
@@ -3736,7 +3578,6 @@ int rdq_fwi_set_variant(rdq_fwi_plan *p, int32_t flags)
     p->adj_tw_fma = twfma;
     p->xcd_mode = xcd;
     p->wide = wide;
-    p->pairs = pairs;
     return 0;
 }
 
@@ -3778,9 +3619,7 @@ int rdq_fwi_launch_info(rdq_fwi_plan *p, int32_t B, int32_t out[6])
     const int adjT = !out[1] && p->wide ? wide_adj_depth(p) : p->adj_T;   // chunked adjoint: the wide kernels' depth
     out[3] = adjT;
     const int ns = B * p->g.ns, nt = p->g.nt;   // persistent: one launch per slice group
-    const int perU = out[0] ? fwd_pair_units(p, B, out[0], perf) : 0;
-    out[4] = perU ? (B * ((p->g.ns + 1) / 2) + perU - 1) / perU
-                  : out[0] ? (ns + perf - 1) / perf : (nt + fwdT - 1) / fwdT;
+    out[4] = out[0] ? (ns + perf - 1) / perf : (nt + fwdT - 1) / fwdT;
     out[5] = out[1] ? (ns + pera - 1) / pera : (nt + adjT - 1) / adjT;
     return 0;
 }

@@ -89,16 +89,15 @@ class FwiPlan:
         _hip.check(self.lib.rdq_fwi_set_graphs(self.handle, int(bool(enable))), "rdq_fwi_set_graphs")
 
     def set_variant(self, fwd_gen_coeffs=True, adj_exact=False, xcd_local=True, wide_chunked=True,
-                    chunked_adj_fma=False, shot_pairs=True):
+                    chunked_adj_fma=False):
         """fwd_gen_coeffs: chunked forward regenerates coefficients; adj_exact: persistent adjoint in
         the oracle's exact fp32 op order (bit-identical gA) instead of FMA contraction; xcd_local:
         persistent kernels keep whole slices on one XCD with L2-resident neighbour hand-offs;
         wide_chunked: chunked kernels on 128-column regions (two columns per lane) instead of 64;
         chunked_adj_fma: the wide chunked adjoint contracts its stencils into FMAs (opt-in; the default
-        chunked adjoint keeps the oracle's exact order); shot_pairs: multi-launch persistent forwards
-        run two shots per workgroup (k_fwd_p2)."""
+        chunked adjoint keeps the oracle's exact order)."""
         flags = ((1 if fwd_gen_coeffs else 0) | (2 if adj_exact else 0) | (0 if xcd_local else 4)
-                 | (0 if wide_chunked else 8) | (16 if chunked_adj_fma else 0) | (0 if shot_pairs else 32))
+                 | (0 if wide_chunked else 8) | (16 if chunked_adj_fma else 0))
         _hip.check(self.lib.rdq_fwi_set_variant(self.handle, flags), "rdq_fwi_set_variant")
 
     def set_wide_adj_steps(self, steps):

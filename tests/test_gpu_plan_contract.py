@@ -248,42 +248,3 @@ def test_sweep_delay_changes_timing_only(cuda):
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert np.array_equal(a_.view(np.uint8), b_.view(np.uint8))
-
-
-@pytest.mark.parametrize("B,ns,nt,mode", [(2, 17, 300, 1), (1, 32, 161, 1), (1, 8, 300, 16)])
-def test_forward_two_shots_per_workgroup_bitexact(cuda, B, ns, nt, mode):
-    """k_fwd_p2: a persistent forward that needs several resident launches runs two shots of one model
-    per workgroup (pairs 2j, 2j + 1; an odd last shot alone), alternating between their epochs so one
-    shot's hand-off is in flight while the other computes.  Seismograms (history and no-grad paths)
-    and the whole store-all history are bitwise those of one shot per workgroup (the kernels the
-    reference fixtures pin), with fewer launches; nt = 161 ends on a short epoch.  mode 16: the 64 x 64
-    region class (configs[1]'s 8 shots need two launches of it one shot per workgroup, one with pairs)."""
-    from red_diffeq.utils.synthetic import make_model
-    ctx = dict(n_grid=70, nt=nt, dx=10.0, dt=0.001, nbc=120, f=15.0, sz=10, gz=10, ng=70, ns=ns)
-    v = torch.from_numpy(vnorm(make_model("curvefault", 70, 70, seed=13, batch=B))).to(cuda)
-    fwi = make_fwi(dict(ctx))
-    plan = fwi._plan(70, 70, v.device)
-    coeffs, _ = plan.coeffs(v, 0)
-    out = {}
-    try:
-        plan.set_persistent(mode)
-        for pairs in (False, True):
-            plan.set_variant(shot_pairs=pairs)
-            info = plan.launch_info(B)
-            assert info["fwd_class"] == (12 if mode == 1 else mode), info
-            seis, hist = plan.forward(coeffs, B, keep_history=True)
-            seis_ng, _ = plan.forward(coeffs, B, keep_history=False)
-            plan.status()
-            out[pairs] = (seis, hist, seis_ng, info["fwd_launches"])
-        torch.cuda.synchronize()
-        (s0, h0, n0, l0), (s1, h1, n1, l1) = out[False], out[True]
-        assert l1 < l0, (l0, l1)
-        assert torch.equal(s0.view(torch.int32), s1.view(torch.int32))
-        assert torch.equal(n0.view(torch.int32), n1.view(torch.int32))
-        assert torch.equal(s0.view(torch.int32), n0.view(torch.int32))
-        sz = plan.sizes(B)
-        hv = lambda h: h.view(nt + 2, B * ns, sz.Hp, sz.ld)[..., :sz.Wp].view(torch.int32)   # (pitch padding: unwritten)
-        assert torch.equal(hv(h0), hv(h1))
-    finally:
-        plan.set_variant()
-        plan.set_persistent(True)

@@ -23,7 +23,6 @@ ap.add_argument("--chunked", action="store_true", help="also time the chunked (l
 ap.add_argument("--profile", action="store_true", help="phase counters of the persistent kernels")
 ap.add_argument("--mode", type=int, default=1, help="persistent mode: 1 auto, 12 / 8 region height")
 ap.add_argument("--rw", default=None, help="rows per wave of the 96-row kernels, 'fwd,adj' (e.g. 12,12)")
-ap.add_argument("--no-pairs", action="store_true", help="one shot per workgroup in multi-launch persistent forwards")
 ap.add_argument("--delay", default=None, help="pre-sweep delays of the persistent kernels, 'fwd,adj' ticks")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -33,8 +32,6 @@ v = v_normalize(torch.from_numpy(make_model("flatvel", 70, 70, batch=a.B))).to(d
 plan = fwi._plan(70, 70, dev)
 if a.rw:
     plan.set_rows_per_wave(*[int(x) for x in a.rw.split(",")])
-if a.no_pairs:
-    plan.set_variant(shot_pairs=False)
 if a.delay:
     plan.set_sweep_delay(*[int(x) for x in a.delay.split(",")])
 sz = plan.sizes(a.B)
@@ -63,7 +60,7 @@ for T, G in cfgs:
         del hist
     plan.status()
     fw, ad = sorted(fw)[len(fw) // 2], sorted(ad)[len(ad) // 2]
-    res.append({"T": T, "persistent": G, "mode": a.mode, "rw": a.rw, "delay": a.delay, "pairs": not a.no_pairs, "ns": a.ns,
+    res.append({"T": T, "persistent": G, "mode": a.mode, "rw": a.rw, "delay": a.delay, "ns": a.ns,
                 "fwd_launches": plan.launch_info(a.B)["fwd_launches"], "fwd_ms": round(fw, 3), "adj_ms": round(ad, 3),
                 "shot_ts_per_s": round(a.ns * a.nt * a.B / ((fw + ad) * 1e-3))})
     if a.profile and G:
