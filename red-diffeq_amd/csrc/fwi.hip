@@ -368,6 +368,17 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
+// Wave priorities of the barrier-free persistent forward (s_setprio; the SIMD's arbiter issues the
+// higher-priority wave first).  A wave polling its neighbours' LDS slots (xq_wait) or the hand-off
+// granules (PT_SWEEP) drops to WAIT, so its spin loop does not take issue cycles from the waves still
+// computing; a wave that got its neighbours' rows runs its two boundary row pairs (what the neighbours
+// wait for next) at EDGE, then its interior pairs at BODY.  Configs[1] forward, interleaved x3
+// (profiles/r6/wave_priority_ab.txt): 1.342 -> 1.262 ms with the LDS spin alone at WAIT, 1.225 with the
+// sweep too, 1.212 with the edge / body split; 1.362 -> 1.204 ms against no priorities in a second run,
+// 1.194 with the post-sweep priority at EDGE (the default) and 1.217 with BODY = 2.  (The adjoint
+// synchronises its waves with a barrier per step and gains nothing: 1.638 -> 1.646 ms with the sweep
+// at WAIT.)
+constexpr int PT_PRIO_WAIT = 0, PT_PRIO_BODY = 1, PT_PRIO_SWEPT = 3, PT_PRIO_EDGE = 3;
 template <int NW>
 __device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
 {
@@ -406,6 +417,7 @@ __device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w,
 {
     if (!__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_setprio(PT_PRIO_WAIT);        // (see PT_PRIO_*)
         for (unsigned it = 1;; ++it) {
             xq_load<NW>(xq, buf, w, lane, u, d);
             if (__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) break;
@@ -417,6 +429,7 @@ __device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w,
             }
         }
     }
+    __builtin_amdgcn_s_setprio(PT_PRIO_EDGE);
     Halo4 h;
     h.u2 = __uint_as_float(u.x); h.u1 = __uint_as_float(u.z);
     h.d1 = __uint_as_float(d.x); h.d2 = __uint_as_float(d.z);
@@ -1392,6 +1405,7 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
     {                                                                                               \
         unsigned long long t0_ = 0;                                                                 \
         const unsigned long long ts_ = prof ? __builtin_amdgcn_s_memrealtime() : 0;                 \
+        if constexpr (PT_PRIO) __builtin_amdgcn_s_setprio(PT_PRIO_WAIT);                            \
         for (unsigned pass_ = 0; live; ++pass_) {                                                   \
             /* the loads of a group of SG rows are all issued before any is checked: lanes        \
                without a halo cell in a row load from an out-of-range offset (no memory access,   \
@@ -1438,6 +1452,7 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
             }                                                                                       \
             __builtin_amdgcn_s_sleep(1);                                                            \
         }                                                                                           \
+        if constexpr (PT_PRIO) __builtin_amdgcn_s_setprio(PT_PRIO_SWEPT);                           \
         /* cells outside the next epoch's dependence cone: zeroed (bounded garbage) */             \
         unsigned rin_ = rin, rcy_ = rcy;                                                            \
         LAUNDER(rin_); LAUNDER(rcy_);                                                               \
@@ -1606,6 +1621,7 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
         FWD_PAIRS_NB(CUR, PRV, 0, 2)                                                                          \
         if (t + 1 < T)                                                                              \
             xq_put<NW>(xq, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0].x, PRV[1].x, PRV[1].y, PRV[0].y); \
+        __builtin_amdgcn_s_setprio(PT_PRIO_BODY);                                                   \
         FWD_PAIRS_NB(CUR, PRV, 2, RP)                                                                         \
         if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
         if (rrow >= 0) {                             /* receiver row: value kept, stored per epoch */ \
@@ -1623,6 +1639,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     constexpr bool PT_MIR = true;                         // mirrored pairs (barrier-free exchange:
                                                           // 1.364 -> 1.287 ms at configs[1])
+    constexpr bool PT_PRIO = true;                        // wave priorities (PT_PRIO_*)
     __shared__ u32x4 xq[2][NW][2][64];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
@@ -1860,6 +1877,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
     constexpr bool PT_MIR = false;                        // stacked pairs {i, i+4} (ADJ_PLOAD / ADJ_GRAD)
+    constexpr bool PT_PRIO = false;                       // (barrier-synchronised steps: PT_PRIO_*)
     __shared__ float xch[2][NW][4][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
@@ -2096,6 +2114,7 @@ template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
+    constexpr bool PT_PRIO = false;                       // (barrier-synchronised steps: PT_PRIO_*)
     constexpr bool PT_MIR = false;                        // stacked pairs {i, i+RP}; the adjoint keeps the
                                                           // barrier (barrier-free form: 1.659 -> 1.688 ms)
     __shared__ float xch[2][NW][4][64];
