@@ -353,7 +353,7 @@ __device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w
     return h;
 }
 
-// ---- Barrier-free wave-to-wave exchange of the persistent forward.
+// ---- Barrier-free wave-to-wave exchange of the persistent forward and adjoint.
 // A wave's boundary rows go to LDS as 16-byte slots {row a, tag, row b, tag} (top: rows 0, 1;
 // bottom: rows R-2, R-1), double-buffered by step parity, and the neighbour waves poll their slot
 // until both tags carry the step's number: each wave waits only for the two waves it reads from,
@@ -375,9 +375,9 @@ constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-writ
 // wait for next) at EDGE, then its interior pairs at BODY.  Configs[1] forward, interleaved x3
 // (profiles/r6/wave_priority_ab.txt): 1.342 -> 1.262 ms with the LDS spin alone at WAIT, 1.225 with the
 // sweep too, 1.212 with the edge / body split; 1.362 -> 1.204 ms against no priorities in a second run,
-// 1.194 with the post-sweep priority at EDGE (the default) and 1.217 with BODY = 2.  (The adjoint
-// synchronises its waves with a barrier per step and gains nothing: 1.638 -> 1.646 ms with the sweep
-// at WAIT.)
+// 1.194 with the post-sweep priority at EDGE (the default) and 1.217 with BODY = 2.  (With a barrier
+// per step the adjoint gained nothing, 1.638 -> 1.646 ms with the sweep at WAIT; its barrier-free form,
+// ADJR_STEP_NB, uses the same exchange and priorities: 1.646 -> 1.577 ms.)
 constexpr int PT_PRIO_WAIT = 0, PT_PRIO_BODY = 1, PT_PRIO_SWEPT = 3, PT_PRIO_EDGE = 3;
 template <int NW>
 __device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
@@ -2110,14 +2110,60 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
     }
 
+// Barrier-free adjoint step (mirrored pairs, the forward's tagged LDS exchange xq_*): the wave waits
+// only for its two neighbours' A L_{k+1} boundary rows, computes its two boundary pairs (receiver
+// residual included), publishes their A L_k rows for the next step, then its interior pair.  Per row
+// the operations and their order are ADJR_STEP's (m1 + p1 commutes: same bits).  (The gradient's
+// history half ahead of the wait, as the forward's time terms, needs 6 more VGPRs: 84 B/lane scratch.)
+#define ADJR_PAIRS_NB(CUR, PRV, LO, HI)                                                             \
+    {                                                                                               \
+        _Pragma("unroll") for (int i = (LO); i < (HI); ++i) {                                        \
+            MIR_VERT(q, i, m1, p1, m2, p2)                                                          \
+            const f32x2 c = q[i];                                                                   \
+            const f32x2 xl1 = {dpp_shr1(c.x), dpp_shr1(c.y)}, xr1 = {dpp_shl1(c.x), dpp_shl1(c.y)}; \
+            f32x2 n1 = m1 + p1; n1 = n1 + xl1; n1 = n1 + xr1;                                       \
+            f32x2 n2 = m2 + p2;                        /* x -+ 2 taps: fused v_add_f32_dpp */       \
+            n2.x = n2.x + dpp_shr1(xl1.x); n2.y = n2.y + dpp_shr1(xl1.y);                           \
+            n2.x = n2.x + dpp_shl1(xr1.x); n2.y = n2.y + dpp_shl1(xr1.y);                           \
+            const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
+            PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
+        }                                                                                           \
+        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+            int rp_ = rpair;                                                                        \
+            LAUNDER(rp_);                                                                           \
+            const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
+            _Pragma("unroll") for (int i = (LO); i < (HI); ++i) if (i == rp_) PRV[i] = PRV[i] + dv_; \
+        }                                                                                           \
+    }
+#define ADJR_STEP_NB(CUR, PRV, P0, P1, P2, PN)                                                      \
+    {                                                                                               \
+        if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
+        const float dcur = dv[t];                                                                   \
+        u32x4 xu_, xd_;                                                                             \
+        xq_load<NW>(xq, j & 1, w, lane, xu_, xd_);                                                  \
+        f32x2 q[RP];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
+        const Halo4 h4 = xq_wait<NW>(xq, j & 1, w, lane, (unsigned)j + 1u, xu_, xd_, a.status, live); \
+        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
+        ADJR_PAIRS_NB(CUR, PRV, 0, 2)                                                               \
+        if (t + 1 < T)                                                                              \
+            xq_put<NW>(xq, (j + 1) & 1, w, lane, (unsigned)j + 2u, A[0].x * PRV[0].x, A[1].x * PRV[1].x, \
+                       A[1].y * PRV[1].y, A[0].y * PRV[0].y);                                       \
+        __builtin_amdgcn_s_setprio(PT_PRIO_BODY);                                                   \
+        ADJR_PAIRS_NB(CUR, PRV, 2, RP)                                                              \
+        if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
+    }
+
 template <int T, int NW, int RW, bool PROF>
 __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 {
     unsigned long long *const prof = PROF ? a.prof : nullptr;   // phase counters: profiled build only
-    constexpr bool PT_PRIO = false;                       // (barrier-synchronised steps: PT_PRIO_*)
-    constexpr bool PT_MIR = false;                        // stacked pairs {i, i+RP}; the adjoint keeps the
-                                                          // barrier (barrier-free form: 1.659 -> 1.688 ms)
-    __shared__ float xch[2][NW][4][64];
+    constexpr bool ADJ_NB = true;                         // barrier-free steps (ADJR_STEP_NB): 1.646 ->
+                                                          // 1.577 ms at configs[1] (profiles/r6/adj_nb_ab.txt)
+    constexpr bool PT_PRIO = ADJ_NB;                      // wave priorities (PT_PRIO_*)
+    constexpr bool PT_MIR = ADJ_NB;                       // mirrored pairs for the exchange's boundary rows
+    __shared__ float xch[2][NW][4][64];                   // (the unused exchange is not allocated)
+    __shared__ u32x4 xq[2][NW][2][64];
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
@@ -2193,7 +2239,12 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     bool live = true;
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
-#define ADJR_STEP_SEL ADJR_STEP
+    if constexpr (ADJ_NB) {
+        xq_init<NW>(xq, w, lane);                         // no slot matches a tag until written
+        __syncthreads();
+        xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // A L_{nt+1} = 0, step 0's tag
+    }
+#define ADJR_STEP_SEL(...) { if constexpr (ADJ_NB) ADJR_STEP_NB(__VA_ARGS__) else ADJR_STEP(__VA_ARGS__) }
     for (int e = 0; e < nep; ++e) {
         const int ke = a.nt - e * T;                      // first step k of this epoch
         const bool last = e + 1 == nep;
@@ -2224,6 +2275,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             PT_PROF(tpb)
             PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
+            if constexpr (ADJ_NB)   // the next step's boundary rows, with the halo cells the sweep reloaded
+                xq_put<NW>(xq, (e + 1) * T & 1, w, lane, (unsigned)((e + 1) * T) + 1u, A[0].x * L1[0].x,
+                           A[1].x * L1[1].x, A[1].y * L1[1].y, A[0].y * L1[0].y);
             ADJ_ISSUE
             PT_PROF(tsw)
         }
