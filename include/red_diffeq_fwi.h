@@ -141,10 +141,10 @@ int rdq_fwi_set_wide_fwd_steps(rdq_fwi_plan *plan, int32_t steps);
  * 6 rows 1.65 ms, 8 rows 1.67, 12 rows 2.08.  Default 6 / 6. */
 int rdq_fwi_set_rows_per_wave(rdq_fwi_plan *plan, int32_t fwd_rows, int32_t adj_rows);
 /* Delay, in 10 ns ticks (0..100000), between a persistent launch's per-epoch publish of its border and
- * its first hand-off sweep pass, for the forward and the adjoint (defaults 25 / 25 = 0.25 us: a pass
- * issued at once mostly finds the neighbours' granules not there yet and queues ahead of the one that
- * would; configs[1] forward 1.371 -> 1.321 ms, adjoint 1.688 -> 1.647 ms).  Results are identical for
- * every delay; only speed changes. */
+ * its first hand-off sweep pass, for the forward and the adjoint (defaults 15 / 0 = 0.15 / 0 us: a
+ * forward pass issued at once mostly finds the neighbours' granules not there yet and queues ahead of
+ * the one that would; configs[1] forward 1.210 -> 1.196 ms against 0.25 us; the barrier-free adjoint
+ * is fastest without a delay).  Results are identical for every delay; only speed changes. */
 int rdq_fwi_set_sweep_delay(rdq_fwi_plan *plan, int32_t fwd_ticks, int32_t adj_ticks);
 /* 1 (default) = run each time loop as ONE persistent launch (regions resident in registers for
  * all nt steps, epoch-wise neighbour hand-offs) whenever the whole grid fits resident on the

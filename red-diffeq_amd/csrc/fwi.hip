@@ -1489,7 +1489,9 @@ __device__ PtTile pt_assign(const TBGeo &g, unsigned *status, int xcd_mode)
 // issued at once mostly finds the neighbours' granules not yet there (1.9 passes per epoch, each an L2
 // round trip of ~0.7 us) and a failed pass's loads sit in the CU's memory queue ahead of the next
 // pass's.  Measured at configs[1] (profiles/r6/sweep_delay_*): 0.25 us takes the forward 1.371 ->
-// 1.321 ms and the adjoint 1.688 -> 1.647 ms; 1 us is flat, 2 us slower.  Timing only: results are
+// 1.321 ms and the adjoint 1.688 -> 1.647 ms; 1 us is flat, 2 us slower.  With the wave priorities and
+// the barrier-free adjoint (profiles/r6/delay_retune_ab.txt): forward best at 0.15 us (1.210 -> 1.196
+// ms against 0.25), adjoint at 0 (1.588 -> 1.562 ms), the defaults.  Timing only: results are
 // identical for every delay.
 #define PT_SWEEP_DELAY()                                                                            \
     if (a.sweep_delay > 0) {                                                                        \
@@ -2651,7 +2653,7 @@ struct GraphEntry {
 };
 
 // default pre-sweep delays of the persistent forward / adjoint, 10 ns ticks (PT_SWEEP_DELAY)
-constexpr int RDQ_SWEEP_DELAY_FWD = 25, RDQ_SWEEP_DELAY_ADJ = 25;
+constexpr int RDQ_SWEEP_DELAY_FWD = 15, RDQ_SWEEP_DELAY_ADJ = 0;
 
 struct rdq_fwi_plan {
     rdq_fwi_geom g;

@@ -226,7 +226,7 @@ def test_plan_calls_from_two_threads(cuda):
 def test_sweep_delay_changes_timing_only(cuda):
     """rdq_fwi_set_sweep_delay (the persistent kernels' wait between an epoch's publish and its first
     hand-off pass) moves only the timing: seismograms and the adjoint accumulators are bitwise those of
-    no delay, for 0, the default and a 5 us delay (many epochs then find their granules at once)."""
+    no delay, for the defaults, 0.25 us and a 5 us delay (many epochs then find their granules at once)."""
     fwi, plan, v = _openfwi_plan(cuda, ns=8, nt=300)
     B = 1
     assert plan.launch_info(B)["fwd_persistent"] and plan.launch_info(B)["adj_persistent"]
@@ -236,7 +236,7 @@ def test_sweep_delay_changes_timing_only(cuda):
     coeffs, _ = plan.coeffs(v, 0)
     outs = []
     try:
-        for d in ((0, 0), (25, 25), (500, 500)):
+        for d in ((0, 0), (15, 0), (25, 25), (500, 500)):
             plan.set_sweep_delay(*d)
             seis, hist = plan.forward(coeffs, B, keep_history=True)
             g = plan.adjoint(coeffs, hist, dseis, B)
@@ -244,7 +244,7 @@ def test_sweep_delay_changes_timing_only(cuda):
             outs.append([seis.cpu().numpy()] + [t.cpu().numpy() for t in g])
             del hist
     finally:
-        plan.set_sweep_delay(25, 25)
+        plan.set_sweep_delay(15, 0)                       # the defaults
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert np.array_equal(a_.view(np.uint8), b_.view(np.uint8))
