@@ -436,6 +436,79 @@ __device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w,
     return h;
 }
 
+// ---- The same exchange with a flag word instead of tagged slots (xf_*), so a step's boundary rows
+// go to LDS straight from their row-pair registers and come back straight into the halo pairs, with
+// no register shuffles: per wave and buffer, data slots {pair 0, pair 1} = rows {0, R-1}, {1, R-2}
+// (8 bytes each, one ds_write_b64 per pair) and a per-lane flag = the step's tag, written after the
+// data.  A wave's LDS instructions execute in order, so a reader that issues its flag read before
+// its data reads and finds the tag reads data written before the flag; the buffer-reuse argument is
+// xq_*'s.  Instructions per step and wave: 3 writes, 6 reads and two compares, against xq_*'s 2 + 2
+// plus 8 register moves to build the tagged slots, 6 compares and 2 moves to unpack them (each
+// instruction a wave issues sits on the step's critical path: profiles/r6/issue_pad_ab.txt).
+typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+template <int NW>
+__device__ __forceinline__ void xf_init(unsigned (*xf)[NW][64], int w, int lane)
+{
+    xf[0][w][lane] = XQ_NONE;
+    xf[1][w][lane] = XQ_NONE;
+}
+template <int NW>
+__device__ __forceinline__ void xf_put(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
+                                       unsigned tag, f32x2 p0, f32x2 p1)
+{
+    lds_f32x2 *d = (lds_f32x2 *)&xd[buf][w][0][lane];
+    d[0] = p0;
+    d[64] = p1;
+    asm volatile("" ::: "memory");                        // data before flag (program order = LDS order)
+    *(lds_u32 *)&xf[buf][w][lane] = tag;
+}
+// flags, then rows -1 / R (E1) and -2 / R+1 (E2): the upper wave's rows R-1, R-2 are the .y halves
+// of its pairs 0, 1, the lower wave's rows 0, 1 their .x halves.  Waves 0 / NW-1 read their own
+// slots there (rows outside the region: any value, the halo absorbs it).
+template <int NW>
+__device__ __forceinline__ void xf_load(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
+                                        unsigned &fu, unsigned &fd, f32x2 &E1, f32x2 &E2)
+{
+    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
+    asm volatile("" ::: "memory");
+    fu = *(const lds_u32 *)&xf[buf][wu][lane];
+    fd = *(const lds_u32 *)&xf[buf][wd][lane];
+    asm volatile("" ::: "memory");                        // flags before data
+    const lds_f32 *up = (const lds_f32 *)&xd[buf][wu][0][lane];
+    const lds_f32 *dn = (const lds_f32 *)&xd[buf][wd][0][lane];
+    E1.x = up[1]; E1.y = dn[0];
+    E2.x = up[129]; E2.y = dn[128];
+}
+// both flags carry the tag in every lane (ballots compared with the full wave: no bool round trip
+// through a VGPR, as __all makes; the persistent workgroups are whole waves)
+__device__ __forceinline__ bool xf_ready(unsigned fu, unsigned fd, unsigned tag)
+{
+    return (__builtin_amdgcn_ballot_w64(fu == tag) & __builtin_amdgcn_ballot_w64(fd == tag)) == ~0ull;
+}
+template <int NW>
+__device__ __forceinline__ void xf_wait(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
+                                        unsigned tag, unsigned fu, unsigned fd, f32x2 &E1, f32x2 &E2,
+                                        unsigned *status, bool &live)
+{
+    if (!xf_ready(fu, fd, tag)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_setprio(PT_PRIO_WAIT);        // (see PT_PRIO_*)
+        for (unsigned it = 1;; ++it) {
+            xf_load<NW>(xd, xf, buf, w, lane, fu, fd, E1, E2);
+            if (xf_ready(fu, fd, tag)) break;
+            if (!live) break;
+            if ((it & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s
+                __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                live = false;
+                break;
+            }
+        }
+    }
+    __builtin_amdgcn_s_setprio(PT_PRIO_EDGE);
+}
+
 // the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
 __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
                                           int lane, const float (&fa)[4], const float (&fb)[4], Halo4 &ha,
@@ -1532,11 +1605,13 @@ struct FwdPtArgs {
 // operation order per row).  With this pairing the vertical neighbours of pair i are pairs i-1 /
 // i+1 / i-2 / i+2 except at the slab ends, where four pairs are assembled from the halo rows.  The
 // horizontal taps stay per-row DPP lane shifts (DPP has no packed form).
+// (one descriptor per epoch, HFe = slot n0 + 2, and the step's slot as the scalar offset: no
+// per-step 64-bit address arithmetic; the lanes' offsets stay OOB for cells the wave does not own)
 #define FWD_HIST(V, N)                                                                              \
     {                                                                                               \
-        const __amdgpu_buffer_rsrc_t HR = rsrc_of(a.hist + (size_t)((N) + 2) * L + so, slice_bytes); \
+        const int so_ = ((N) - n0) * L4;                                                            \
         _Pragma("unroll") for (int r = 0; r < R; ++r)                                               \
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(V, r)), HR, hv[r], 0, CP_NT); \
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(V, r)), HFe, hv[r], so_, CP_NT); \
     }
 // the receiver row's values of the epoch's steps n0 .. n0+T-1 (after the hand-off sweep)
 #define FWD_RECORD                                                                                  \
@@ -1589,9 +1664,15 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
             const f32x2 a3 = A[i] * lap;                                                            \
             PRV[i] = tt[i] + a3;                                                                    \
         }                                                                                           \
-        if ((HI) > (LO) && smask) {                  /* pde.py:80-81 (uniform: source row waves) */ \
-            const float add = scol ? bsrc * wv[t] : -0.0f;                                          \
-            if (s1row) {                                                                            \
+        unsigned sm0_ = (HI) > (LO) ? smask : 0u;                                                  \
+        LAUNDER(sm0_);                               /* scalar branch; nothing of it hoisted */     \
+        if (sm0_) {                                  /* pde.py:80-81 (uniform: source row waves) */ \
+            float wt_ = wv[t];                                                                      \
+            asm volatile("" : "+s"(wt_));                                                           \
+            const float add = scol ? bsrc * wt_ : -0.0f;                                            \
+            unsigned one_ = s1row;                                                                  \
+            LAUNDER(one_);                                                                          \
+            if (one_) {                                                                             \
                 const f32x2 av = shalf ? f32x2{-0.0f, add} : f32x2{add, -0.0f};                     \
                 int sp_ = spair;                                                                    \
                 LAUNDER(sp_);                                                                       \
@@ -1608,8 +1689,9 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
     }
 #define FWD_STEP_NB(CUR, PRV)                                                                       \
     {                                                                                               \
-        u32x4 xu_, xd_;                                                                             \
-        xq_load<NW>(xq, n & 1, w, lane, xu_, xd_);                                                  \
+        unsigned fu_, fd_;                                                                          \
+        f32x2 E1, E2;                                                                               \
+        xf_load<NW>(xd, xf, n & 1, w, lane, fu_, fd_, E1, E2);                                      \
         f32x2 xl1[RP], xr1[RP], tt[RP];                                                             \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             const f32x2 c = CUR[i];                                                                 \
@@ -1617,16 +1699,17 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
             xr1[i] = f32x2{dpp_shl1(c.x), dpp_shl1(c.y)};                                           \
             f32x2 a1 = C1[i] * c; const f32x2 a2 = C2v[i] * PRV[i]; a1 = a1 - a2;                   \
             tt[i] = a1;                                                                             \
+            asm volatile("" : "+v"(tt[i]));          /* computed here, not sunk past the wait */    \
         }                                                                                           \
-        const Halo4 h4 = xq_wait<NW>(xq, n & 1, w, lane, (unsigned)n + 1u, xu_, xd_, a.status, live); \
-        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
+        xf_wait<NW>(xd, xf, n & 1, w, lane, (unsigned)n + 1u, fu_, fd_, E1, E2, a.status, live);    \
         FWD_PAIRS_NB(CUR, PRV, 0, 2)                                                                          \
-        if (t + 1 < T)                                                                              \
-            xq_put<NW>(xq, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0].x, PRV[1].x, PRV[1].y, PRV[0].y); \
+        if (t + 1 < T) xf_put<NW>(xd, xf, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0], PRV[1]);  \
         __builtin_amdgcn_s_setprio(PT_PRIO_BODY);                                                   \
         FWD_PAIRS_NB(CUR, PRV, 2, RP)                                                                         \
         if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
-        if (rrow >= 0) {                             /* receiver row: value kept, stored per epoch */ \
+        int rr_ = rrow;                                                                             \
+        LAUNDER(rr_);                                                                               \
+        if (rr_ >= 0) {                              /* receiver row: value kept, stored per epoch */ \
             int rp_ = rpair;                                                                        \
             LAUNDER(rp_);                                                                           \
             f32x2 v_ = PRV[0];                                                                      \
@@ -1642,7 +1725,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     constexpr bool PT_MIR = true;                         // mirrored pairs (barrier-free exchange:
                                                           // 1.364 -> 1.287 ms at configs[1])
     constexpr bool PT_PRIO = true;                        // wave priorities (PT_PRIO_*)
-    __shared__ u32x4 xq[2][NW][2][64];
+    __shared__ f32x2 xd[2][NW][2][64];                    // boundary row pairs (xf_*)
+    __shared__ unsigned xf[2][NW][64];                    // their flags
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
@@ -1659,6 +1743,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         if (gz == g.isz) smask |= 1u << r;
         if (gz == g.igz && ((rin >> r) & 1u)) rrow = r;
     }
+    smask = __builtin_amdgcn_readfirstlane(smask);        // wave-uniform (row-only): scalar branches,
+    rrow = __builtin_amdgcn_readfirstlane(rrow);          // no per-lane masks held across the loop
     const int isx = g.isx[s];
     const bool scol = gx == isx;
     const float bsrc = (smask != 0) ? AL[4 * g.cstride + (size_t)g.isz * g.ld + isx] : 0.0f;
@@ -1671,7 +1757,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     const bool rec = rrow >= 0 && xin && rcv0 >= 0;
     const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
     // source / receiver rows as (row pair, half): the step touches one pair, not all eight rows
-    const bool s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
+    const unsigned s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
     const int sr1 = smask ? __builtin_ctz(smask) : 0;
     // wave-uniform by construction; readfirstlane makes that visible to the compiler (LAUNDER "+s")
     const int spair = __builtin_amdgcn_readfirstlane(PT_MIR ? (sr1 < RP ? sr1 : R - 1 - sr1) : sr1 % RP);
@@ -1681,7 +1767,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
 #pragma unroll
     for (int t = 0; t < T; ++t) rv[t] = 0.0f;
     const size_t L = g.level;
-    const int slice_bytes = (int)(g.slice * 4);
+    const int L4 = (int)(L * 4);                          // bytes per history slot (< 2 GB: resident surveys)
     int hv[R];                                            // history store offset of (row, lane), OOB if not own
 #pragma unroll
     for (int r = 0; r < R; ++r) hv[r] = (((rin >> r) & 1u) && xin) ? (PT_ROFS(r) + gx) * 4 : OOB;
@@ -1696,12 +1782,13 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(t, a.nt - 1));
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
 #define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(n0 + T + t, a.nt - 1));
-    xq_init<NW>(xq, w, lane);                             // no slot matches a tag until written
+    xf_init<NW>(xf, w, lane);                             // no flag matches a tag until written
     __syncthreads();
-    xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // P_0 = 0, step 0's tag
+    xf_put<NW>(xd, xf, 0, w, lane, 1u, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f});   // P_0 = 0, step 0's tag
 #define FWD_STEP_SEL FWD_STEP_NB
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
+        const __amdgpu_buffer_rsrc_t HFe = rsrc_of(a.hist + (size_t)(n0 + 2) * L + so);   // FWD_HIST
         PT_PROF(tsw)
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -1727,7 +1814,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
             // the next step's boundary rows, with the halo cells the sweep reloaded
-            xq_put<NW>(xq, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0].x, P1[1].x, P1[1].y, P1[0].y);
+            xf_put<NW>(xd, xf, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0], P1[1]);
         }
         FWD_RECORD
     }
@@ -2165,7 +2252,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     constexpr bool PT_PRIO = ADJ_NB;                      // wave priorities (PT_PRIO_*)
     constexpr bool PT_MIR = ADJ_NB;                       // mirrored pairs for the exchange's boundary rows
     __shared__ float xch[2][NW][4][64];                   // (the unused exchange is not allocated)
-    __shared__ u32x4 xq[2][NW][2][64];
+    __shared__ u32x4 xq[2][NW][2][64];                    // (the flag form, xf_*, needs more VGPRs here)
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
