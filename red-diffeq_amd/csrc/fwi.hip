@@ -331,45 +331,24 @@ __device__ __forceinline__ Halo4 exchange_nw(float (*xch)[NW][4][64], int buf, i
     return h;
 }
 
-// exchange_nw in two halves, so a step can schedule work between the barrier and the reads' use
-template <int NW>
-__device__ __forceinline__ void xch_put(float (*xch)[NW][4][64], int buf, int w, int lane, float top0, float top1,
-                                        float bot1, float bot0)
-{
-    xch[buf][w][0][lane] = top0;
-    xch[buf][w][1][lane] = top1;
-    xch[buf][w][2][lane] = bot1;
-    xch[buf][w][3][lane] = bot0;
-}
-template <int NW>
-__device__ __forceinline__ Halo4 xch_get(float (*xch)[NW][4][64], int buf, int w, int lane)
-{
-    Halo4 h;
-    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
-    h.u2 = xch[buf][wu][2][lane];
-    h.u1 = xch[buf][wu][3][lane];
-    h.d1 = xch[buf][wd][0][lane];
-    h.d2 = xch[buf][wd][1][lane];
-    return h;
-}
-
-// ---- Barrier-free wave-to-wave exchange of the persistent forward and adjoint.
-// A wave's boundary rows go to LDS as 16-byte slots {row a, tag, row b, tag} (top: rows 0, 1;
-// bottom: rows R-2, R-1), double-buffered by step parity, and the neighbour waves poll their slot
-// until both tags carry the step's number: each wave waits only for the two waves it reads from,
-// not for all NW waves at a workgroup barrier, and a wave publishes its boundary rows as soon as
-// they are computed (its interior rows follow), so the neighbours' data is normally there at the
-// first read.  Overwrite safety of the two buffers: a wave writes step n+1's rows only after it
-// read both neighbours' step-n rows, which they wrote after reading its step n-1 rows (LDS
-// instructions of one wave execute in order).  Each 8-byte half carries its own tag, so a torn
-// 16-byte read is re-polled, never consumed.
+// ---- Barrier-free wave-to-wave exchange of the persistent forward and adjoint.  Each step a wave
+// needs two rows above and below its own from its neighbour waves; instead of a workgroup barrier per
+// step, each wave waits only for the two waves it reads from, and publishes its boundary rows as soon
+// as they are computed (its interior rows follow), so the neighbours' rows are normally there at the
+// first read.  History of the form (configs[1], profiles/r3/barrier_free_ab.txt, profiles/r6/
+// fwd_xf_ab.txt, mailbox_ab.txt): 16-byte tagged slots {row, tag, row, tag} (round 3: forward 1.364 ->
+// 1.31 ms); a per-lane flag word after the rows, which drops the 8 register moves that built the
+// tagged slots and the 6 compares that checked them (1.208 -> 1.111 ms with the trims of the same
+// change; every instruction a wave issues sits on the step's path: profiles/r6/issue_pad_ab.txt); the
+// mailbox below (same speed for the forward, adjoint 1.560 -> 1.548 ms: it needs fewer VGPRs, which
+// the 128-VGPR adjoint has none of).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-written slot
-// Wave priorities of the barrier-free persistent forward (s_setprio; the SIMD's arbiter issues the
-// higher-priority wave first).  A wave polling its neighbours' LDS slots (xq_wait) or the hand-off
+constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // flag of a never-written inbox
+// Wave priorities of the barrier-free persistent kernels (s_setprio; the SIMD's arbiter issues the
+// higher-priority wave first).  A wave polling its LDS inbox (xm_wait) or the hand-off
 // granules (PT_SWEEP) drops to WAIT, so its spin loop does not take issue cycles from the waves still
 // computing; a wave that got its neighbours' rows runs its two boundary row pairs (what the neighbours
 // wait for next) at EDGE, then its interior pairs at BODY.  Configs[1] forward, interleaved x3
@@ -379,48 +358,66 @@ constexpr unsigned XQ_NONE = 0xFFFFFFFFu;                 // tag of a never-writ
 // per step the adjoint gained nothing, 1.638 -> 1.646 ms with the sweep at WAIT; its barrier-free form,
 // ADJR_STEP_NB, uses the same exchange and priorities: 1.646 -> 1.577 ms.)
 constexpr int PT_PRIO_WAIT = 0, PT_PRIO_BODY = 1, PT_PRIO_SWEPT = 3, PT_PRIO_EDGE = 3;
+// ---- Mailbox exchange (xm_*): each wave owns an inbox per buffer, {rows -1, R, -2, R+1} as 16 bytes
+// (halo pairs E1 = {-1, R}, E2 = {-2, R+1}: one ds_read_b128 straight into them) and a flag pair
+// {from above, from below}.  A wave writes its rows R-1, R-2 into the lower wave's inbox and its rows
+// 0, 1 into the upper wave's (ds_write2_b32 straight from its row-pair registers), each followed by
+// its flag there (the step's tag); waves 0 / NW-1 fill their own inbox's missing half (rows outside
+// the region: any value, the halo absorbs it).  A wave's LDS instructions execute in order, so a
+// reader that reads its flags before its rows and finds both tags reads rows written before them;
+// buffer reuse is safe without a barrier (a wave writes step n+1's rows only after it read its step-n inbox,
+// whose writers wrote it after reading their step n-1 inboxes).  Per step and wave: 4 writes, 2 reads
+// and 2 compares, no register moves on either side.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) unsigned lds_uint;
+template <int NW> struct XmBox { f32x4 rows[2][NW][64]; u32x4 flags[2][NW][64]; };   // [buffer][wave][lane]
 template <int NW>
-__device__ __forceinline__ void xq_init(u32x4 (*xq)[NW][2][64], int w, int lane)
+__device__ __forceinline__ void xm_init(XmBox<NW> &m, int w, int lane)
 {
-    const u32x4 z = {0u, XQ_NONE, 0u, XQ_NONE};
-#pragma unroll
-    for (int b = 0; b < 2; ++b) { xq[b][w][0][lane] = z; xq[b][w][1][lane] = z; }
+    const u32x4 z = {XQ_NONE, XQ_NONE, 0u, 0u};
+    m.flags[0][w][lane] = z;
+    m.flags[1][w][lane] = z;
 }
-// LDS-qualified slot pointers: ds_read_b128 / ds_write_b128 (a volatile generic pointer would be
-// flat accesses with sc0 sc1 and a full wait after each); the poll re-reads after a compiler memory
-// barrier, so no load is hoisted out of it.
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+// p0 = rows {0, R-1}, p1 = rows {1, R-2} (mirrored pairs 0, 1)
 template <int NW>
-__device__ __forceinline__ void xq_put(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, unsigned tag, float top0,
-                                       float top1, float bot1, float bot0)
+__device__ __forceinline__ void xm_put(XmBox<NW> &m, int buf, int w, int lane, unsigned tag, f32x2 p0, f32x2 p1)
 {
-    lds_u32x4 *q = (lds_u32x4 *)&xq[buf][w][0][lane];
-    q[0] = u32x4{__float_as_uint(top0), tag, __float_as_uint(top1), tag};
-    q[64] = u32x4{__float_as_uint(bot1), tag, __float_as_uint(bot0), tag};
+    constexpr int FLAGS = NW * 64 * 4 * 2;                // flags[buf] - rows[buf] in floats (same layout)
+    lds_float *dn = (lds_float *)&m.rows[buf][w < NW - 1 ? w + 1 : w][lane] + (w < NW - 1 ? 0 : 1);
+    lds_float *up = (lds_float *)&m.rows[buf][w > 0 ? w - 1 : w][lane] + (w > 0 ? 1 : 0);
+    dn[0] = p0.y; dn[2] = p1.y;                           // the lower wave's rows -1, -2
+    up[0] = p0.x; up[2] = p1.x;                           // the upper wave's rows R, R+1
+    asm volatile("" ::: "memory");                        // rows before flags (program order = LDS order)
+    ((lds_uint *)dn)[FLAGS] = tag;
+    ((lds_uint *)up)[FLAGS] = tag;
 }
-// rows -2, -1 (the upper wave's R-2, R-1) and R, R+1 (the lower wave's 0, 1); waves 0 / NW-1 read
-// their own slot there (rows outside the region: any value, the halo absorbs it).  `live` false =
-// the launch already failed: no wait.
-// Two halves so a step can run its halo-free work while the reads are in flight: xq_load issues
-// the reads, xq_wait checks the tags (re-polling until they match) and unpacks the rows.
 template <int NW>
-__device__ __forceinline__ void xq_load(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, u32x4 &u, u32x4 &d)
+__device__ __forceinline__ void xm_load(XmBox<NW> &m, int buf, int w, int lane, u32x2 &f, f32x2 &E1, f32x2 &E2)
 {
-    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
     asm volatile("" ::: "memory");
-    u = *(const lds_u32x4 *)&xq[buf][wu][1][lane];
-    d = *(const lds_u32x4 *)&xq[buf][wd][0][lane];
+    f = *(const lds_u32x2 *)&m.flags[buf][w][lane];
+    asm volatile("" ::: "memory");                        // flags before rows
+    const f32x4 e = *(const lds_f32x4 *)&m.rows[buf][w][lane];
+    E1 = f32x2{e.x, e.y};
+    E2 = f32x2{e.z, e.w};
+}
+__device__ __forceinline__ bool xm_ready(u32x2 f, unsigned tag)
+{
+    return (__builtin_amdgcn_ballot_w64(f.x == tag) & __builtin_amdgcn_ballot_w64(f.y == tag)) == ~0ull;
 }
 template <int NW>
-__device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w, int lane, unsigned tag, u32x4 u,
-                                         u32x4 d, unsigned *status, bool &live)
+__device__ __forceinline__ void xm_wait(XmBox<NW> &m, int buf, int w, int lane, unsigned tag, u32x2 f, f32x2 &E1,
+                                        f32x2 &E2, unsigned *status, bool &live)
 {
-    if (!__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) {
+    if (!xm_ready(f, tag)) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_s_setprio(PT_PRIO_WAIT);        // (see PT_PRIO_*)
         for (unsigned it = 1;; ++it) {
-            xq_load<NW>(xq, buf, w, lane, u, d);
-            if (__all(u.y == tag && u.w == tag && d.y == tag && d.w == tag)) break;
+            xm_load<NW>(m, buf, w, lane, f, E1, E2);
+            if (xm_ready(f, tag)) break;
             if (!live) break;
             if ((it & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s
                 __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -430,84 +427,8 @@ __device__ __forceinline__ Halo4 xq_wait(u32x4 (*xq)[NW][2][64], int buf, int w,
         }
     }
     __builtin_amdgcn_s_setprio(PT_PRIO_EDGE);
-    Halo4 h;
-    h.u2 = __uint_as_float(u.x); h.u1 = __uint_as_float(u.z);
-    h.d1 = __uint_as_float(d.x); h.d2 = __uint_as_float(d.z);
-    return h;
 }
 
-// ---- The same exchange with a flag word instead of tagged slots (xf_*), so a step's boundary rows
-// go to LDS straight from their row-pair registers and come back straight into the halo pairs, with
-// no register shuffles: per wave and buffer, data slots {pair 0, pair 1} = rows {0, R-1}, {1, R-2}
-// (8 bytes each, one ds_write_b64 per pair) and a per-lane flag = the step's tag, written after the
-// data.  A wave's LDS instructions execute in order, so a reader that issues its flag read before
-// its data reads and finds the tag reads data written before the flag; the buffer-reuse argument is
-// xq_*'s.  Instructions per step and wave: 3 writes, 6 reads and two compares, against xq_*'s 2 + 2
-// plus 8 register moves to build the tagged slots, 6 compares and 2 moves to unpack them (each
-// instruction a wave issues sits on the step's critical path: profiles/r6/issue_pad_ab.txt).
-typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
-typedef __attribute__((address_space(3))) float lds_f32;
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-template <int NW>
-__device__ __forceinline__ void xf_init(unsigned (*xf)[NW][64], int w, int lane)
-{
-    xf[0][w][lane] = XQ_NONE;
-    xf[1][w][lane] = XQ_NONE;
-}
-template <int NW>
-__device__ __forceinline__ void xf_put(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
-                                       unsigned tag, f32x2 p0, f32x2 p1)
-{
-    lds_f32x2 *d = (lds_f32x2 *)&xd[buf][w][0][lane];
-    d[0] = p0;
-    d[64] = p1;
-    asm volatile("" ::: "memory");                        // data before flag (program order = LDS order)
-    *(lds_u32 *)&xf[buf][w][lane] = tag;
-}
-// flags, then rows -1 / R (E1) and -2 / R+1 (E2): the upper wave's rows R-1, R-2 are the .y halves
-// of its pairs 0, 1, the lower wave's rows 0, 1 their .x halves.  Waves 0 / NW-1 read their own
-// slots there (rows outside the region: any value, the halo absorbs it).
-template <int NW>
-__device__ __forceinline__ void xf_load(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
-                                        unsigned &fu, unsigned &fd, f32x2 &E1, f32x2 &E2)
-{
-    const int wu = w > 0 ? w - 1 : 0, wd = w < NW - 1 ? w + 1 : NW - 1;
-    asm volatile("" ::: "memory");
-    fu = *(const lds_u32 *)&xf[buf][wu][lane];
-    fd = *(const lds_u32 *)&xf[buf][wd][lane];
-    asm volatile("" ::: "memory");                        // flags before data
-    const lds_f32 *up = (const lds_f32 *)&xd[buf][wu][0][lane];
-    const lds_f32 *dn = (const lds_f32 *)&xd[buf][wd][0][lane];
-    E1.x = up[1]; E1.y = dn[0];
-    E2.x = up[129]; E2.y = dn[128];
-}
-// both flags carry the tag in every lane (ballots compared with the full wave: no bool round trip
-// through a VGPR, as __all makes; the persistent workgroups are whole waves)
-__device__ __forceinline__ bool xf_ready(unsigned fu, unsigned fd, unsigned tag)
-{
-    return (__builtin_amdgcn_ballot_w64(fu == tag) & __builtin_amdgcn_ballot_w64(fd == tag)) == ~0ull;
-}
-template <int NW>
-__device__ __forceinline__ void xf_wait(f32x2 (*xd)[NW][2][64], unsigned (*xf)[NW][64], int buf, int w, int lane,
-                                        unsigned tag, unsigned fu, unsigned fd, f32x2 &E1, f32x2 &E2,
-                                        unsigned *status, bool &live)
-{
-    if (!xf_ready(fu, fd, tag)) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_setprio(PT_PRIO_WAIT);        // (see PT_PRIO_*)
-        for (unsigned it = 1;; ++it) {
-            xf_load<NW>(xd, xf, buf, w, lane, fu, fd, E1, E2);
-            if (xf_ready(fu, fd, tag)) break;
-            if (!live) break;
-            if ((it & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {   // 1 s
-                __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                live = false;
-                break;
-            }
-        }
-    }
-    __builtin_amdgcn_s_setprio(PT_PRIO_EDGE);
-}
 
 // the same for two fields with ONE barrier (adjoint: A*L_{k+1} and the history P_{k-1})
 __device__ __forceinline__ void exchange2(float (*xa)[TB_NW][4][64], float (*xb)[TB_NW][4][64], int buf, int w,
@@ -1613,17 +1534,26 @@ struct FwdPtArgs {
         _Pragma("unroll") for (int r = 0; r < R; ++r)                                               \
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PT_AT(V, r)), HFe, hv[r], so_, CP_NT); \
     }
-// the receiver row's values of the epoch's steps n0 .. n0+T-1 (after the hand-off sweep)
+// the receiver row's values of the epoch's steps n0 .. n0+T-1 (after the hand-off sweep): one buffer
+// store per recorded step (lanes without a receiver at an OOB offset, the record row as the scalar
+// offset), the per-column receiver lists only where a column has several
 #define FWD_RECORD                                                                                  \
-    if (rrow >= 0) {                                                                                \
-        _Pragma("unroll") for (int t = 0; t < T; ++t) {                                             \
-            const int n = n0 + t;                                                                   \
-            const int ri_ = n < a.nt ? rec_index(n, g.st) : -1;                                     \
-            if (ri_ >= 0) {                                                                         \
-                float *SK = a.seis + ((size_t)bs * g.nrec + ri_) * g.ng;                            \
-                if (rec) SK[rcv0] = rv[t];                                                          \
-                if (rmulti && rec)                           /* several receivers in one column */  \
-                    for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = rv[t];                    \
+    {                                                                                               \
+        int rrw_ = rrow;                                                                            \
+        LAUNDER(rrw_);                                                                              \
+        if (rrw_ >= 0) {                                                                            \
+            _Pragma("unroll") for (int t = 0; t < T; ++t) {                                         \
+                const int n = n0 + t;                                                               \
+                const int ri_ = n < a.nt ? rec_index(n, g.st) : -1;                                 \
+                if (ri_ >= 0) {                                                                     \
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rv[t]), SKR, vrec, ri_ * ng4, 0); \
+                    unsigned rm_ = rmulti;                                                          \
+                    LAUNDER(rm_);                                                                   \
+                    if (rm_ && rec) {                        /* several receivers in one column */  \
+                        float *SK = a.seis + ((size_t)bs * g.nrec + ri_) * g.ng;                    \
+                        for (int j = rs + 1; j < re; ++j) SK[g.rcv_list[j]] = rv[t];                \
+                    }                                                                               \
+                }                                                                                   \
             }                                                                                       \
         }                                                                                           \
     }
@@ -1689,9 +1619,9 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
     }
 #define FWD_STEP_NB(CUR, PRV)                                                                       \
     {                                                                                               \
-        unsigned fu_, fd_;                                                                          \
+        u32x2 f_;                                                                                   \
         f32x2 E1, E2;                                                                               \
-        xf_load<NW>(xd, xf, n & 1, w, lane, fu_, fd_, E1, E2);                                      \
+        xm_load<NW>(xm, n & 1, w, lane, f_, E1, E2);                                                \
         f32x2 xl1[RP], xr1[RP], tt[RP];                                                             \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             const f32x2 c = CUR[i];                                                                 \
@@ -1701,9 +1631,9 @@ __device__ __forceinline__ f32x2 swp(f32x2 v) { return f32x2{v.y, v.x}; }
             tt[i] = a1;                                                                             \
             asm volatile("" : "+v"(tt[i]));          /* computed here, not sunk past the wait */    \
         }                                                                                           \
-        xf_wait<NW>(xd, xf, n & 1, w, lane, (unsigned)n + 1u, fu_, fd_, E1, E2, a.status, live);    \
+        xm_wait<NW>(xm, n & 1, w, lane, (unsigned)n + 1u, f_, E1, E2, a.status, live);              \
         FWD_PAIRS_NB(CUR, PRV, 0, 2)                                                                          \
-        if (t + 1 < T) xf_put<NW>(xd, xf, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0], PRV[1]);  \
+        if (t + 1 < T) xm_put<NW>(xm, (n + 1) & 1, w, lane, (unsigned)n + 2u, PRV[0], PRV[1]);      \
         __builtin_amdgcn_s_setprio(PT_PRIO_BODY);                                                   \
         FWD_PAIRS_NB(CUR, PRV, 2, RP)                                                                         \
         if (a.hist && (t + 1 < T || e + 1 == nep)) FWD_HIST(PRV, n)                                 \
@@ -1725,8 +1655,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     constexpr bool PT_MIR = true;                         // mirrored pairs (barrier-free exchange:
                                                           // 1.364 -> 1.287 ms at configs[1])
     constexpr bool PT_PRIO = true;                        // wave priorities (PT_PRIO_*)
-    __shared__ f32x2 xd[2][NW][2][64];                    // boundary row pairs (xf_*)
-    __shared__ unsigned xf[2][NW][64];                    // their flags
+    __shared__ XmBox<NW> xm;                              // the waves' inboxes (xm_*)
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
     const float *AL = a.coeffs + (size_t)b * g.slice;
@@ -1755,7 +1684,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
         rcv0 = rs < re ? g.rcv_list[rs] : -1;             // the (usually only) receiver of this column
     }
     const bool rec = rrow >= 0 && xin && rcv0 >= 0;
-    const bool rmulti = __any(re - rs > 1);               // wave-uniform: a column with several receivers
+    const unsigned rmulti = __any(re - rs > 1);           // wave-uniform: a column with several receivers
+    const __amdgpu_buffer_rsrc_t SKR = rsrc_of(a.seis + (size_t)bs * g.nrec * g.ng);   // FWD_RECORD
+    const int vrec = rec ? rcv0 * 4 : OOB, ng4 = g.ng * 4;
     // source / receiver rows as (row pair, half): the step touches one pair, not all eight rows
     const unsigned s1row = smask != 0 && (smask & (smask - 1u)) == 0;   // one source row in the slab
     const int sr1 = smask ? __builtin_ctz(smask) : 0;
@@ -1782,9 +1713,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
     for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(t, a.nt - 1));
     __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
 #define FWD_ISSUE _Pragma("unroll") for (int t = 0; t < T; ++t) wv[t] = wav_s(a.wav, min(n0 + T + t, a.nt - 1));
-    xf_init<NW>(xf, w, lane);                             // no flag matches a tag until written
+    xm_init<NW>(xm, w, lane);                             // no flag matches a tag until written
     __syncthreads();
-    xf_put<NW>(xd, xf, 0, w, lane, 1u, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f});   // P_0 = 0, step 0's tag
+    xm_put<NW>(xm, 0, w, lane, 1u, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f});   // P_0 = 0, step 0's tag
 #define FWD_STEP_SEL FWD_STEP_NB
     for (int e = 0; e < nep; ++e) {
         const int n0 = e * T;
@@ -1814,7 +1745,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_pt(FwdPtArgs a)
             if (a.hist) FWD_HIST(P1, n0 + T - 1)          // the epoch's last step (own cells: the sweep
                                                           // reloads halo cells only)
             // the next step's boundary rows, with the halo cells the sweep reloaded
-            xf_put<NW>(xd, xf, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0], P1[1]);
+            xm_put<NW>(xm, (n0 + T) & 1, w, lane, (unsigned)(n0 + T) + 1u, P1[0], P1[1]);
         }
         FWD_RECORD
     }
@@ -2133,7 +2064,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             u[i] = fma2(-T1v[i], P1[i], P0[i]);                                                     \
             u[i] = fma2(T2v[i], P2[i], u[i]);                                                       \
         }                                                                                           \
-        if (srow >= 0) {                             /* the forward's source add, undone */        \
+        int sg_ = srow;                                                                             \
+        LAUNDER(sg_);                                                                               \
+        if (sg_ >= 0) {                              /* the forward's source add, undone */        \
             int sp_ = spair;                                                                        \
             LAUNDER(sp_);                                                                           \
             const float sa_ = scol ? bsrc * (WK) : 0.0f;                                            \
@@ -2145,7 +2078,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
 #define ADJR_GRAD_POST(CU, LN, WK, P1)                                                              \
     {                                                                                               \
-        if (srow >= 0) {                                                                            \
+        int sg_ = srow;                                                                             \
+        LAUNDER(sg_);                                                                               \
+        if (sg_ >= 0) {                                                                             \
             int sp_ = spair;                                                                        \
             LAUNDER(sp_);                                                                           \
             f32x2 lp_ = LN[0];                                                                      \
@@ -2199,7 +2134,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
     }
 
-// Barrier-free adjoint step (mirrored pairs, the forward's tagged LDS exchange xq_*): the wave waits
+// Barrier-free adjoint step (mirrored pairs, the forward's LDS mailbox xm_*): the wave waits
 // only for its two neighbours' A L_{k+1} boundary rows, computes its two boundary pairs (receiver
 // residual included), publishes their A L_k rows for the next step, then its interior pair.  Per row
 // the operations and their order are ADJR_STEP's (m1 + p1 commutes: same bits).  (The gradient's
@@ -2217,7 +2152,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
             PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
         }                                                                                           \
-        if (rrow >= 0 && rec_index(k - 1, g.st) >= 0) {   /* uniform: the receiver row's wave */    \
+        int rr_ = rrow;                                                                             \
+        LAUNDER(rr_);                                                                               \
+        if ((HI) > (LO) && rr_ >= 0 && rec_index(k - 1, g.st) >= 0) {   /* the receiver row's wave */ \
             int rp_ = rpair;                                                                        \
             LAUNDER(rp_);                                                                           \
             const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
@@ -2228,16 +2165,14 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     {                                                                                               \
         if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
         const float dcur = dv[t];                                                                   \
-        u32x4 xu_, xd_;                                                                             \
-        xq_load<NW>(xq, j & 1, w, lane, xu_, xd_);                                                  \
+        u32x2 f_;                                                                                   \
+        f32x2 E1, E2;                                                                               \
+        xm_load<NW>(xm, j & 1, w, lane, f_, E1, E2);                                                \
         f32x2 q[RP];                                                                                \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) q[i] = A[i] * CUR[i];                         \
-        const Halo4 h4 = xq_wait<NW>(xq, j & 1, w, lane, (unsigned)j + 1u, xu_, xd_, a.status, live); \
-        const f32x2 E1 = {h4.u1, h4.d1}, E2 = {h4.u2, h4.d2};                                       \
+        xm_wait<NW>(xm, j & 1, w, lane, (unsigned)j + 1u, f_, E1, E2, a.status, live);              \
         ADJR_PAIRS_NB(CUR, PRV, 0, 2)                                                               \
-        if (t + 1 < T)                                                                              \
-            xq_put<NW>(xq, (j + 1) & 1, w, lane, (unsigned)j + 2u, A[0].x * PRV[0].x, A[1].x * PRV[1].x, \
-                       A[1].y * PRV[1].y, A[0].y * PRV[0].y);                                       \
+        if (t + 1 < T) xm_put<NW>(xm, (j + 1) & 1, w, lane, (unsigned)j + 2u, A[0] * PRV[0], A[1] * PRV[1]); \
         __builtin_amdgcn_s_setprio(PT_PRIO_BODY);                                                   \
         ADJR_PAIRS_NB(CUR, PRV, 2, RP)                                                              \
         if (t + 1 < T || last) ADJR_GRAD(CUR, PRV, wv[t], P0, P1, P2)                               \
@@ -2252,7 +2187,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     constexpr bool PT_PRIO = ADJ_NB;                      // wave priorities (PT_PRIO_*)
     constexpr bool PT_MIR = ADJ_NB;                       // mirrored pairs for the exchange's boundary rows
     __shared__ float xch[2][NW][4][64];                   // (the unused exchange is not allocated)
-    __shared__ u32x4 xq[2][NW][2][64];                    // (the flag form, xf_*, needs more VGPRs here)
+    __shared__ XmBox<NW> xm;                              // the waves' inboxes (xm_*)
     __shared__ double red[64 * NW];
     const TBGeo &g = a.g;
     PT_REGION_INIT(NW, RW)
@@ -2329,9 +2264,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     unsigned long long tsw = 0, tst = 0, tpb = 0, tm = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tfp = 0, npass = 0;                // profile: first-pass latency, sweep passes
     if constexpr (ADJ_NB) {
-        xq_init<NW>(xq, w, lane);                         // no slot matches a tag until written
+        xm_init<NW>(xm, w, lane);                         // no flag matches a tag until written
         __syncthreads();
-        xq_put<NW>(xq, 0, w, lane, 1u, 0.0f, 0.0f, 0.0f, 0.0f);   // A L_{nt+1} = 0, step 0's tag
+        xm_put<NW>(xm, 0, w, lane, 1u, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f});   // A L_{nt+1} = 0, step 0's tag
     }
 #define ADJR_STEP_SEL(...) { if constexpr (ADJ_NB) ADJR_STEP_NB(__VA_ARGS__) else ADJR_STEP(__VA_ARGS__) }
     for (int e = 0; e < nep; ++e) {
@@ -2365,8 +2300,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
             PT_SWEEP_DELAY()
             PT_SWEEP(GR, tag, L0, L1, PT_ADJ_SG)
             if constexpr (ADJ_NB)   // the next step's boundary rows, with the halo cells the sweep reloaded
-                xq_put<NW>(xq, (e + 1) * T & 1, w, lane, (unsigned)((e + 1) * T) + 1u, A[0].x * L1[0].x,
-                           A[1].x * L1[1].x, A[1].y * L1[1].y, A[0].y * L1[0].y);
+                xm_put<NW>(xm, (e + 1) * T & 1, w, lane, (unsigned)((e + 1) * T) + 1u, A[0] * L1[0], A[1] * L1[1]);
             ADJ_ISSUE
             PT_PROF(tsw)
         }

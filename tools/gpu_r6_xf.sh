@@ -7,4 +7,4 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fwi.py -m gpu -x -q --timeout 120 --timeout-method thread \
     > $O/fwi_tests.log 2>&1 || { echo "fwi pytest rc=$?"; tail -30 $O/fwi_tests.log; exit 1; }
 tail -1 $O/fwi_tests.log
-bash tools/gpu_r6_spin.sh $O/ab head || exit $?
+bash tools/gpu_r6_spin.sh $O/ab ${2:-head} || exit $?
