@@ -2054,51 +2054,38 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
 
 // gradient of step k (CU = L_{k+1}, LN = L_k; wavelet sample WK = w[k-1]; window P0 = P_k,
-// P1 = P_{k-1}, P2 = P_{k-2}), in two halves: PRE forms d = 2c1 P_{k-1} + lap'(P_{k-1}) from the
-// history alone (no L, no neighbour data: it runs while the step's halo reads are in flight),
-// POST accumulates with L_k.
-#define ADJR_GRAD_PRE(WK, P0, P1, P2)                                                               \
-    {                                                                                               \
+// P1 = P_{k-1}, P2 = P_{k-2}): u = lap'(P_{k-1}) x A from the history (the forward's source add undone
+// on the source row), d = 2c1 P_{k-1} + lap'(P_{k-1}), then the accumulations with L_k; the source
+// row's two terms share one scalar branch.
+#define ADJR_GRAD(CU, LN, WK, P0, P1, P2)                                                           \
+    if (grad) {                                                                                     \
         f32x2 u[RP];                                                                                \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
             u[i] = fma2(-T1v[i], P1[i], P0[i]);                                                     \
             u[i] = fma2(T2v[i], P2[i], u[i]);                                                       \
         }                                                                                           \
-        int sg_ = srow;                                                                             \
-        LAUNDER(sg_);                                                                               \
-        if (sg_ >= 0) {                              /* the forward's source add, undone */        \
-            int sp_ = spair;                                                                        \
-            LAUNDER(sp_);                                                                           \
-            const float sa_ = scol ? bsrc * (WK) : 0.0f;                                            \
-            const f32x2 sv_ = shalf ? f32x2{0.0f, sa_} : f32x2{sa_, 0.0f};                          \
-            _Pragma("unroll") for (int i = 0; i < RP; ++i) if (i == sp_) u[i] = u[i] - sv_;          \
-        }                                                                                           \
-        /* A d = A 2c1 P_{k-1} + u: the 1/A is applied once to the sum (gA = sum L A d / A) */     \
-        _Pragma("unroll") for (int i = 0; i < RP; ++i) dd[i] = fma2(A[i], kC1X2 * P1[i], u[i]);      \
-    }
-#define ADJR_GRAD_POST(CU, LN, WK, P1)                                                              \
-    {                                                                                               \
-        int sg_ = srow;                                                                             \
+        int sg_ = srow;                              /* one scalar branch for both source terms */  \
         LAUNDER(sg_);                                                                               \
         if (sg_ >= 0) {                                                                             \
             int sp_ = spair;                                                                        \
             LAUNDER(sp_);                                                                           \
+            const float sa_ = scol ? bsrc * (WK) : 0.0f;  /* the forward's source add, undone */    \
+            const f32x2 sv_ = shalf ? f32x2{0.0f, sa_} : f32x2{sa_, 0.0f};                          \
             f32x2 lp_ = LN[0];                                                                      \
-            _Pragma("unroll") for (int i = 1; i < RP; ++i) if (i == sp_) lp_ = LN[i];                \
+            _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                         \
+                if (i == sp_) u[i] = u[i] - sv_;                                                    \
+                if (i > 0 && i == sp_) lp_ = LN[i];                                                 \
+            }                                                                                       \
             const float ls_ = shalf ? lp_.y : lp_.x;                                                \
-            const float gb = scol ? ls_ * (WK) : -0.0f;                                             \
+            const float gb = scol ? ls_ * (WK) : -0.0f;  /* gbeta: the source cell's lane only */   \
             gbacc = gbacc + gb;                                                                     \
         }                                                                                           \
+        /* A d = A 2c1 P_{k-1} + u: the 1/A is applied once to the sum (gA = sum L A d / A) */     \
         _Pragma("unroll") for (int i = 0; i < RP; ++i) {                                             \
-            GA[i] = fma2(LN[i], dd[i], GA[i]);                                                      \
+            const f32x2 dd = fma2(A[i], kC1X2 * P1[i], u[i]);                                       \
+            GA[i] = fma2(LN[i], dd, GA[i]);                                                         \
             GK[i] = fma2(P1[i], CU[i] - LN[i], GK[i]);                                              \
         }                                                                                           \
-    }
-#define ADJR_GRAD(CU, LN, WK, P0, P1, P2)                                                           \
-    if (grad) {                                                                                     \
-        f32x2 dd[RP];                                                                               \
-        ADJR_GRAD_PRE(WK, P0, P1, P2)                                                               \
-        ADJR_GRAD_POST(CU, LN, WK, P1)                                                              \
     }
 
 // one adjoint step k: CUR = L_{k+1}, PRV = L_{k+2} -> L_k; window P0 / P1 / P2 as ADJR_GRAD;
@@ -2152,9 +2139,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
             const f32x2 nb = fma2(kC3, n2, kC2 * n1);                                               \
             PRV[i] = fma2(T1v[i], CUR[i], fma2(-T2v[i], PRV[i], nb));                               \
         }                                                                                           \
-        int rr_ = rrow;                                                                             \
+        int rr_ = (LO) == 0 ? rlo : rhi;             /* the receiver's pair is in this half */      \
         LAUNDER(rr_);                                                                               \
-        if ((HI) > (LO) && rr_ >= 0 && rec_index(k - 1, g.st) >= 0) {   /* the receiver row's wave */ \
+        if ((HI) > (LO) && rr_ && rec_index(k - 1, g.st) >= 0) {                                    \
             int rp_ = rpair;                                                                        \
             LAUNDER(rp_);                                                                           \
             const f32x2 dv_ = rhalf ? f32x2{-0.0f, dcur} : f32x2{dcur, -0.0f};   /* -0: no-op */     \
@@ -2163,7 +2150,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pt(AdjPtArgs a)
     }
 #define ADJR_STEP_NB(CUR, PRV, P0, P1, P2, PN)                                                      \
     {                                                                                               \
-        if (grad && k >= 2) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                                    \
+        if (ldall || (grad && k >= 2)) ADJR_LOAD(PN, HRe, (T - 1 - t) * L4)                         \
         const float dcur = dv[t];                                                                   \
         u32x2 f_;                                                                                   \
         f32x2 E1, E2;                                                                               \
@@ -2215,6 +2202,9 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
     const int spair = __builtin_amdgcn_readfirstlane(srow < 0 ? 0 : PT_MIR ? (srow < RP ? srow : R - 1 - srow) : srow % RP);
     const int rpair = __builtin_amdgcn_readfirstlane(rrow < 0 ? 0 : PT_MIR ? (rrow < RP ? rrow : R - 1 - rrow) : rrow % RP);
     const bool shalf = srow >= RP, rhalf = rrow >= RP;   // the half is r >= RP in both pairings
+    // the receiver's row pair among the boundary pairs 0, 1 (rlo) or the interior ones (rhi): wave-uniform
+    const int rlo = __builtin_amdgcn_readfirstlane(rrow >= 0 && rpair < 2 ? 1 : 0);
+    const int rhi = __builtin_amdgcn_readfirstlane(rrow >= 0 && rpair >= 2 ? 1 : 0);
 #define DLOAD(KK)                                                                                   \
     ({                                                                                              \
         const int ri_ = (KK) >= 1 ? rec_index((KK) - 1, g.st) : -1;                                 \
@@ -2273,6 +2263,10 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
         const int ke = a.nt - e * T;                      // first step k of this epoch
         const bool last = e + 1 == nep;
         const __amdgpu_buffer_rsrc_t HRe = HIST_RSRC(ke);
+        // every step of the epoch prefetches a history slot that exists (k >= 2): one scalar test per
+        // epoch instead of per step (the barrier-free step, ADJR_STEP_NB)
+        int ldall = grad && ke >= T + 1;
+        LAUNDER(ldall);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int j = e * T + t;
@@ -2351,8 +2345,6 @@ __global__ __launch_bounds__(64 * NW) void k_adj_pr(AdjPtArgs a)
 #undef FWD_PAIRS_NB
 #undef MIR_VERT
 #undef ADJR_GRAD
-#undef ADJR_GRAD_PRE
-#undef ADJR_GRAD_POST
 #undef ADJR_LOAD
 #undef ADJ_STEP
 #undef ADJ_GRAD
