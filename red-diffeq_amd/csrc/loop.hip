@@ -136,19 +136,31 @@ __global__ __launch_bounds__(256) void k_metrics_tile(MetArgs a)
     }
 }
 
-__global__ void k_metrics_final(MetArgs a)
+// one workgroup per model: thread t sums tiles t, t + 256, ... in tile order, then a fixed tree
+// (deterministic; one thread per model summed the configs[4] model's tiles serially: 184 us)
+__global__ __launch_bounds__(256) void k_metrics_final(MetArgs a)
 {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.B) return;
+    __shared__ double sh[3][256];
+    const int b = blockIdx.x, tid = threadIdx.x;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int t = 0; t < a.ntiles; ++t) {
+    for (int t = tid; t < a.ntiles; t += 256) {
         const double *o = a.part + ((size_t)b * a.ntiles + t) * NPART;
         s0 += o[0]; s1 += o[1]; s2 += o[2];
     }
-    const double n = (double)a.H * a.W;
-    a.out[b] = (float)(s0 / n);
-    a.out[a.B + b] = (float)std::sqrt(s1 / n);
-    a.out[2 * a.B + b] = (float)(s2 / n);
+    sh[0][tid] = s0; sh[1][tid] = s1; sh[2][tid] = s2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            sh[0][tid] += sh[0][tid + w]; sh[1][tid] += sh[1][tid + w]; sh[2][tid] += sh[2][tid + w];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const double n = (double)a.H * a.W;
+        a.out[b] = (float)(sh[0][0] / n);
+        a.out[a.B + b] = (float)std::sqrt(sh[1][0] / n);
+        a.out[2 * a.B + b] = (float)(sh[2][0] / n);
+    }
 }
 
 }  // namespace
@@ -190,7 +202,7 @@ int rdq_metrics(int32_t B, int32_t H, int32_t W, const float *pred, const int64_
     for (int k = 0; k < WIN; ++k) sum += g[k];
     for (int k = 0; k < WIN; ++k) a.win[k] = g[k] / sum;
     hipLaunchKernelGGL(k_metrics_tile, dim3(a.ntiles, B), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(k_metrics_final, dim3((B + 63) / 64), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(k_metrics_final, dim3(B), dim3(256), 0, stream, a);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }

@@ -1450,8 +1450,8 @@ __global__ __launch_bounds__(256) void k_linear_silu_multi_b(int in, int B, cons
 // shfl_down tree over k (pairs 32 apart first, then 16, ..., 1) -- evaluated with one SAMPLE per
 // lane instead of one sample per wave: the tree is evaluated depth-first in registers
 // (wdot_tree), so no cross-lane instruction is needed.  Each sample's result is bit for bit
-// k_linear_silu_multi's.  Workgroup: 64 samples (SiLU'd into LDS, rows padded to 257 floats:
-// conflict-free column reads) x 4 waves x WDR rows; the rows' weights in LDS as [row][k][u]
+// k_linear_silu_multi's.  Workgroup: 64 samples (SiLU'd into LDS as [k][u], rows of 260 floats: a
+// leaf's four x values are one conflict-free ds_read_b128, round 6) x 4 waves x WDR rows; the rows' weights in LDS as [row][k][u]
 // (one broadcast read per leaf).
 constexpr int WDR = 8;
 // wave_dot's shfl_down tree as a recursion: F(o, l) = F(2o, l) + F(2o, l + o), F(64, l) = lane l's
@@ -1467,9 +1467,10 @@ __device__ __forceinline__ float wdot_tree(const float *__restrict__ xrow, const
         int ox = LX;
         asm volatile("" : "+v"(ox) : "v"(dep));
         const f32x4 w4 = *reinterpret_cast<const f32x4 *>(wrow + 4 * ox);    // [k][u]: one broadcast read
+        const f32x4 x4 = *reinterpret_cast<const f32x4 *>(xrow + 4 * ox);    // [k][u]: one read per lane
         float sacc = 0.0f;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sacc = fmaf(w4[u], xrow[ox + 64 * u], sacc);
+        for (int u = 0; u < 4; ++u) sacc = fmaf(w4[u], x4[u], sacc);
         return sacc;
     } else {
         const float a = wdot_tree<2 * O, LX>(xrow, wrow, dep);
@@ -1481,7 +1482,8 @@ __device__ __forceinline__ float wdot_tree(const float *__restrict__ xrow, const
 
 __global__ __launch_bounds__(256) void k_wdot_silu_b(int B, const float *__restrict__ x, LinMulti L)
 {
-    __shared__ float xs[64][257];
+    __shared__ __attribute__((aligned(16))) float xs[64][260];   // [sample][k][u] (x index k + 64u); 1040-B rows:
+                                                                   // a lane's ds_read_b128 per leaf, conflict-free
     __shared__ __attribute__((aligned(16))) float wt[4][WDR][64][4];   // [wave][row][k][u]
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b0 = blockIdx.y * 64, nb = min(64, B - b0), gend = L.start[L.n];
@@ -1517,7 +1519,7 @@ __global__ __launch_bounds__(256) void k_wdot_silu_b(int B, const float *__restr
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int idx = (it + q) * 256 + tid;
-            xs[idx >> 8][idx & 255] = v[q] / (1.0f + expf(-v[q]));
+            xs[idx >> 8][(idx & 63) * 4 + ((idx >> 6) & 3)] = v[q] / (1.0f + expf(-v[q]));
         }
     }
     __syncthreads();
