@@ -1289,6 +1289,7 @@ __global__ __launch_bounds__(256) void k_time_mlp(TmArgs m)
 // workgroup, so the hidden layer's weights are read once per sample block instead of once per
 // (row block, sample); per sample the arithmetic is time_mlp_rows' (bit for bit k_time_mlp's).
 constexpr int TMB = 8;
+constexpr int TMB_RW = 8;                             // k_time_mlp_b: second-layer rows per wave
 __global__ __launch_bounds__(256) void k_time_mlp_b(TmArgs m, int B)
 {
     extern __shared__ float tmb_sm[];                 // [TMB][dim + hid]
@@ -1324,11 +1325,15 @@ __global__ __launch_bounds__(256) void k_time_mlp_b(TmArgs m, int B)
         }
     }
     __syncthreads();
-    const int o = blockIdx.x * TM_ROWS + wv;
-    if (o >= out) return;
-    for (int bb = 0; bb < nb; ++bb) {
-        const float s = wave_dot(m.w2 + (size_t)o * hid, tmb_sm + bb * ld + dim, hid, lane, false);
-        if (lane == 0) m.y[(size_t)(b0 + bb) * out + o] = s + m.b2[o];
+    // second layer: TMB_RW rows per wave (the first layer above is formed once per block for them all,
+    // not once per 4 rows: 311 -> a few us at 344 samples); per sample wave_dot's arithmetic
+    for (int r = 0; r < TMB_RW; ++r) {
+        const int o = (blockIdx.x * 4 + wv) * TMB_RW + r;
+        if (o >= out) return;                         // wave-uniform
+        for (int bb = 0; bb < nb; ++bb) {
+            const float s = wave_dot(m.w2 + (size_t)o * hid, tmb_sm + bb * ld + dim, hid, lane, false);
+            if (lane == 0) m.y[(size_t)(b0 + bb) * out + o] = s + m.b2[o];
+        }
     }
 }
 
@@ -2936,6 +2941,52 @@ __global__ __launch_bounds__(256) void k_stem7(int H, int W, const float *__rest
     for (int c = 0; c < ST_C; ++c) yb[(size_t)c * HW] = acc[c];
 }
 
+// k_stem7 with two horizontally adjacent pixels per thread (even W): every weight read and every packed
+// FMA (v_pk_fma_f32: IEEE fma per half) serves both pixels, each pixel's taps in k_stem7's order, so the
+// outputs are k_stem7's bit for bit with half its LDS reads and VALU instructions per pixel.
+constexpr int ST_ROWS2 = 16;                          // input rows a 512-pixel tile reads (W >= 64)
+__global__ __launch_bounds__(256) void k_stem7x2(int H, int W, const float *__restrict__ x, const float *__restrict__ w,
+                                                 const float *__restrict__ bias, float *__restrict__ y)
+{
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    __shared__ float xs[ST_ROWS2][C3_WMAX + ST_K];
+    __shared__ __attribute__((aligned(16))) float ws_[ST_K * ST_K][ST_C];   // [tap][channel]: broadcast reads
+    const int b = blockIdx.y, HW = H * W, p0 = blockIdx.x * 512, p = p0 + 2 * (int)threadIdx.x;
+    for (int i = threadIdx.x; i < ST_K * ST_K * ST_C; i += 256) {
+        const int c = i / (ST_K * ST_K), t = i - c * ST_K * ST_K;
+        ws_[t][c] = w[i];
+    }
+    const int r0 = p0 / W - ST_K / 2;
+    const float *xb = x + (size_t)b * HW;
+    for (int i = threadIdx.x; i < ST_ROWS2 * (W + ST_K - 1); i += 256) {
+        const int rr = i / (W + ST_K - 1), cc = i - rr * (W + ST_K - 1);
+        const int ih = r0 + rr, iw = cc - ST_K / 2;
+        xs[rr][cc] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xb[ih * W + iw] : 0.0f;
+    }
+    __syncthreads();
+    if (p >= HW) return;                              // HW even: p + 1 < HW too, in the same row
+    const int oh = p / W, ow = p - oh * W, lr = oh - ST_K / 2 - r0;
+    f2 acc[ST_C];
+#pragma unroll
+    for (int c = 0; c < ST_C; ++c) { const float bv = bias ? bias[c] : 0.0f; acc[c] = f2{bv, bv}; }
+#pragma unroll
+    for (int ky = 0; ky < ST_K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < ST_K; ++kx) {
+            const f2 v = {xs[lr + ky][ow + kx], xs[lr + ky][ow + kx + 1]};
+            const f32x4 *wt = reinterpret_cast<const f32x4 *>(&ws_[ky * ST_K + kx][0]);
+#pragma unroll
+            for (int c4 = 0; c4 < ST_C / 4; ++c4) {
+                const f32x4 w4 = wt[c4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[4 * c4 + q] = __builtin_elementwise_fma(v, f2{w4[q], w4[q]}, acc[4 * c4 + q]);
+            }
+        }
+    float *yb = y + (size_t)b * ST_C * HW + p;
+#pragma unroll
+    for (int c = 0; c < ST_C; ++c) *reinterpret_cast<f2 *>(yb + (size_t)c * HW) = acc[c];
+}
+
 // ------------------------------------------------- linear attention, bf16, whole block fused
 // LinearAttention.forward(x) + x (reference diffusion.py:182-195 and the residual at 286 / 297) for the
 // batched bf16 U-Net (configs[4]: hundreds of 72 x 72 tiles).  The unfused form writes and re-reads
@@ -3877,7 +3928,10 @@ int rdq_conv2d_stem(const rdq_conv_desc *d, const float *x, const float *w, cons
         d->pad != ST_K / 2 || d->cout != ST_C || d->in_mode != RDQ_IN_PLAIN || d->W < 64 || d->W > C3_WMAX ||
         (int64_t)d->B * ST_C * d->H * d->W >= ((int64_t)1 << 31))
         return RDQ_E_INVALID;
-    hipLaunchKernelGGL(k_stem7, dim3((d->H * d->W + 255) / 256, d->B), dim3(256), 0, st, d->H, d->W, x, w, bias, y);
+    if (d->W % 2 == 0)
+        hipLaunchKernelGGL(k_stem7x2, dim3((d->H * d->W + 511) / 512, d->B), dim3(256), 0, st, d->H, d->W, x, w, bias, y);
+    else
+        hipLaunchKernelGGL(k_stem7, dim3((d->H * d->W + 255) / 256, d->B), dim3(256), 0, st, d->H, d->W, x, w, bias, y);
     RDQ_CHECK(hipGetLastError());
     return 0;
 }
@@ -4128,7 +4182,7 @@ int rdq_time_mlp(int32_t B, int32_t dim, float theta, const int64_t *t, const fl
     const float emb = (float)(std::log((double)theta) / (double)(half - 1));   // python float math
     const TmArgs m{dim, hid, out, -emb, t, w1, b1, w2, b2, y};
     if (B > 2 * TMB)
-        hipLaunchKernelGGL(k_time_mlp_b, dim3((out + TM_ROWS - 1) / TM_ROWS, (B + TMB - 1) / TMB), dim3(256),
+        hipLaunchKernelGGL(k_time_mlp_b, dim3((out + 4 * TMB_RW - 1) / (4 * TMB_RW), (B + TMB - 1) / TMB), dim3(256),
                            TMB * (dim + hid) * sizeof(float), st, m, B);
     else
         hipLaunchKernelGGL(k_time_mlp, dim3((out + TM_ROWS - 1) / TM_ROWS, B), dim3(256), (dim + hid) * sizeof(float),
