@@ -992,6 +992,77 @@ __global__ __launch_bounds__(256) void k_gn_apply8(int C, int HW, int G, const T
     }
 }
 
+// k_gn_apply8 on the bf16 conv output with two adjacent pixels per thread (even HW): one 4-byte load per
+// channel and 32 contiguous output bytes per thread instead of 2-byte loads and one 16-byte store;
+// per element the same arithmetic, so the octets are k_gn_apply8's bit for bit.
+__device__ __forceinline__ float2 ldx2(const __bf16 *p)
+{
+    const unsigned u = *reinterpret_cast<const unsigned *>(p);
+    return float2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+__global__ __launch_bounds__(256) void k_gn_apply8x2(int C, int HW, int G, const __bf16 *__restrict__ x,
+                                                     const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                     const float *__restrict__ ss, const double *__restrict__ gnp,
+                                                     float eps, __bf16 *__restrict__ y, int bm)
+{
+    const int bg = blockIdx.y, b = bg / G, g = bg - b * G, cpg = C / G;
+    const int p = (blockIdx.x * 256 + (int)threadIdx.x) * 2;   // HW even: p + 1 < HW whenever p < HW
+    __shared__ float st2[2];
+    if (threadIdx.x < 64) {                     // (sample, group) statistics: k_gn_apply_t's reduction
+        const int lane = threadIdx.x;
+        const int mlo = (int)(((int64_t)b * HW) / bm), mhi = (int)(((int64_t)(b + 1) * HW - 1) / bm);
+        double s = 0.0, q = 0.0;
+        for (int mt = mlo + lane; mt <= mhi; mt += 64) {
+            const int slot = (int)(((int64_t)mt * bm) / HW) == b ? 0 : 1;
+            const double *pp = gnp + (((size_t)mt * G + g) * 2 + slot) * 2;
+            s += pp[0];
+            q += pp[1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            q += __shfl_xor(q, o, 64);
+        }
+        if (lane == 0) {
+            const double n = (double)cpg * HW, mean = s / n;
+            double var = q / n - mean * mean;
+            var = var < 0.0 ? 0.0 : var;
+            st2[0] = (float)mean;
+            st2[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+    }
+    const int pc = min(p, HW - 2);
+    const __bf16 *xb = x + ((size_t)b * C + g * cpg) * HW + pc;
+    float2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ldx2(xb + (size_t)j * HW);
+    __syncthreads();
+    const float mean = st2[0], rstd = st2[1];
+    const bool sso = ss != nullptr;
+    for (int o = 0; o < cpg / 8; ++o) {
+        float2 nx[8];
+        if (o + 1 < cpg / 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nx[j] = ldx2(xb + (size_t)(8 * (o + 1) + j) * HW);
+        }
+        bf16x8 h0, h1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = g * cpg + 8 * o + j;
+            const float sc1 = sso ? ss[(size_t)b * 2 * C + c] + 1.0f : 0.0f, sh = sso ? ss[(size_t)b * 2 * C + C + c] : 0.0f;
+            h0[j] = (__bf16)gn_silu1(v[j].x, mean, rstd, gamma[c], beta[c], sso, sc1, sh);
+            h1[j] = (__bf16)gn_silu1(v[j].y, mean, rstd, gamma[c], beta[c], sso, sc1, sh);
+        }
+        if (p < HW) {
+            bf16x8 *yo = reinterpret_cast<bf16x8 *>(y + (((size_t)b * (C >> 3) + (g * cpg >> 3) + o) * HW + p) * 8);
+            yo[0] = h0;
+            yo[1] = h1;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = nx[j];
+    }
+}
+
 // The U-Net's last two steps in one pass (diffusion.py:299-301): final_res_block's block2
 // normalise pass (k_gn_apply_t's arithmetic: statistics from the conv's per-tile partials, GN ->
 // scale/shift -> SiLU, + the res_conv shortcut) feeding final_conv, a 1x1 conv to NF <= 4 channels,
@@ -4040,7 +4111,10 @@ int rdq_conv2d_bf16_gn_silu8(const rdq_conv_desc *d, const float *x, const float
         !bf16_gn_conv(d, x, x2, wp, bias, G, ws, ws_bytes, c, st))
         return RDQ_E_INVALID;
     const int HW = c.HW;
-    if (c.yb)
+    if (c.yb && HW % 2 == 0)
+        hipLaunchKernelGGL(k_gn_apply8x2, dim3((HW + 511) / 512, d->B * G), dim3(256), 0, st,
+                           d->cout, HW, G, c.yb, gamma, beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
+    else if (c.yb)
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gn_apply8<__bf16>), dim3((HW + 255) / 256, d->B * G), dim3(256), 0, st, d->cout,
                            HW, G, c.yb, gamma, beta, scale_shift, c.gnp, eps, static_cast<__bf16 *>(y8), C3_BM);
     else
