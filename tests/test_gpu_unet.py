@@ -580,10 +580,11 @@ def test_bf16_block_pair_bitexact(cuda, cin1, cin2, cout, H, B, ss, post):
     assert torch.equal(got, ref), (got - ref).abs().max().item()
 
 
-@pytest.mark.parametrize("B,H,W", [(3, 72, 72), (2, 64, 64), (1, 40, 70)])
+@pytest.mark.parametrize("B,H,W", [(3, 72, 72), (2, 64, 64), (1, 40, 70), (2, 33, 67)])
 def test_stem_direct_conv(cuda, B, H, W):
     """Unet.init_conv (Conv2d(1, 64, 7, padding=3)) under the bf16 precision: the direct fp32 conv
-    (rdq_conv2d_stem: a thread per pixel, all 64 channels) vs the torch fp32 conv."""
+    (rdq_conv2d_stem: two adjacent pixels per thread for even W, a thread per pixel for odd W, all 64
+    channels) vs the torch fp32 conv."""
     from red_diffeq.models import unet_ops as ops
     torch.manual_seed(23)
     conv = nn.Conv2d(1, 64, 7, padding=3).to(cuda)
